@@ -1,0 +1,84 @@
+"""Build the gfx950 HIP kernel library in-tree.
+
+    python csrc/build.py [--force] [--jobs N]
+
+Compiles every csrc/*.hip with `hipcc --offload-arch=gfx950` into object
+files under build/, links them into
+`distributed_kfac_pytorch_amd/_native/libkfac_hip.so` (plain C ABI, loaded
+through ctypes by ops/_lib.py; no torch headers, no hipify).  Rebuilds only
+when a source or header is newer than the library.
+"""
+import argparse
+import concurrent.futures
+import glob
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, 'csrc')
+OUT_DIR = os.path.join(ROOT, 'distributed_kfac_pytorch_amd', '_native')
+LIB = os.path.join(OUT_DIR, 'libkfac_hip.so')
+BUILD = os.path.join(ROOT, 'build', 'hip')
+ARCH = os.environ.get('KFAC_HIP_ARCH', 'gfx950')
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+FLAGS = ['-O3', '-std=c++17', '-fPIC', '--offload-arch=' + ARCH, '-munsafe-fp-atomics',
+         '-Wno-unused-result']
+
+
+def sources():
+    return sorted(glob.glob(os.path.join(CSRC, '*.hip')))
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _compile(src):
+    obj = os.path.join(BUILD, os.path.basename(src) + '.o')
+    headers = glob.glob(os.path.join(CSRC, '*.h'))
+    if _stale(obj, [src] + headers):
+        cmd = [HIPCC] + FLAGS + ['-I', CSRC, '-c', src, '-o', obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError('hipcc failed for {}:\n{}\n{}'.format(src, ' '.join(cmd), r.stderr))
+    return obj
+
+
+def build(force=False, jobs=None, verbose=True):
+    os.makedirs(BUILD, exist_ok=True)
+    os.makedirs(OUT_DIR, exist_ok=True)
+    srcs = sources()
+    deps = srcs + glob.glob(os.path.join(CSRC, '*.h'))
+    if not force and not _stale(LIB, deps):
+        return LIB
+    if force:
+        for o in glob.glob(os.path.join(BUILD, '*.o')):
+            os.remove(o)
+    jobs = jobs or min(8, len(srcs))
+    with concurrent.futures.ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(_compile, srcs))
+    tmp = LIB + '.tmp'
+    cmd = [HIPCC, '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', tmp] + objs
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError('link failed:\n{}\n{}'.format(' '.join(cmd), r.stderr))
+    os.replace(tmp, LIB)
+    if verbose:
+        print('built', LIB, 'from', len(objs), 'sources for', ARCH)
+    return LIB
+
+
+if __name__ == '__main__':
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--force', action='store_true')
+    ap.add_argument('--jobs', type=int, default=None)
+    a = ap.parse_args()
+    try:
+        build(force=a.force, jobs=a.jobs)
+    except RuntimeError as e:
+        print(e, file=sys.stderr)
+        sys.exit(1)

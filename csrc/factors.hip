@@ -1,0 +1,426 @@
+// Kronecker-factor kernels for gfx950.
+//
+//   syrk_patch   K1+K2+K3/K4: C += scale * P^T P where P is the *implicit*
+//                im2col patch matrix of a Conv2d input (rows (b,oh,ow),
+//                columns (c,kh,kw) [+ a ones column for the bias]).  Linear
+//                inputs and conv grad_outputs are the degenerate 1x1 case.
+//                The patch matrix is never materialised: each workgroup
+//                gathers a [BK rows x 128 cols] slab straight from the NCHW /
+//                NHWC activation into LDS (k-contiguous) and feeds MFMA
+//                (32x32x16 bf16/f16, or 32x32x2 f32 for fp32 data).  Only
+//                upper-triangular 128x128 output tiles are computed (SYRK);
+//                the row dimension (up to 4e5 rows) is split over
+//                blockIdx.y and combined with f32 atomics into a workspace.
+//   factor_ema   K5: state = alpha*state + (1-alpha)*sym(ws), mirrored from
+//                the upper triangle, in the factor's storage dtype.
+//   triu pack/unpack K12: symmetric factors <-> packed upper triangles for
+//                the bucketed RCCL all-reduce; unpack folds the 1/world
+//                averaging in.
+//
+// Reference semantics: kfac/layers/conv.py:24-70, kfac/layers/linear.py:12-24,
+// kfac/layers/utils.py:4-43,164-178 (A_conv = P^T P / (B * S^3), G_conv =
+// g^T g / (B * S^3), linear: a^T a / rows).
+#include "common.h"
+#include <type_traits>
+
+namespace {
+
+struct PatchArgs {
+  const void* x;          // activation base pointer
+  long long sb, sc, sh, sw;  // element strides of x for (b, c, h, w)
+  int B, C, H, W;
+  int kh, kw, sth, stw, ph, pw, dh, dw;
+  int OH, OW;
+  int kcols;              // C*kh*kw
+  int ncols;              // kcols + has_bias
+  long long M;            // B*OH*OW rows
+  long long rows_per_split;
+  int ntiles;             // ceil(ncols / 128)
+  float scale;
+  float* ws;              // f32 workspace, row-major, leading dim ldw
+  int ldw;
+};
+
+constexpr int BT = 128;   // output tile
+constexpr int BK = 32;    // rows per k-step
+
+template <int DT> struct SyrkCfg;
+template <> struct SyrkCfg<KDT_F32> { static constexpr int LDK = BK + 1; };   // 33 floats: conflict-free b32 reads
+template <> struct SyrkCfg<KDT_BF16> { static constexpr int LDK = BK + 8; };  // 80 B rows: conflict-free b128 reads
+template <> struct SyrkCfg<KDT_F16> { static constexpr int LDK = BK + 8; };
+
+// Per-thread column descriptor for the gather: element offset of the column
+// inside one patch, and its (kh, kw) displacement packed as (di << 16) | dj.
+// Special values of `disp`: -1 = padding column (zero), -2 = bias column (one).
+struct ColInfo { int off; int disp; };
+
+__device__ __forceinline__ ColInfo make_col(const PatchArgs& p, int gcol) {
+  ColInfo ci;
+  if (gcol < p.kcols) {
+    int kk = p.kh * p.kw;
+    int c = gcol / kk;
+    int r = gcol - c * kk;
+    int i = r / p.kw;
+    int j = r - i * p.kw;
+    int di = i * p.dh, dj = j * p.dw;
+    ci.off = (int)(c * p.sc + (long long)di * p.sh + (long long)dj * p.sw);
+    ci.disp = (di << 16) | dj;
+  } else if (gcol < p.ncols) {
+    ci.off = 0; ci.disp = -2;
+  } else {
+    ci.off = 0; ci.disp = -1;
+  }
+  return ci;
+}
+
+template <int DT>
+__device__ __forceinline__ typename DTypeTraits<DT>::raw_t gather(
+    const PatchArgs& p, const typename DTypeTraits<DT>::raw_t* x, long long base,
+    int hb, int wb, bool row_ok, ColInfo ci) {
+  typedef typename DTypeTraits<DT>::raw_t raw_t;
+  if (!row_ok || ci.disp == -1) return (raw_t)0;
+  if (ci.disp == -2) return DTypeTraits<DT>::from_f32(1.0f);
+  int h = hb + (ci.disp >> 16);
+  int w = wb + (ci.disp & 0xffff);
+  if ((unsigned)h >= (unsigned)p.H || (unsigned)w >= (unsigned)p.W) return (raw_t)0;
+  return x[base + ci.off];
+}
+
+__device__ __forceinline__ void decompose_row(const PatchArgs& p, long long row,
+                                              long long& base, int& hb, int& wb) {
+  long long ohw = (long long)p.OH * p.OW;
+  long long b = row / ohw;
+  int rem = (int)(row - b * ohw);
+  int oh = rem / p.OW;
+  int ow = rem - oh * p.OW;
+  hb = oh * p.sth - p.ph;
+  wb = ow * p.stw - p.pw;
+  base = b * p.sb + (long long)hb * p.sh + (long long)wb * p.sw;
+}
+
+// LANE_COLS = true when channels are the unit-stride dim (NHWC / Linear):
+// consecutive lanes then gather consecutive columns (coalesced); otherwise
+// (NCHW) consecutive lanes gather consecutive rows (= consecutive ow).
+template <int DT, bool LANE_COLS>
+__global__ __launch_bounds__(256) void syrk_patch_kernel(PatchArgs p) {
+  typedef typename DTypeTraits<DT>::raw_t raw_t;
+  constexpr int LDK = SyrkCfg<DT>::LDK;
+  __shared__ __attribute__((aligned(16))) raw_t smem[2 * BT * LDK];
+  raw_t* sA = smem;
+  raw_t* sB = smem + BT * LDK;
+
+  // upper-triangular tile decode: blockIdx.x -> (ti <= tj)
+  int t = blockIdx.x, ti = 0, rem = p.ntiles;
+  while (t >= rem) { t -= rem; ++ti; --rem; }
+  const int tj = ti + t;
+  const bool diag = (ti == tj);
+
+  const long long r_begin = (long long)blockIdx.y * p.rows_per_split;
+  long long r_end = r_begin + p.rows_per_split;
+  if (r_end > p.M) r_end = p.M;
+  if (r_begin >= r_end) return;
+  const int nk = (int)((r_end - r_begin + BK - 1) / BK);
+
+  const raw_t* x = (const raw_t*)p.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+
+  // ---- loader geometry ----
+  // LANE_COLS : col = tid & 127, rows rg*16 .. rg*16+15, rg = tid >> 7
+  // !LANE_COLS: row = tid & 31,  cols cg*16 .. cg*16+15, cg = tid >> 5
+  constexpr int NPER = 16;
+  ColInfo ca[LANE_COLS ? 1 : NPER], cb[LANE_COLS ? 1 : NPER];
+  if (LANE_COLS) {
+    int col = tid & 127;
+    ca[0] = make_col(p, ti * BT + col);
+    cb[0] = make_col(p, tj * BT + col);
+  } else {
+    int cg = tid >> 5;
+#pragma unroll
+    for (int q = 0; q < NPER; ++q) {
+      ca[q] = make_col(p, ti * BT + cg * 16 + q);
+      cb[q] = make_col(p, tj * BT + cg * 16 + q);
+    }
+  }
+  raw_t va[NPER], vb[NPER];
+
+  auto load_step = [&](int k) {
+    long long r0 = r_begin + (long long)k * BK;
+    if (LANE_COLS) {
+      int rg = tid >> 7;
+      long long row = r0 + rg * 16;
+      // decompose the first row once, then walk the next 15 incrementally
+      long long rs = row < r_end ? row : r_begin;
+      long long ohw = (long long)p.OH * p.OW;
+      long long b = rs / ohw;
+      int rr = (int)(rs - b * ohw);
+      int oh = rr / p.OW, ow = rr - oh * p.OW;
+#pragma unroll
+      for (int q = 0; q < NPER; ++q) {
+        bool ok = (row + q) < r_end;
+        int hb = oh * p.sth - p.ph;
+        int wb = ow * p.stw - p.pw;
+        long long base = b * p.sb + (long long)hb * p.sh + (long long)wb * p.sw;
+        va[q] = gather<DT>(p, x, base, hb, wb, ok, ca[0]);
+        if (!diag) vb[q] = gather<DT>(p, x, base, hb, wb, ok, cb[0]);
+        if (++ow == p.OW) { ow = 0; if (++oh == p.OH) { oh = 0; ++b; } }
+      }
+    } else {
+      long long row = r0 + (tid & 31);
+      bool ok = row < r_end;
+      long long base = 0; int hb = 0, wb = 0;
+      if (ok) decompose_row(p, row, base, hb, wb);
+#pragma unroll
+      for (int q = 0; q < NPER; ++q) {
+        va[q] = gather<DT>(p, x, base, hb, wb, ok, ca[q]);
+        if (!diag) vb[q] = gather<DT>(p, x, base, hb, wb, ok, cb[q]);
+      }
+    }
+  };
+
+  auto store_step = [&]() {
+    if (LANE_COLS) {
+      int col = tid & 127, rg = tid >> 7;
+      raw_t* da = sA + col * LDK + rg * 16;
+      raw_t* db = sB + col * LDK + rg * 16;
+#pragma unroll
+      for (int q = 0; q < NPER; ++q) { da[q] = va[q]; if (!diag) db[q] = vb[q]; }
+    } else {
+      int r = tid & 31, cg = tid >> 5;
+#pragma unroll
+      for (int q = 0; q < NPER; ++q) {
+        sA[(cg * 16 + q) * LDK + r] = va[q];
+        if (!diag) sB[(cg * 16 + q) * LDK + r] = vb[q];
+      }
+    }
+  };
+
+  // ---- MFMA geometry: 4 waves as 2x2, each a 64x64 sub-tile = 2x2 MFMA 32x32 tiles
+  const int wr = wave >> 1, wc = wave & 1;
+  const int lr = lane & 31, lh = lane >> 5;
+  f32x16_t acc[2][2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
+
+  const raw_t* sBr = diag ? sA : sB;
+
+  load_step(0);
+  for (int k = 0; k < nk; ++k) {
+    store_step();
+    __syncthreads();
+    if (k + 1 < nk) load_step(k + 1);   // global gathers in flight under the MFMAs
+    if constexpr (DT == KDT_F32) {
+#pragma unroll
+      for (int ks = 0; ks < BK / 2; ++ks) {
+        float a[2], b[2];
+#pragma unroll
+        for (int m = 0; m < 2; ++m) a[m] = sA[(wr * 64 + m * 32 + lr) * LDK + ks * 2 + lh];
+#pragma unroll
+        for (int n = 0; n < 2; ++n) b[n] = sBr[(wc * 64 + n * 32 + lr) * LDK + ks * 2 + lh];
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m], b[n], acc[m][n], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        typedef typename std::conditional<DT == KDT_BF16, bf16x8_t, f16x8_t>::type frag_t;
+        frag_t a[2], b[2];
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+          a[m] = *(const frag_t*)(sA + (wr * 64 + m * 32 + lr) * LDK + ks * 16 + lh * 8);
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+          b[n] = *(const frag_t*)(sBr + (wc * 64 + n * 32 + lr) * LDK + ks * 16 + lh * 8);
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int n = 0; n < 2; ++n) {
+            if constexpr (DT == KDT_BF16)
+              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m], b[n], acc[m][n], 0, 0, 0);
+            else
+              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[m], b[n], acc[m][n], 0, 0, 0);
+          }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: scaled f32 atomics into the upper triangle of ws
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int row = ti * BT + wr * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        int col = tj * BT + wc * 64 + n * 32 + lr;
+        if (row < p.ncols && col < p.ncols && (!diag || row <= col))
+          atomicAdd(p.ws + (long long)row * p.ldw + col, p.scale * acc[m][n][r]);
+      }
+}
+
+// state = a2 * (a1 * state + ws_sym)   (mode 0: EMA, a1 = alpha/(1-alpha), a2 = 1-alpha)
+// state = ws_sym                       (mode 1: assign)
+// The workspace holds only the upper triangle; (i, j) with i > j reads ws[j][i].
+template <int SDT>
+__global__ __launch_bounds__(256) void factor_ema_kernel(
+    typename DTypeTraits<SDT>::raw_t* __restrict__ state, const float* __restrict__ ws,
+    int n, int ldw, float a1, float a2, int mode) {
+  typedef DTypeTraits<SDT> Tr;
+  __shared__ float tile[32][33];
+  const int bi = blockIdx.y, bj = blockIdx.x;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
+  if (bi > bj) {
+    for (int r = ty; r < 32; r += 8) {
+      int i = bj * 32 + r, j = bi * 32 + tx;
+      tile[r][tx] = (i < n && j < n) ? ws[(long long)i * ldw + j] : 0.f;
+    }
+    __syncthreads();
+  }
+  for (int r = ty; r < 32; r += 8) {
+    int i = bi * 32 + r, j = bj * 32 + tx;
+    if (i >= n || j >= n) continue;
+    float w;
+    if (bi > bj) w = tile[tx][r];
+    else w = (i <= j) ? ws[(long long)i * ldw + j] : ws[(long long)j * ldw + i];
+    long long o = (long long)i * n + j;
+    float s = (mode == 0) ? (Tr::to_f32(state[o]) * a1 + w) * a2 : w;
+    state[o] = Tr::from_f32(s);
+  }
+}
+
+// Pack the upper triangle (row-major, diagonal included) of a symmetric n x n
+// matrix into `out` (dtype of the matrix).
+template <int DT>
+__global__ void triu_pack_kernel(const typename DTypeTraits<DT>::raw_t* __restrict__ a,
+                                 typename DTypeTraits<DT>::raw_t* __restrict__ out, int n) {
+  const int i = blockIdx.y;
+  const long long row_off = (long long)i * n - (long long)i * (i - 1) / 2;  // packed start of row i
+  for (int j = i + blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x)
+    out[row_off + (j - i)] = a[(long long)i * n + j];
+}
+
+// Unpack + mirror + scale (scale = 1/world folds the AVERAGE in).
+template <int DT>
+__global__ __launch_bounds__(256) void triu_unpack_kernel(
+    const typename DTypeTraits<DT>::raw_t* __restrict__ packed,
+    typename DTypeTraits<DT>::raw_t* __restrict__ a, int n, float scale) {
+  typedef DTypeTraits<DT> Tr;
+  __shared__ float tile[32][33];
+  const int bi = blockIdx.y, bj = blockIdx.x;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  auto pidx = [n](long long i, long long j) { return i * n - i * (i - 1) / 2 + (j - i); };
+  if (bi > bj) {
+    for (int r = ty; r < 32; r += 8) {
+      int i = bj * 32 + r, j = bi * 32 + tx;
+      tile[r][tx] = (i < n && j < n) ? Tr::to_f32(packed[pidx(i, j)]) : 0.f;
+    }
+    __syncthreads();
+  }
+  for (int r = ty; r < 32; r += 8) {
+    int i = bi * 32 + r, j = bj * 32 + tx;
+    if (i >= n || j >= n) continue;
+    float v;
+    if (bi > bj) v = tile[tx][r];
+    else v = Tr::to_f32(packed[(i <= j) ? pidx(i, j) : pidx(j, i)]);
+    a[(long long)i * n + j] = Tr::from_f32(v * scale);
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ C ABI
+KFAC_API int kfac_syrk_patch(int dtype, const void* x, long long sb, long long sc, long long sh,
+                             long long sw, int B, int C, int H, int W, int kh, int kw, int sth,
+                             int stw, int ph, int pw, int dh, int dw, int has_bias, float scale,
+                             float* ws, int ldw, int max_blocks, hipStream_t stream) {
+  PatchArgs p;
+  p.x = x; p.sb = sb; p.sc = sc; p.sh = sh; p.sw = sw;
+  p.B = B; p.C = C; p.H = H; p.W = W;
+  p.kh = kh; p.kw = kw; p.sth = sth; p.stw = stw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
+  p.OH = (H + 2 * ph - dh * (kh - 1) - 1) / sth + 1;
+  p.OW = (W + 2 * pw - dw * (kw - 1) - 1) / stw + 1;
+  p.kcols = C * kh * kw;
+  p.ncols = p.kcols + (has_bias ? 1 : 0);
+  p.M = (long long)B * p.OH * p.OW;
+  p.ntiles = (p.ncols + BT - 1) / BT;
+  p.scale = scale; p.ws = ws; p.ldw = ldw;
+  if (p.M <= 0 || p.OH <= 0 || p.OW <= 0) return 0;
+  const int tiles = p.ntiles * (p.ntiles + 1) / 2;
+  // split the row dimension so the grid covers the chip several times over
+  if (max_blocks <= 0) max_blocks = 2048;
+  long long ksteps = (p.M + BK - 1) / BK;
+  long long splits = (max_blocks + tiles - 1) / tiles;
+  if (splits < 1) splits = 1;
+  if (splits > ksteps) splits = ksteps;
+  long long steps_per = (ksteps + splits - 1) / splits;
+  p.rows_per_split = steps_per * BK;
+  splits = (p.M + p.rows_per_split - 1) / p.rows_per_split;
+  dim3 grid(tiles, (unsigned)splits), block(256);
+  const bool lane_cols = (sc == 1);
+  if (dtype == KDT_BF16) {
+    if (lane_cols) hipLaunchKernelGGL((syrk_patch_kernel<KDT_BF16, true>), grid, block, 0, stream, p);
+    else hipLaunchKernelGGL((syrk_patch_kernel<KDT_BF16, false>), grid, block, 0, stream, p);
+  } else if (dtype == KDT_F16) {
+    if (lane_cols) hipLaunchKernelGGL((syrk_patch_kernel<KDT_F16, true>), grid, block, 0, stream, p);
+    else hipLaunchKernelGGL((syrk_patch_kernel<KDT_F16, false>), grid, block, 0, stream, p);
+  } else if (dtype == KDT_F32) {
+    if (lane_cols) hipLaunchKernelGGL((syrk_patch_kernel<KDT_F32, true>), grid, block, 0, stream, p);
+    else hipLaunchKernelGGL((syrk_patch_kernel<KDT_F32, false>), grid, block, 0, stream, p);
+  } else {
+    return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+KFAC_API int kfac_factor_ema(int sdtype, void* state, const float* ws, int n, int ldw, float alpha,
+                             int mode, hipStream_t stream) {
+  float a1 = 0.f, a2 = 1.f;
+  if (mode == 0) { a1 = alpha / (1.f - alpha); a2 = 1.f - alpha; }
+  int nb = (n + 31) / 32;
+  dim3 grid(nb, nb), block(256);
+  if (sdtype == KDT_F32)
+    hipLaunchKernelGGL(factor_ema_kernel<KDT_F32>, grid, block, 0, stream, (float*)state, ws, n, ldw, a1, a2, mode);
+  else if (sdtype == KDT_BF16)
+    hipLaunchKernelGGL(factor_ema_kernel<KDT_BF16>, grid, block, 0, stream, (uint16_t*)state, ws, n, ldw, a1, a2, mode);
+  else if (sdtype == KDT_F16)
+    hipLaunchKernelGGL(factor_ema_kernel<KDT_F16>, grid, block, 0, stream, (uint16_t*)state, ws, n, ldw, a1, a2, mode);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
+KFAC_API int kfac_triu_pack(int dtype, const void* a, void* out, int n, hipStream_t stream) {
+  dim3 grid((n + 255) / 256, n), block(256);
+  if (dtype == KDT_F32)
+    hipLaunchKernelGGL(triu_pack_kernel<KDT_F32>, grid, block, 0, stream, (const float*)a, (float*)out, n);
+  else if (dtype == KDT_BF16)
+    hipLaunchKernelGGL(triu_pack_kernel<KDT_BF16>, grid, block, 0, stream, (const uint16_t*)a, (uint16_t*)out, n);
+  else if (dtype == KDT_F16)
+    hipLaunchKernelGGL(triu_pack_kernel<KDT_F16>, grid, block, 0, stream, (const uint16_t*)a, (uint16_t*)out, n);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
+KFAC_API int kfac_triu_unpack(int dtype, const void* packed, void* a, int n, float scale,
+                              hipStream_t stream) {
+  int nb = (n + 31) / 32;
+  dim3 grid(nb, nb), block(256);
+  if (dtype == KDT_F32)
+    hipLaunchKernelGGL(triu_unpack_kernel<KDT_F32>, grid, block, 0, stream, (const float*)packed, (float*)a, n, scale);
+  else if (dtype == KDT_BF16)
+    hipLaunchKernelGGL(triu_unpack_kernel<KDT_BF16>, grid, block, 0, stream, (const uint16_t*)packed, (uint16_t*)a, n, scale);
+  else if (dtype == KDT_F16)
+    hipLaunchKernelGGL(triu_unpack_kernel<KDT_F16>, grid, block, 0, stream, (const uint16_t*)packed, (uint16_t*)a, n, scale);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}

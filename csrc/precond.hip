@@ -1,0 +1,182 @@
+// Preconditioning epilogue kernels for gfx950.
+//
+//   outer_recip     K7: dGdA[i][j] = 1 / (dG[i] * dA[j] + damping)
+//                   (reference kfac/layers/base.py:300-306)
+//   hadamard        K8 middle step, in place on v1 (nG x nA, f32):
+//                   mode 0: v1 *= dGdA ; mode 1: v1 /= (dG[i]*dA[j] + damping)
+//                   (reference kfac/layers/base.py:459-470)
+//   grouped_kl_dot  K10: vg += sum over ALL layers of <v, g> in ONE launch,
+//                   accumulated in f64 on the device (the reference does one
+//                   .item() per layer: kfac/preconditioner.py:661-682).
+//   grouped_apply   K11: g = nu * v for ALL layers in ONE launch, where nu is
+//                   computed on the device from vg (no host sync):
+//                   nu = vg==0 ? 1 : min(1, sqrt(kl_clip / |vg * lr^2|)).
+//                   (reference kfac/layers/base.py:419-430,477-483; the .grad
+//                   tensors are written in place so DDP bucket views survive)
+// Descriptor tables travel by value in the kernel arguments (< 4 KB), so a
+// table can be rebuilt every step without any H2D copy.
+#include "common.h"
+
+namespace {
+
+constexpr int MAXG = 48;
+
+struct Mat2D {
+  const float* v;   // preconditioned gradient, f32, row stride ldv
+  void* g;          // .grad, contiguous rows x cols (f32 / bf16 / f16)
+  int ldv;
+  int rows, cols;
+  int gdtype;
+};
+
+struct GroupTable {
+  int count;
+  int block_prefix[MAXG + 1];   // exclusive prefix sum of blocks per entry
+  Mat2D m[MAXG];
+};
+
+constexpr int ELEMS_PER_BLOCK = 256 * 8;
+
+__device__ __forceinline__ int find_entry(const GroupTable& t, int blk) {
+  int lo = 0, hi = t.count - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (t.block_prefix[mid] <= blk) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ float load_g(const Mat2D& m, long long idx) {
+  if (m.gdtype == KDT_F32) return ((const float*)m.g)[idx];
+  if (m.gdtype == KDT_BF16) return bf16_bits_to_f32(((const uint16_t*)m.g)[idx]);
+  return f16_bits_to_f32(((const uint16_t*)m.g)[idx]);
+}
+
+__device__ __forceinline__ void store_g(const Mat2D& m, long long idx, float v) {
+  if (m.gdtype == KDT_F32) ((float*)m.g)[idx] = v;
+  else if (m.gdtype == KDT_BF16) ((uint16_t*)m.g)[idx] = f32_to_bf16_bits(v);
+  else ((uint16_t*)m.g)[idx] = f32_to_f16_bits(v);
+}
+
+__global__ __launch_bounds__(256) void grouped_kl_dot_kernel(GroupTable t, double* vg) {
+  const int e = find_entry(t, blockIdx.x);
+  const Mat2D m = t.m[e];
+  const long long n = (long long)m.rows * m.cols;
+  const long long start = (long long)(blockIdx.x - t.block_prefix[e]) * ELEMS_PER_BLOCK;
+  float acc = 0.f;
+  for (long long i = start + threadIdx.x; i < n && i < start + ELEMS_PER_BLOCK; i += 256) {
+    int r = (int)(i / m.cols), c = (int)(i - (long long)r * m.cols);
+    acc += m.v[(long long)r * m.ldv + c] * load_g(m, i);
+  }
+  double d = wave_reduce_sum_d((double)acc);
+  __shared__ double part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = d;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(vg, part[0] + part[1] + part[2] + part[3]);
+}
+
+__global__ __launch_bounds__(256) void grouped_apply_kernel(GroupTable t, const double* vg,
+                                                            double lr2, double kl_clip,
+                                                            int use_clip) {
+  float nu = 1.f;
+  if (use_clip) {
+    double s = (*vg) * lr2;
+    if (s != 0.0) {
+      double q = sqrt(kl_clip / fabs(s));
+      nu = (float)(q < 1.0 ? q : 1.0);
+    }
+  }
+  const int e = find_entry(t, blockIdx.x);
+  const Mat2D m = t.m[e];
+  const long long n = (long long)m.rows * m.cols;
+  const long long start = (long long)(blockIdx.x - t.block_prefix[e]) * ELEMS_PER_BLOCK;
+  for (long long i = start + threadIdx.x; i < n && i < start + ELEMS_PER_BLOCK; i += 256) {
+    int r = (int)(i / m.cols), c = (int)(i - (long long)r * m.cols);
+    store_g(m, i, nu * m.v[(long long)r * m.ldv + c]);
+  }
+}
+
+__global__ __launch_bounds__(256) void outer_recip_kernel(const float* __restrict__ dG,
+                                                          const float* __restrict__ dA,
+                                                          float* __restrict__ out, int nG, int nA,
+                                                          float damping) {
+  const int i = blockIdx.y;
+  const float g = dG[i];
+  for (int j = blockIdx.x * 256 + threadIdx.x; j < nA; j += gridDim.x * 256)
+    out[(long long)i * nA + j] = 1.0f / (g * dA[j] + damping);
+}
+
+__global__ __launch_bounds__(256) void hadamard_kernel(float* __restrict__ v, int ldv,
+                                                       const float* __restrict__ dGdA,
+                                                       const float* __restrict__ dG,
+                                                       const float* __restrict__ dA, int nG,
+                                                       int nA, float damping, int mode) {
+  const int i = blockIdx.y;
+  for (int j = blockIdx.x * 256 + threadIdx.x; j < nA; j += gridDim.x * 256) {
+    long long o = (long long)i * ldv + j;
+    if (mode == 0) v[o] *= dGdA[(long long)i * nA + j];
+    else v[o] /= (dG[i] * dA[j] + damping);
+  }
+}
+
+}  // namespace
+
+// entries: flat array of `count` records {v, g, ldv, rows, cols, gdtype}
+struct KfacMatRecord {
+  const float* v;
+  void* g;
+  long long ldv, rows, cols, gdtype;
+};
+
+static int build_tables_and_launch(const KfacMatRecord* recs, int count, bool dot, double* vg,
+                                   double lr2, double kl_clip, int use_clip, hipStream_t stream) {
+  for (int base = 0; base < count; base += MAXG) {
+    GroupTable t;
+    t.count = count - base < MAXG ? count - base : MAXG;
+    int blocks = 0;
+    for (int k = 0; k < t.count; ++k) {
+      const KfacMatRecord& r = recs[base + k];
+      t.m[k].v = r.v; t.m[k].g = r.g; t.m[k].ldv = (int)r.ldv;
+      t.m[k].rows = (int)r.rows; t.m[k].cols = (int)r.cols; t.m[k].gdtype = (int)r.gdtype;
+      t.block_prefix[k] = blocks;
+      long long n = r.rows * r.cols;
+      blocks += (int)((n + ELEMS_PER_BLOCK - 1) / ELEMS_PER_BLOCK);
+    }
+    t.block_prefix[t.count] = blocks;
+    if (blocks == 0) continue;
+    if (dot)
+      hipLaunchKernelGGL(grouped_kl_dot_kernel, dim3(blocks), dim3(256), 0, stream, t, vg);
+    else
+      hipLaunchKernelGGL(grouped_apply_kernel, dim3(blocks), dim3(256), 0, stream, t, vg, lr2,
+                         kl_clip, use_clip);
+    int err = (int)hipGetLastError();
+    if (err) return err;
+  }
+  return 0;
+}
+
+KFAC_API int kfac_grouped_kl_dot(const KfacMatRecord* recs, int count, double* vg,
+                                 hipStream_t stream) {
+  return build_tables_and_launch(recs, count, true, vg, 0.0, 0.0, 0, stream);
+}
+
+KFAC_API int kfac_grouped_apply(const KfacMatRecord* recs, int count, const double* vg,
+                                double lr2, double kl_clip, int use_clip, hipStream_t stream) {
+  return build_tables_and_launch(recs, count, false, const_cast<double*>(vg), lr2, kl_clip,
+                                 use_clip, stream);
+}
+
+KFAC_API int kfac_outer_recip(const float* dG, const float* dA, float* out, int nG, int nA,
+                              float damping, hipStream_t stream) {
+  dim3 grid((nA + 255) / 256 < 16 ? (nA + 255) / 256 : 16, nG);
+  hipLaunchKernelGGL(outer_recip_kernel, grid, dim3(256), 0, stream, dG, dA, out, nG, nA, damping);
+  return (int)hipGetLastError();
+}
+
+KFAC_API int kfac_hadamard(float* v, int ldv, const float* dGdA, const float* dG, const float* dA,
+                           int nG, int nA, float damping, int mode, hipStream_t stream) {
+  dim3 grid((nA + 255) / 256 < 16 ? (nA + 255) / 256 : 16, nG);
+  hipLaunchKernelGGL(hadamard_kernel, grid, dim3(256), 0, stream, v, ldv, dGdA, dG, dA, nG, nA,
+                     damping, mode);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,214 @@
+"""Communication backends for K-FAC traffic.
+
+API parity with the reference (kfac/comm.py:1-275): a module-global
+`backend`, `init_comm_backend()`, `CommGroup(ranks)`, `Ops.{Average,Sum}`
+and `backend.{size,rank,local_rank,allreduce,broadcast,reduce,barrier,
+sync,wait}`.
+
+Differences by design (SURVEY.md section 7.4 defects #6/#7):
+  * No Horovod.  Selection is torch.distributed (RCCL on ROCm, gloo on CPU)
+    > null single-process backend.
+  * AVERAGE over a sub-group divides by the *group* size, and the post-wait
+    division is carried by each handle (the reference inspected only
+    `handles[0]`).
+  * `local_rank()` returns an int.
+  * Sub-communicators are cached by rank tuple; every rank must create them
+    in the same order (the execution plan does so once, at build time).
+
+The bulk K-FAC traffic does not go through these per-tensor calls on the
+fast path: parallel/collectives.py packs factors, eigendata and gradients
+into flat arenas and issues one collective per bucket / per root.
+"""
+import enum
+import os
+
+import torch
+import torch.distributed as dist
+
+__all__ = ['Ops', 'CommGroup', 'CommBackend', 'TorchBackend', 'Handle',
+           'init_comm_backend', 'reset_comm_backend', 'backend']
+
+backend = None
+
+
+class Ops(enum.Enum):
+    Average = 'average'
+    Sum = 'sum'
+
+
+def init_comm_backend():
+    """Select the backend once: torch.distributed if initialised, else null."""
+    global backend
+    if backend is None:
+        backend = TorchBackend() if _dist_ready() else CommBackend()
+    return backend
+
+
+def reset_comm_backend():
+    """Forget the selected backend and cached groups (tests / re-init)."""
+    global backend
+    backend = None
+    CommGroup._cache.clear()
+
+
+def _dist_ready():
+    return dist.is_available() and dist.is_initialized()
+
+
+class CommGroup(object):
+    """A set of ranks plus its communicator.
+
+    `group` is None when the ranks are the whole world (use the default
+    group) or a single rank (collectives are no-ops).
+    """
+    _cache = {}
+
+    def __init__(self, ranks):
+        self.ranks = sorted(int(r) for r in ranks)
+        key = tuple(self.ranks)
+        self.group = None
+        if _dist_ready():
+            world = dist.get_world_size()
+            if 1 < len(self.ranks) < world:
+                if key not in CommGroup._cache:
+                    CommGroup._cache[key] = dist.new_group(self.ranks)
+                self.group = CommGroup._cache[key]
+
+    @property
+    def size(self):
+        return len(self.ranks)
+
+    def __contains__(self, rank):
+        return rank in self.ranks
+
+    def __repr__(self):
+        return 'CommGroup({})'.format(self.ranks)
+
+
+class Handle(object):
+    """Async work handle; `wait()` finishes the op including any averaging."""
+    __slots__ = ('work', 'tensor', 'divisor')
+
+    def __init__(self, work, tensor=None, divisor=None):
+        self.work, self.tensor, self.divisor = work, tensor, divisor
+
+    def wait(self):
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
+        if self.divisor is not None:
+            self.tensor.div_(self.divisor)
+            self.divisor = None
+
+
+class CommBackend(object):
+    """Single-process backend: size 1, every collective is a no-op."""
+    Average = Ops.Average
+    Sum = Ops.Sum
+
+    def size(self):
+        return 1
+
+    def rank(self):
+        return 0
+
+    def local_rank(self):
+        return 0
+
+    def allreduce(self, tensor, op=Ops.Average, group=None, async_op=True):
+        return None
+
+    def broadcast(self, tensor, src, group=None, async_op=True):
+        return None
+
+    def reduce(self, tensor, dst, op=Ops.Average, group=None, async_op=True):
+        return None
+
+    def allgather(self, outputs, tensor, group=None, async_op=True):
+        for o in outputs:
+            o.copy_(tensor)
+        return None
+
+    def barrier(self):
+        return None
+
+    def sync(self, handles):
+        if handles is None:
+            return
+        if not isinstance(handles, (list, tuple)):
+            handles = [handles]
+        for h in handles:
+            self.wait(h)
+
+    def wait(self, handle):
+        if handle is not None:
+            handle.wait()
+
+
+class TorchBackend(CommBackend):
+    """torch.distributed backend (RCCL over xGMI on MI355X, gloo on CPU)."""
+
+    def size(self):
+        return dist.get_world_size()
+
+    def rank(self):
+        return dist.get_rank()
+
+    def local_rank(self):
+        v = os.environ.get('LOCAL_RANK')
+        if v is None:
+            raise RuntimeError('LOCAL_RANK must be set in the environment '
+                               'when using torch.distributed')
+        return int(v)
+
+    @staticmethod
+    def _resolve(group):
+        """-> (skip, kwargs, group_size)."""
+        if group is None:
+            return False, {}, dist.get_world_size()
+        if group.size <= 1:
+            return True, {}, 1
+        kw = {'group': group.group} if group.group is not None else {}
+        return False, kw, group.size
+
+    def allreduce(self, tensor, op=Ops.Average, group=None, async_op=True):
+        skip, kw, gsize = self._resolve(group)
+        if skip:
+            return None
+        divisor = gsize if op == Ops.Average else None
+        work = dist.all_reduce(tensor, async_op=async_op, **kw)
+        h = Handle(work if async_op else None, tensor, divisor)
+        if not async_op:
+            h.wait()
+            return None
+        return h
+
+    def broadcast(self, tensor, src, group=None, async_op=True):
+        skip, kw, _ = self._resolve(group)
+        if skip:
+            return None
+        work = dist.broadcast(tensor, src=src, async_op=async_op, **kw)
+        return Handle(work) if async_op else None
+
+    def reduce(self, tensor, dst, op=Ops.Average, group=None, async_op=True):
+        skip, kw, gsize = self._resolve(group)
+        if skip:
+            return None
+        work = dist.reduce(tensor, dst=dst, async_op=async_op, **kw)
+        divisor = gsize if (op == Ops.Average and self.rank() == dst) else None
+        h = Handle(work if async_op else None, tensor, divisor)
+        if not async_op:
+            h.wait()
+            return None
+        return h
+
+    def allgather(self, outputs, tensor, group=None, async_op=True):
+        skip, kw, _ = self._resolve(group)
+        if skip:
+            outputs[0].copy_(tensor)
+            return None
+        work = dist.all_gather(outputs, tensor, async_op=async_op, **kw)
+        return Handle(work) if async_op else None
+
+    def barrier(self):
+        dist.barrier()

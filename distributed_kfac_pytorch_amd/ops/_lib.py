@@ -1,0 +1,121 @@
+"""ctypes binding to the in-tree gfx950 kernel library (`_native/libkfac_hip.so`).
+
+The library exposes a plain C ABI (csrc/*.hip, `KFAC_API` functions); every
+entry point takes raw device pointers plus the hipStream_t of torch's
+current stream, so kernels are stream-ordered with PyTorch work and can be
+captured into hipGraphs.  On a GPU process the library is REQUIRED: the
+ops fail loudly instead of silently falling back (the CPU plumbing path is
+used only for CPU tensors).
+"""
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_HERE, '_native', 'libkfac_hip.so')
+
+_lock = threading.Lock()
+_lib = None
+_load_error = None
+
+DTYPE_CODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64: 3}
+
+c_vp = ctypes.c_void_p
+c_int = ctypes.c_int
+c_ll = ctypes.c_longlong
+c_f = ctypes.c_float
+c_d = ctypes.c_double
+
+
+class MatRecord(ctypes.Structure):
+    _fields_ = [('v', c_vp), ('g', c_vp), ('ldv', c_ll), ('rows', c_ll), ('cols', c_ll),
+                ('gdtype', c_ll)]
+
+
+class EigRecord(ctypes.Structure):
+    _fields_ = [('A', c_vp), ('Q', c_vp), ('d', c_vp), ('Vt', c_vp), ('n', c_ll)]
+
+
+_SIGS = {
+    'kfac_syrk_patch': [c_int, c_vp, c_ll, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_int, c_int,
+                        c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_vp, c_int,
+                        c_int, c_vp],
+    'kfac_factor_ema': [c_int, c_vp, c_vp, c_int, c_int, c_f, c_int, c_vp],
+    'kfac_triu_pack': [c_int, c_vp, c_vp, c_int, c_vp],
+    'kfac_triu_unpack': [c_int, c_vp, c_vp, c_int, c_f, c_vp],
+    'kfac_grouped_kl_dot': [ctypes.POINTER(MatRecord), c_int, c_vp, c_vp],
+    'kfac_grouped_apply': [ctypes.POINTER(MatRecord), c_int, c_vp, c_d, c_d, c_int, c_vp],
+    'kfac_outer_recip': [c_vp, c_vp, c_vp, c_int, c_int, c_f, c_vp],
+    'kfac_hadamard': [c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_f, c_int, c_vp],
+    'kfac_eig_jacobi_small': [ctypes.POINTER(EigRecord), c_int, c_int, c_f, c_int, c_f, c_vp],
+    'kfac_max_small_eig_n': [],
+}
+
+
+def _load():
+    global _lib, _load_error
+    with _lock:
+        if _lib is not None or _load_error is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            _load_error = 'native library not built: {} (run `python csrc/build.py`)'.format(LIB_PATH)
+            return None
+        try:
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, argt in _SIGS.items():
+                fn = getattr(lib, name)
+                fn.argtypes = argt
+                fn.restype = c_int
+            _lib = lib
+        except OSError as e:
+            _load_error = str(e)
+        return _lib
+
+
+def available():
+    return _load() is not None
+
+
+def lib():
+    """The loaded library; raises (never falls back) when it is missing."""
+    l = _load()
+    if l is None:
+        raise RuntimeError('distributed_kfac_pytorch_amd native kernels unavailable: ' +
+                           str(_load_error))
+    return l
+
+
+def use_native(t):
+    """True when tensor `t` must go through the HIP kernels."""
+    if t is None or not t.is_cuda:
+        return False
+    lib()  # loud failure on a GPU tensor without the library
+    return True
+
+
+def stream(device=None):
+    return c_vp(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return c_vp(t.data_ptr())
+
+
+def check(err, name):
+    if err != 0:
+        raise RuntimeError('{} failed with HIP error {}'.format(name, err))
+
+
+_ws = {}
+
+
+def workspace(device, numel, dtype=torch.float32, tag='main'):
+    """A grow-only scratch buffer per (device, tag, dtype); stream-ordered reuse."""
+    key = (str(device), tag, dtype)
+    buf = _ws.get(key)
+    if buf is None or buf.numel() < numel:
+        buf = torch.empty(max(numel, 1), dtype=dtype, device=device)
+        _ws[key] = buf
+    return buf[:numel]

@@ -1,0 +1,117 @@
+"""Symmetric eigendecomposition / damped inverse of Kronecker factors (K6, K9).
+
+GPU path (MI355X):
+  * n <= 192: every such factor of the step is solved by ONE launch of the
+    batched LDS Jacobi kernel (csrc/eig_jacobi.hip), one workgroup per matrix.
+  * larger n: rocSOLVER through torch.linalg.eigh, issued on a small pool of
+    side streams so independent latency-bound solves overlap (each call is
+    dominated by serial panel steps at these sizes: profiles/r1_probe_baseline.json).
+CPU path: torch.linalg.eigh (the reference semantics, kfac/layers/utils.py:45-74).
+
+Results: ascending eigenvalues clipped at `clip` (reference default 0.0),
+Q row-major contiguous with eigenvector k in column k.
+"""
+import torch
+
+from . import _lib
+
+__all__ = ['symeig_many', 'inverse_many', 'SMALL_N']
+
+SMALL_N = 192
+_streams = {}
+
+
+def _side_streams(device, k):
+    key = str(device)
+    pool = _streams.get(key)
+    if pool is None or len(pool) < k:
+        pool = [torch.cuda.Stream(device=device) for _ in range(k)]
+        _streams[key] = pool
+    return pool[:k]
+
+
+def _jacobi_small(mats, clip, max_sweeps=30, tol=1e-7):
+    dev = mats[0].device
+    outs = []
+    recs = (_lib.EigRecord * len(mats))()
+    scratch = []
+    for i, A in enumerate(mats):
+        n = A.shape[0]
+        A = A.contiguous()
+        Q = torch.empty(n, n, dtype=torch.float32, device=dev)
+        d = torch.empty(n, dtype=torch.float32, device=dev)
+        Vt = torch.empty(n, n, dtype=torch.float32, device=dev)
+        scratch.append((A, Vt))
+        recs[i].A = A.data_ptr(); recs[i].Q = Q.data_ptr(); recs[i].d = d.data_ptr()
+        recs[i].Vt = Vt.data_ptr(); recs[i].n = n
+        outs.append((Q, d))
+    _lib.check(_lib.lib().kfac_eig_jacobi_small(recs, len(mats), max_sweeps, tol,
+                                                 int(clip is not None),
+                                                 float(clip if clip is not None else 0.0),
+                                                 _lib.stream(dev)), 'kfac_eig_jacobi_small')
+    # keep inputs / scratch alive until the kernel has consumed them
+    cur = torch.cuda.current_stream(dev)
+    for A, Vt in scratch:
+        A.record_stream(cur)
+        Vt.record_stream(cur)
+    return outs
+
+
+def _library_eigh(mats, clip, n_streams=4):
+    dev = mats[0].device
+    cur = torch.cuda.current_stream(dev)
+    pool = _side_streams(dev, min(n_streams, len(mats)))
+    outs = [None] * len(mats)
+    for s in pool:
+        s.wait_stream(cur)
+    # largest first so the long solves start early
+    order = sorted(range(len(mats)), key=lambda i: -mats[i].shape[0])
+    for k, i in enumerate(order):
+        s = pool[k % len(pool)]
+        with torch.cuda.stream(s):
+            d, Q = torch.linalg.eigh(mats[i])
+            Q = Q.contiguous()
+            if clip is not None:
+                d = torch.clamp(d, min=clip)
+        mats[i].record_stream(s)
+        Q.record_stream(cur)
+        d.record_stream(cur)
+        outs[i] = (Q, d)
+    for s in pool:
+        cur.wait_stream(s)
+    return outs
+
+
+def symeig_many(mats, clip=0.0, solver='auto'):
+    """Eigendecompose a list of symmetric fp32 matrices -> list of (Q, d)."""
+    if len(mats) == 0:
+        return []
+    if not _lib.use_native(mats[0]):
+        outs = []
+        for A in mats:
+            d, Q = torch.linalg.eigh(A)
+            Q = Q.contiguous()
+            if clip is not None:
+                d = torch.clamp(d, min=clip)
+            outs.append((Q, d))
+        return outs
+    small = [i for i, A in enumerate(mats)
+             if A.shape[0] <= SMALL_N and solver in ('auto', 'jacobi')]
+    large = [i for i in range(len(mats)) if i not in set(small)]
+    outs = [None] * len(mats)
+    if small:
+        for i, r in zip(small, _jacobi_small([mats[i] for i in small], clip)):
+            outs[i] = r
+    if large:
+        for i, r in zip(large, _library_eigh([mats[i] for i in large], clip)):
+            outs[i] = r
+    return outs
+
+
+def inverse_many(mats, damping):
+    """(F + damping I)^-1 for symmetric positive definite F (Cholesky)."""
+    outs = []
+    for A in mats:
+        M = A + torch.diag(A.new_full((A.shape[0],), damping))
+        outs.append(torch.cholesky_inverse(torch.linalg.cholesky(M)))
+    return outs

@@ -1,0 +1,148 @@
+"""Bucketed K-FAC collectives over RCCL (xGMI) / gloo.
+
+FactorAllreduce   X1+X2: the upper triangles of every
+                  A and G factor are packed (K12 kernel) into one flat arena
+                  per dtype, all-reduced (SUM) in buckets of whole factors of
+                  about `bucket_cap_mb`, and unpacked with the 1/world
+                  averaging folded into the unpack kernel.  Halves the bytes
+                  on the wire and turns 2 x #layers NCCL calls into a handful.
+                  Buckets are issued back to back (async) and each bucket is
+                  unpacked as soon as its own handle completes.
+broadcast_eigendata  X3/X4: one broadcast per owner region of the plan's
+                  eigen arena within the owner's inverse group.
+broadcast_gradients  X5: one broadcast per inverse block within this rank's
+                  gradient group (MEM_OPT / HYBRID_OPT).
+All calls are asynchronous collectives whose completion only orders the
+current HIP stream behind RCCL's stream: no host synchronisation.
+"""
+import torch
+
+from .. import comm
+from ..ops import comm_pack
+
+__all__ = ['FactorAllreduce', 'broadcast_eigendata', 'broadcast_gradients']
+
+
+class _Entry(object):
+    __slots__ = ('layer', 'key', 'n', 'off', 'numel')
+
+    def __init__(self, layer, key, n, off):
+        self.layer, self.key, self.n, self.off = layer, key, n, off
+        self.numel = comm_pack.triu_numel(n)
+
+
+class FactorAllreduce(object):
+    def __init__(self, layers, bucket_cap_mb=64.0, symmetric=True):
+        self.layers = layers
+        self.bucket_cap = int(bucket_cap_mb * 2 ** 20)
+        self.symmetric = symmetric
+        self._signature = None
+        self.arenas = {}    # dtype -> flat tensor
+        self.buckets = []   # (dtype, start, end, [entries])
+
+    def _current_signature(self):
+        sig = []
+        for layer in self.layers:
+            for key in ('A', 'G'):
+                t = layer.state.get(key)
+                sig.append(None if t is None else (tuple(t.shape), t.dtype, str(t.device)))
+        return tuple(sig)
+
+    def _build(self):
+        by_dtype = {}
+        device = None
+        for layer in self.layers:
+            for key in ('A', 'G'):
+                t = layer.state.get(key)
+                if t is None:
+                    continue
+                device = t.device
+                by_dtype.setdefault(t.dtype, []).append((layer, key, t.shape[0]))
+        self.arenas, self.buckets = {}, []
+        for dtype, items in by_dtype.items():
+            # reverse registration order: the last layers' factors are the
+            # first complete in backward, so they open the first bucket
+            items = list(reversed(items))
+            off, entries = 0, []
+            for layer, key, n in items:
+                e = _Entry(layer, key, n, off)
+                entries.append(e)
+                off += e.numel if self.symmetric else n * n
+            esize = torch.tensor([], dtype=dtype).element_size()
+            self.arenas[dtype] = torch.empty(max(off, 1), dtype=dtype, device=device)
+            cur, start, size = [], 0, 0
+            for e in entries:
+                nbytes = (e.numel if self.symmetric else e.n * e.n) * esize
+                if cur and size + nbytes > self.bucket_cap:
+                    self.buckets.append((dtype, start, e.off, cur))
+                    cur, start, size = [], e.off, 0
+                cur.append(e)
+                size += nbytes
+            if cur:
+                self.buckets.append((dtype, start, off, cur))
+        self._signature = self._current_signature()
+
+    def __call__(self):
+        backend = comm.backend
+        world = backend.size()
+        if world == 1:
+            return
+        if self._signature != self._current_signature():
+            self._build()
+        for dtype, arena in self.arenas.items():
+            for b_dtype, s, e, entries in self.buckets:
+                if b_dtype != dtype:
+                    continue
+                for ent in entries:
+                    self._pack(ent, arena)
+        pending = []
+        for dtype, s, e, entries in self.buckets:
+            h = backend.allreduce(self.arenas[dtype][s:e], op=comm.Ops.Sum)
+            pending.append((h, dtype, entries))
+        for h, dtype, entries in pending:
+            backend.wait(h)
+            arena = self.arenas[dtype]
+            for ent in entries:
+                self._unpack(ent, arena, world)
+
+    def _pack(self, ent, arena):
+        t = ent.layer.state[ent.key]
+        if self.symmetric:
+            comm_pack.pack_triu(t, arena[ent.off:ent.off + ent.numel])
+        else:
+            arena[ent.off:ent.off + ent.n * ent.n].copy_(t.reshape(-1))
+
+    def _unpack(self, ent, arena, world):
+        t = ent.layer.state[ent.key]
+        if self.symmetric:
+            comm_pack.unpack_triu(arena[ent.off:ent.off + ent.numel], t, divisor=world)
+        else:
+            t.view(-1).copy_(arena[ent.off:ent.off + ent.n * ent.n])
+            t /= world
+
+
+def broadcast_eigendata(plan):
+    backend = comm.backend
+    if backend.size() == 1 or plan.eig_arena is None:
+        return
+    handles = []
+    for owner in sorted(plan.eig_regions):
+        s, e = plan.eig_regions[owner]
+        if e <= s:
+            continue
+        handles.append(backend.broadcast(plan.eig_arena[s:e], src=owner,
+                                         group=plan.eig_group(owner)))
+    backend.sync(handles)
+
+
+def broadcast_gradients(plan):
+    backend = comm.backend
+    if backend.size() == 1 or plan.grad_group.size <= 1:
+        return
+    handles = []
+    for b, (s, e) in enumerate(plan.grad_blocks):
+        if e <= s:
+            continue
+        handles.append(backend.broadcast(plan.grad_arena[s:e], src=plan.grad_block_src(b),
+                                         group=plan.grad_group))
+    backend.sync(handles)

@@ -1,0 +1,140 @@
+"""Layer-wise work distribution: LPT load balancing and rank-group layout.
+
+Parity targets (reference, read-only at /root/reference):
+  * `load_balance`           ~ kfac/utils.py:169-196 (greedy LPT, goldens in
+                               tests/load_balance.py)
+  * `partition_grad_ranks`   ~ kfac/utils.py:150-153 (strided groups)
+  * `partition_inv_ranks`    ~ kfac/utils.py:156-159 (contiguous blocks)
+  * `WorkerAllocator`        ~ kfac/utils.py:59-147
+  * `get_block_boundary`     ~ kfac/utils.py:199-212
+
+The allocator here is pure bookkeeping: it never creates communicators
+itself.  Group objects are produced lazily through a `group_factory`
+callback so the execution plan (parallel/plan.py) can create every
+sub-communicator once, in a rank-independent order, at plan build time.
+"""
+import heapq
+
+__all__ = ['load_balance', 'partition_grad_ranks', 'partition_inv_ranks',
+           'WorkerAllocator', 'get_block_boundary', 'try_contiguous']
+
+
+def load_balance(n_workers, work):
+    """Greedy longest-processing-time assignment of `work` items to workers.
+
+    Items are visited in decreasing cost (ties keep their original order) and
+    each goes to the currently least-loaded worker (ties -> lowest index).
+    Returns a list `assignment[i] = worker of item i`.
+    """
+    if n_workers <= 0:
+        raise ValueError('n_workers must be > 0')
+    if len(work) == 0:
+        raise ValueError('work cannot be an empty list')
+    order = sorted(range(len(work)), key=lambda i: -work[i])
+    heap = [(0, w) for w in range(n_workers)]  # (load, worker) -> ties by index
+    heapq.heapify(heap)
+    assignment = [0] * len(work)
+    for i in order:
+        load, w = heapq.heappop(heap)
+        assignment[i] = w
+        heapq.heappush(heap, (load + work[i], w))
+    return assignment
+
+
+def partition_grad_ranks(size, grad_workers):
+    """Strided gradient-broadcast groups: group k = {k, k+gw, k+2gw, ...}."""
+    return [list(range(k, size, grad_workers)) for k in range(grad_workers)]
+
+
+def partition_inv_ranks(size, grad_workers):
+    """Contiguous inverse-broadcast groups of `grad_workers` ranks each."""
+    return [list(range(s, min(s + grad_workers, size)))
+            for s in range(0, size, grad_workers)]
+
+
+class WorkerAllocator(object):
+    """Rank-group layout for COMM_OPT / MEM_OPT / HYBRID_OPT.
+
+    Args:
+      size: world size.
+      compute_grad_fraction: fraction of ranks that precondition each layer
+        (1 -> COMM_OPT, 0 -> MEM_OPT, in between -> HYBRID_OPT).
+      group_factory: callable(ranks) -> group object.  Defaults to
+        `comm.CommGroup`, created eagerly in a rank-independent order.
+    """
+
+    def __init__(self, size, compute_grad_fraction, group_factory=None):
+        grad_workers = max(1, int(round(size * compute_grad_fraction)))
+        if size % grad_workers != 0:
+            raise ValueError('compute_grad_fraction must produce equally '
+                             'sized groups')
+        self.size = size
+        self.compute_grad_fraction = compute_grad_fraction
+        self.grad_workers = grad_workers
+        self.bcast_grad_ranks = partition_grad_ranks(size, grad_workers)
+        self.bcast_inv_ranks = partition_inv_ranks(size, grad_workers)
+        if group_factory is None:
+            from .. import comm
+            group_factory = comm.CommGroup
+        # creation order is identical on every rank: inverse groups, then
+        # gradient groups (each sub-communicator is a collective call)
+        self.bcast_inv_groups = [group_factory(r) for r in self.bcast_inv_ranks]
+        self.bcast_grad_groups = [group_factory(r) for r in self.bcast_grad_ranks]
+        self._inv_index = {r: i for i, g in enumerate(self.bcast_inv_ranks) for r in g}
+        self._grad_index = {r: i for i, g in enumerate(self.bcast_grad_ranks) for r in g}
+
+    @property
+    def grad_groups(self):
+        return len(self.bcast_grad_groups)
+
+    @property
+    def inv_groups(self):
+        return len(self.bcast_inv_groups)
+
+    def get_inv_ranks(self, rank):
+        return self.bcast_inv_ranks[self._inv_index[rank]]
+
+    def get_inv_group(self, rank):
+        return self.bcast_inv_groups[self._inv_index[rank]]
+
+    def get_grad_ranks(self, rank):
+        return self.bcast_grad_ranks[self._grad_index[rank]]
+
+    def get_grad_group(self, rank):
+        return self.bcast_grad_groups[self._grad_index[rank]]
+
+    def get_grad_src(self, src_ranks, rank):
+        """The member of `src_ranks` that lives in `rank`'s gradient group."""
+        members = set(self.get_grad_ranks(rank))
+        hits = [s for s in src_ranks if s in members]
+        if len(hits) != 1:
+            raise RuntimeError('gradient group of rank {} intersects compute '
+                               'ranks {} in {} ranks'.format(rank, src_ranks, len(hits)))
+        return hits[0]
+
+    def get_grad_groups(self, src_ranks):
+        """Per world rank: (src rank, gradient group) for a layer whose
+        preconditioned gradient is computed on `src_ranks`."""
+        return [(self.get_grad_src(src_ranks, r), self.get_grad_group(r))
+                for r in range(self.size)]
+
+
+def get_block_boundary(index, block_count, shape):
+    """Start/end indices of diagonal block `index` when splitting `shape`
+    into `block_count` blocks (last block absorbs the remainder)."""
+    if index >= block_count:
+        raise ValueError('Index ({}) greater than number of requested blocks '
+                         '({})'.format(index, block_count))
+    if block_count > min(shape):
+        raise ValueError('Requested blocks ({}) greater than minimum possible '
+                         'blocks for shape {}'.format(block_count, shape))
+    starts, ends = [], []
+    for dim in shape:
+        step = dim // block_count
+        starts.append(step * index)
+        ends.append(step * (index + 1) if index + 1 < block_count else dim)
+    return starts, ends
+
+
+def try_contiguous(x):
+    return x if x.is_contiguous() else x.contiguous()
