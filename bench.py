@@ -1,0 +1,166 @@
+"""Headline benchmark: ResNet-50 K-FAC + SGD training throughput on MI355X.
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Metric (BASELINE.json): images/sec (whole node) for ResNet-50 / ImageNet-1k
+shaped synthetic data, K-FAC (COMM_OPT) preconditioning SGD, bf16 autocast,
+per-GPU batch 32 (reference: examples/torch_imagenet_resnet.py:49-60), factor
+update every 10 steps, eigendecomposition every 100 steps, damping 1e-3,
+kl_clip 1e-3 (reference: scripts/slurm/horovod_imagenet_kfac.slurm:26-31).
+
+Timing: W untimed warmup steps, then exactly K steps bracketed by a barrier +
+device synchronize on both sides; the max over ranks is reported.  The K-FAC
+step counter is reset to 0 at the start of the timed window so the window
+always OPENS with an inverse (eigendecomposition) step: with K < 100 the
+window contains more inverse work per step than steady state (conservative),
+with K = 100 exactly the steady-state mix.  Nothing is skipped inside the
+timed region (factors, inverses, preconditioning, KL clip, DDP all-reduce,
+SGD update all run).  Random-init weights, synthetic data (no network).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import distributed_kfac_pytorch_amd as kfac  # noqa: E402
+from distributed_kfac_pytorch_amd.models import resnet  # noqa: E402
+from distributed_kfac_pytorch_amd.parallel import launch  # noqa: E402
+
+METRIC = 'images/sec (whole node) ResNet-50 K-FAC+SGD'
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=100)
+    ap.add_argument('--warmup', type=int, default=10)
+    ap.add_argument('--model', default='resnet50')
+    ap.add_argument('--batch-size', type=int, default=32, help='per-GPU batch')
+    ap.add_argument('--image-size', type=int, default=224)
+    ap.add_argument('--kfac-update-freq', type=int, default=100)
+    ap.add_argument('--kfac-cov-update-freq', type=int, default=10)
+    ap.add_argument('--damping', type=float, default=0.001)
+    ap.add_argument('--kl-clip', type=float, default=0.001)
+    ap.add_argument('--comm-method', default='comm-opt',
+                    choices=['comm-opt', 'mem-opt', 'hybrid-opt'])
+    ap.add_argument('--grad-worker-fraction', type=float, default=0.25)
+    ap.add_argument('--no-kfac', action='store_true', help='SGD-only baseline')
+    ap.add_argument('--channels-last', type=int, default=1)
+    ap.add_argument('--eigen-solver', default='auto')
+    ap.add_argument('--profile-phases', action='store_true')
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    device = launch.init_distributed()
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    if world != args.gpus and rank == 0:
+        print('warning: --gpus {} but world size {}'.format(args.gpus, world), file=sys.stderr)
+    torch.manual_seed(1234 + rank)
+    torch.backends.cudnn.benchmark = True
+
+    model = resnet.get_model(args.model).to(device)
+    mf = torch.channels_last if args.channels_last else torch.contiguous_format
+    model = model.to(memory_format=mf)
+    model = launch.wrap_ddp(model, device, broadcast_buffers=False)
+    base_lr = 0.0125 * world
+    opt = torch.optim.SGD(model.parameters(), lr=base_lr, momentum=0.9, weight_decay=5e-5)
+    pre = None
+    if not args.no_kfac:
+        method = {'comm-opt': kfac.CommMethod.COMM_OPT, 'mem-opt': kfac.CommMethod.MEM_OPT,
+                  'hybrid-opt': kfac.CommMethod.HYBRID_OPT}[args.comm_method]
+        pre = kfac.KFAC(model, damping=args.damping, factor_decay=0.95,
+                        factor_update_freq=args.kfac_cov_update_freq,
+                        inv_update_freq=args.kfac_update_freq, kl_clip=args.kl_clip, lr=base_lr,
+                        comm_method=method, grad_worker_fraction=args.grad_worker_fraction,
+                        distribute_layer_factors=False, eigen_solver=args.eigen_solver,
+                        profile=args.profile_phases)
+
+    B, S = args.batch_size, args.image_size
+    g = torch.Generator(device=device).manual_seed(rank)
+    x = torch.randn(B, 3, S, S, device=device, generator=g).to(memory_format=mf)
+    y = torch.randint(0, 1000, (B,), device=device, generator=g)
+
+    def step():
+        opt.zero_grad(set_to_none=False)
+        with torch.autocast(device_type=device.type, dtype=torch.bfloat16):
+            out = model(x)
+            loss = F.cross_entropy(out, y, label_smoothing=0.1)
+        loss.backward()
+        if pre is not None:
+            pre.step()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    if pre is not None:
+        pre.param_groups[0]['step'] = 0
+        pre.timer.reset()
+    if dist.is_initialized():
+        dist.barrier()
+    if device.type == 'cuda':
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    if device.type == 'cuda':
+        torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if dist.is_initialized():
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    ms = elapsed / args.steps * 1e3
+    gbatch = B * world
+    value = gbatch * args.steps / elapsed
+    phases = pre.timer.summary() if (pre is not None and args.profile_phases) else None
+    if rank == 0:
+        rec = {
+            'metric': METRIC if pre is not None else 'images/sec (whole node) ResNet-50 SGD-only',
+            'value': round(value, 2),
+            'unit': 'images/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': round(ms, 3),
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'bf16',
+            'data': 'synthetic (random ImageNet-shaped 3x224x224 images, random labels, '
+                    'random-init weights)',
+            'config': {'model': args.model, 'global_batch': gbatch, 'per_gpu_batch': B,
+                       'image_size': S, 'seq_len': None, 'parallelism': 'dp{}'.format(world),
+                       'kfac': None if pre is None else {
+                           'comm_method': args.comm_method,
+                           'factor_update_freq': args.kfac_cov_update_freq,
+                           'inv_update_freq': args.kfac_update_freq,
+                           'damping': args.damping, 'kl_clip': args.kl_clip},
+                       'final_loss': round(float(loss.item()), 4)},
+        }
+        if phases is not None:
+            rec['kfac_phase_ms_total'] = {k: round(v, 2) for k, v in phases.items()}
+            rec['kfac_step_ms'] = round(sum(phases.values()) / args.steps, 3)
+        print(json.dumps(rec), flush=True)
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -41,7 +41,8 @@ struct EigBatch {
 
 __global__ __launch_bounds__(256) void jacobi_small_kernel(EigBatch batch) {
   extern __shared__ float S[];
-  __shared__ float rc[NMAX / 2], rs[NMAX / 2];
+  __shared__ float rc[NMAX / 2], rs[NMAX / 2], rt[NMAX / 2], rpp[NMAX / 2], rqq[NMAX / 2],
+      rpq[NMAX / 2];
   __shared__ int rp[NMAX / 2], rq[NMAX / 2];
   __shared__ int nrot;
   __shared__ float dsh[NMAX];
@@ -75,15 +76,16 @@ __global__ __launch_bounds__(256) void jacobi_small_kernel(EigBatch batch) {
         else { a = (r + k) % m; b = (r - k + m) % m; }
         int p = a < b ? a : b, q = a < b ? b : a;
         float app = S[p * ld + p], aqq = S[q * ld + q], apq = S[p * ld + q];
-        float c = 1.f, s = 0.f;
+        float c = 1.f, s = 0.f, t = 0.f;
         if (apq != 0.f && fabsf(apq) > batch.tol * sqrtf(fabsf(app) * fabsf(aqq))) {
           float theta = (aqq - app) / (2.f * apq);
-          float t = (theta >= 0.f ? 1.f : -1.f) / (fabsf(theta) + sqrtf(1.f + theta * theta));
+          t = (theta >= 0.f ? 1.f : -1.f) / (fabsf(theta) + sqrtf(1.f + theta * theta));
           c = 1.f / sqrtf(1.f + t * t);
           s = t * c;
           atomicAdd(&nrot, 1);
         }
         rp[k] = p; rq[k] = q; rc[k] = c; rs[k] = s;
+        rt[k] = t; rpp[k] = app; rqq[k] = aqq; rpq[k] = apq;
       }
       __syncthreads();
       // --- column phase: S <- S J, and V <- V J (rows p, q of V^T)
@@ -92,13 +94,14 @@ __global__ __launch_bounds__(256) void jacobi_small_kernel(EigBatch batch) {
         float c = rc[k], s = rs[k];
         if (s == 0.f) continue;
         int p = rp[k], q = rq[k];
+        const float tau = s / (1.f + c);
         float sp = S[i * ld + p], sq = S[i * ld + q];
-        S[i * ld + p] = c * sp - s * sq;
-        S[i * ld + q] = s * sp + c * sq;
+        S[i * ld + p] = sp - s * (sq + tau * sp);
+        S[i * ld + q] = sq + s * (sp - tau * sq);
         if (i < n && q < n) {
           float vp = J.Vt[(long long)p * n + i], vq = J.Vt[(long long)q * n + i];
-          J.Vt[(long long)p * n + i] = c * vp - s * vq;
-          J.Vt[(long long)q * n + i] = s * vp + c * vq;
+          J.Vt[(long long)p * n + i] = vp - s * (vq + tau * vp);
+          J.Vt[(long long)q * n + i] = vq + s * (vp - tau * vq);
         }
       }
       __syncthreads();
@@ -108,14 +111,22 @@ __global__ __launch_bounds__(256) void jacobi_small_kernel(EigBatch batch) {
         float c = rc[k], s = rs[k];
         if (s == 0.f) continue;
         int p = rp[k], q = rq[k];
+        const float tau = s / (1.f + c);
         float sp = S[p * ld + j], sq = S[q * ld + j];
-        S[p * ld + j] = c * sp - s * sq;
-        S[q * ld + j] = s * sp + c * sq;
+        S[p * ld + j] = sp - s * (sq + tau * sp);
+        S[q * ld + j] = sq + s * (sp - tau * sq);
       }
       __syncthreads();
-      // exact zero for the annihilated entries
+      // annihilated entries are exactly zero; the rotated diagonal uses the
+      // cancellation-free a_pp - t a_pq / a_qq + t a_pq (the generic two-sided
+      // update of the diagonal loses ~20x accuracy in fp32)
       for (int k = tid; k < npairs; k += 256) {
-        if (rs[k] != 0.f) { S[rp[k] * ld + rq[k]] = 0.f; S[rq[k] * ld + rp[k]] = 0.f; }
+        if (rs[k] != 0.f) {
+          int p = rp[k], q = rq[k];
+          S[p * ld + q] = 0.f; S[q * ld + p] = 0.f;
+          S[p * ld + p] = rpp[k] - rt[k] * rpq[k];
+          S[q * ld + q] = rqq[k] + rt[k] * rpq[k];
+        }
       }
       __syncthreads();
     }

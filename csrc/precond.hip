@@ -19,14 +19,20 @@
 
 namespace {
 
-constexpr int MAXG = 48;
+constexpr int MAXG = 40;
 
+// v: (rows x cols) f32 with row stride ldv.  g: the parameter's .grad in ANY
+// memory layout: column `col` of the K-FAC matrix is (c, i, j) =
+// (col / kk, (col % kk) / kw, col % kw) -> element r*gs0 + c*gs1 + i*gs2 + j*gs3
+// (conv weights in channels_last, linear weights, bias vectors alike).
 struct Mat2D {
-  const float* v;   // preconditioned gradient, f32, row stride ldv
-  void* g;          // .grad, contiguous rows x cols (f32 / bf16 / f16)
+  const float* v;
+  void* g;
+  long long gs0, gs1, gs2, gs3;
   int ldv;
   int rows, cols;
   int gdtype;
+  int kk, kw;
 };
 
 struct GroupTable {
@@ -44,6 +50,14 @@ __device__ __forceinline__ int find_entry(const GroupTable& t, int blk) {
     if (t.block_prefix[mid] <= blk) lo = mid; else hi = mid - 1;
   }
   return lo;
+}
+
+__device__ __forceinline__ long long g_index(const Mat2D& m, int r, int col) {
+  int c = col / m.kk;
+  int rem = col - c * m.kk;
+  int i = rem / m.kw;
+  int j = rem - i * m.kw;
+  return (long long)r * m.gs0 + (long long)c * m.gs1 + (long long)i * m.gs2 + (long long)j * m.gs3;
 }
 
 __device__ __forceinline__ float load_g(const Mat2D& m, long long idx) {
@@ -66,7 +80,7 @@ __global__ __launch_bounds__(256) void grouped_kl_dot_kernel(GroupTable t, doubl
   float acc = 0.f;
   for (long long i = start + threadIdx.x; i < n && i < start + ELEMS_PER_BLOCK; i += 256) {
     int r = (int)(i / m.cols), c = (int)(i - (long long)r * m.cols);
-    acc += m.v[(long long)r * m.ldv + c] * load_g(m, i);
+    acc += m.v[(long long)r * m.ldv + c] * load_g(m, g_index(m, r, c));
   }
   double d = wave_reduce_sum_d((double)acc);
   __shared__ double part[4];
@@ -92,7 +106,7 @@ __global__ __launch_bounds__(256) void grouped_apply_kernel(GroupTable t, const 
   const long long start = (long long)(blockIdx.x - t.block_prefix[e]) * ELEMS_PER_BLOCK;
   for (long long i = start + threadIdx.x; i < n && i < start + ELEMS_PER_BLOCK; i += 256) {
     int r = (int)(i / m.cols), c = (int)(i - (long long)r * m.cols);
-    store_g(m, i, nu * m.v[(long long)r * m.ldv + c]);
+    store_g(m, g_index(m, r, c), nu * m.v[(long long)r * m.ldv + c]);
   }
 }
 
@@ -121,11 +135,12 @@ __global__ __launch_bounds__(256) void hadamard_kernel(float* __restrict__ v, in
 
 }  // namespace
 
-// entries: flat array of `count` records {v, g, ldv, rows, cols, gdtype}
+// entries: flat array of `count` records (ops/_lib.py MatRecord)
 struct KfacMatRecord {
   const float* v;
   void* g;
   long long ldv, rows, cols, gdtype;
+  long long gs0, gs1, gs2, gs3, kk, kw;
 };
 
 static int build_tables_and_launch(const KfacMatRecord* recs, int count, bool dot, double* vg,
@@ -138,6 +153,8 @@ static int build_tables_and_launch(const KfacMatRecord* recs, int count, bool do
       const KfacMatRecord& r = recs[base + k];
       t.m[k].v = r.v; t.m[k].g = r.g; t.m[k].ldv = (int)r.ldv;
       t.m[k].rows = (int)r.rows; t.m[k].cols = (int)r.cols; t.m[k].gdtype = (int)r.gdtype;
+      t.m[k].gs0 = r.gs0; t.m[k].gs1 = r.gs1; t.m[k].gs2 = r.gs2; t.m[k].gs3 = r.gs3;
+      t.m[k].kk = (int)r.kk; t.m[k].kw = (int)r.kw;
       t.block_prefix[k] = blocks;
       long long n = r.rows * r.cols;
       blocks += (int)((n + ELEMS_PER_BLOCK - 1) / ELEMS_PER_BLOCK);

@@ -232,7 +232,7 @@ class KFACLayer(object):
         """Store an eigendecomposition (Q, d) or inverse for factor `which`."""
         if isinstance(result, tuple):
             self._store_result('Q' + which, result[0])
-            self.state['d' + which] = result[1].to(self.inv_dtype)
+            self._store_result('d' + which, result[1])
             if which == 'G' and self.prediv_eigenvalues:
                 if self.state.get('dA') is None:
                     raise ValueError('compute_A_inv must be called before compute_G_inv if '
@@ -309,14 +309,18 @@ class KFACLayer(object):
         return [buf.view(w.shape)]
 
     def grad_pairs(self):
-        """[(v 2-D view, .grad 2-D view)] for the grouped KL-dot / apply kernels."""
+        """[(v 2-D view, .grad tensor)] for the grouped KL-dot / apply kernels.
+
+        The .grad keeps its own memory layout (e.g. channels_last conv weights);
+        the kernels map K-FAC column (c, kh, kw) onto its strides."""
         buf = self._pgrad_matrix()
         g = self._get_weight_grad()
-        nG = buf.shape[0]
+        if g is None:
+            raise RuntimeError('{} has no gradient; K-FAC needs every registered layer to '
+                               'take part in backward'.format(self))
         if self.has_bias:
-            return [(buf[:, :-1], g.view(nG, -1)),
-                    (buf[:, -1:], self._get_bias_grad().view(nG, 1))]
-        return [(buf, g.view(nG, -1))]
+            return [(buf[:, :-1], g), (buf[:, -1:], self._get_bias_grad())]
+        return [(buf, g)]
 
     def compute_preconditioned_gradient(self, damping=0.001):
         if self.compute_grad_ranks is None:

@@ -64,7 +64,7 @@ class Conv2dLayer(KFACLayer):
         for x in a_inputs:
             p = self._patches(x)
             spatial = p.size(1) * p.size(2)
-            p = p.view(-1, p.size(-1))
+            p = p.reshape(-1, p.size(-1))
             if self.has_bias:
                 p = lutils.append_bias_ones(p)
             parts.append(p / spatial)

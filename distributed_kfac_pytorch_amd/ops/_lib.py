@@ -31,7 +31,8 @@ c_d = ctypes.c_double
 
 class MatRecord(ctypes.Structure):
     _fields_ = [('v', c_vp), ('g', c_vp), ('ldv', c_ll), ('rows', c_ll), ('cols', c_ll),
-                ('gdtype', c_ll)]
+                ('gdtype', c_ll), ('gs0', c_ll), ('gs1', c_ll), ('gs2', c_ll), ('gs3', c_ll),
+                ('kk', c_ll), ('kw', c_ll)]
 
 
 class EigRecord(ctypes.Structure):

@@ -72,16 +72,33 @@ def precondition_inverse(grad, A_inv, G_inv, out=None):
 
 
 def _records(pairs):
+    """pairs: (v, g) with v a row-strided (rows x cols) f32 view of the
+    preconditioned gradient and g the parameter's .grad in any layout whose
+    logical shape flattens to (rows, cols) in K-FAC column order (c, kh, kw)."""
     recs = (_lib.MatRecord * len(pairs))()
     for i, (v, g) in enumerate(pairs):
-        if v.dim() != 2 or v.stride(1) != 1 or not g.is_contiguous():
-            raise ValueError('kl/apply expects row-strided v and contiguous grads')
-        recs[i].v = v.data_ptr()
-        recs[i].g = g.data_ptr()
-        recs[i].ldv = v.stride(0)
-        recs[i].rows = v.shape[0]
-        recs[i].cols = v.shape[1]
-        recs[i].gdtype = _lib.DTYPE_CODE[g.dtype]
+        if v.dim() != 2 or v.stride(1) != 1:
+            raise ValueError('kl/apply expects a row-strided 2-D v')
+        r = recs[i]
+        r.v = v.data_ptr()
+        r.g = g.data_ptr()
+        r.ldv = v.stride(0)
+        r.rows, r.cols = v.shape
+        r.gdtype = _lib.DTYPE_CODE[g.dtype]
+        st = g.stride()
+        if g.dim() == 4:
+            r.gs0, r.gs1, r.gs2, r.gs3 = st
+            r.kk, r.kw = g.shape[2] * g.shape[3], g.shape[3]
+        elif g.dim() == 2:
+            r.gs0, r.gs1, r.gs2, r.gs3 = st[0], st[1], 0, 0
+            r.kk, r.kw = 1, 1
+        elif g.dim() == 1:
+            r.gs0, r.gs1, r.gs2, r.gs3 = st[0], 0, 0, 0
+            r.kk, r.kw = 1, 1
+        else:
+            raise ValueError('unsupported gradient rank {}'.format(g.dim()))
+        if g.numel() != v.numel():
+            raise ValueError('gradient / preconditioned gradient size mismatch')
     return recs
 
 
@@ -89,7 +106,7 @@ def kl_dot(pairs):
     """sum over (v, g) pairs of <v, g> as a device float64 scalar.
 
     v: 2-D row-strided float32 view of a preconditioned gradient;
-    g: the matching .grad viewed with the same 2-D shape (contiguous).
+    g: the matching .grad (any memory layout, e.g. channels_last conv weights).
     """
     v0 = pairs[0][0]
     if _lib.use_native(v0):
@@ -99,7 +116,7 @@ def kl_dot(pairs):
         return vg
     vg = torch.zeros((), dtype=torch.float64)
     for v, g in pairs:
-        vg += (v * g).sum().double()
+        vg += (v.reshape(g.shape) * g).sum().double()
     return vg
 
 
@@ -124,7 +141,5 @@ def apply_gradients(pairs, vg=None, lr=0.0, kl_clip=None):
         return
     nu = kl_scale(vg, lr, kl_clip) if use_clip else None
     for v, g in pairs:
-        if nu is None:
-            g.copy_(v)
-        else:
-            g.copy_(nu * v)
+        v = v.reshape(g.shape)
+        g.copy_(v if nu is None else nu * v)

@@ -81,7 +81,7 @@ class KFAC(optim.Optimizer):
                  grad_worker_fraction=0.25, factor_dtype=None, precompute_outer_eigen=True,
                  use_eigen_decomp=True, skip_layers=[], verbose=False,
                  bucket_cap_mb=64.0, symmetry_aware_comm=True, eigen_solver='auto',
-                 profile=False):
+                 profile=False, use_hip_graphs=True):
         if not 0.0 <= lr:
             raise ValueError('Invalid learning rate: {}'.format(lr))
         if not 0.0 < factor_decay <= 1:
@@ -144,6 +144,11 @@ class KFAC(optim.Optimizer):
         self.workers_assigned = False
         self.plan = None
         self.timer = PhaseTimer(enabled=profile)
+        self.use_hip_graphs = use_hip_graphs
+        self._graph = None
+        self._graph_sig = None
+        self._graph_scale = None
+        self._graph_warm = False
 
         comm.init_comm_backend()
         size = comm.backend.size()
@@ -367,16 +372,80 @@ class KFAC(optim.Optimizer):
             if self.comm_method in (CommMethod.COMM_OPT, CommMethod.HYBRID_OPT):
                 with t('inverse_comm'):
                     self.broadcast_inverses()
-        with t('precondition'):
-            self.compute_preconditioned_gradients(damping=p['damping'])
-        if self.comm_method in (CommMethod.MEM_OPT, CommMethod.HYBRID_OPT):
-            with t('grad_comm'):
-                self.broadcast_gradients()
-        with t('update'):
-            scale = None if p['kl_clip'] is None else self._compute_grad_scale()
-            self.update_gradients(scale)
+        if self._graph_eligible():
+            with t('precondition'):
+                self._graph_replay()
+        else:
+            with t('precondition'):
+                self.compute_preconditioned_gradients(damping=p['damping'])
+            if self.comm_method in (CommMethod.MEM_OPT, CommMethod.HYBRID_OPT):
+                with t('grad_comm'):
+                    self.broadcast_gradients()
+            with t('update'):
+                scale = None if p['kl_clip'] is None else self._compute_grad_scale()
+                self.update_gradients(scale)
         p['step'] += 1
         return loss
+
+    # ------------------------------------------------------------ hipGraphs
+    def _precondition_and_apply(self):
+        p = self.param_groups[0]
+        self.compute_preconditioned_gradients(damping=p['damping'])
+        scale = None if p['kl_clip'] is None else self._compute_grad_scale()
+        self.update_gradients(scale)
+        return scale
+
+    def _graph_eligible(self):
+        """The steady-state tail (precondition -> KL dot -> apply) is captured
+        into one hipGraph when it contains no collective (single rank or
+        COMM_OPT) and runs on a GPU."""
+        if not self.use_hip_graphs or self.plan is None or not self.layers:
+            return False
+        if not self.layers[0].module.weight.is_cuda:
+            return False
+        return comm.backend.size() == 1 or self.comm_method == CommMethod.COMM_OPT
+
+    def _graph_signature(self):
+        p = self.param_groups[0]
+        ptrs = []
+        for layer in self.layers:
+            w = layer._get_weight_grad()
+            ptrs.append(None if w is None else (w.data_ptr(), tuple(w.stride())))
+            if layer.has_bias:
+                b = layer._get_bias_grad()
+                ptrs.append(None if b is None else b.data_ptr())
+            for k in ('QA', 'QG', 'dGdA', 'dA', 'dG', 'A_inv', 'G_inv'):
+                v = layer.state.get(k)
+                if v is not None:
+                    ptrs.append(v.data_ptr())
+        return (tuple(ptrs), p['lr'], p['kl_clip'], p['damping'])
+
+    def _graph_replay(self):
+        sig = self._graph_signature()
+        if self._graph is not None and sig == self._graph_sig:
+            self._graph.replay()
+            return
+        if not self._graph_warm or sig != self._graph_sig:
+            # eager run doubles as the capture warm-up (allocator / library handles)
+            self._graph = None
+            self._graph_sig = sig
+            self._graph_warm = True
+            self._precondition_and_apply()
+            return
+        try:
+            g = torch.cuda.CUDAGraph()
+            # the captured ops read .grad; run them on a clean copy of the
+            # current grads after capture (capture itself does not execute)
+            with torch.cuda.graph(g):
+                self._graph_scale = self._precondition_and_apply()
+            self._graph = g
+            self._graph.replay()
+        except Exception as e:  # pragma: no cover - depends on the HIP runtime
+            warnings.warn('hipGraph capture of the K-FAC step failed ({}); running eagerly'
+                          .format(e))
+            self.use_hip_graphs = False
+            self._graph = None
+            self._precondition_and_apply()
 
     def allreduce_factors(self):
         if comm.backend.size() == 1:

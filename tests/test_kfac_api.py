@@ -1,0 +1,211 @@
+"""KFAC public API behaviour on CPU (SURVEY.md Appendix A contract)."""
+import copy
+import warnings
+
+import pytest
+import torch
+import torch.nn as nn
+
+import distributed_kfac_pytorch_amd as kfac
+from distributed_kfac_pytorch_amd.models import resnet_cifar, resnet, LSTMModel
+from tests._oracle_common import SmallNet, build_case, run_steps
+
+
+def _step(model, pre, x, y):
+    model.zero_grad()
+    nn.functional.cross_entropy(model(x), y).backward()
+    pre.step()
+
+
+def test_registration_counts():
+    assert len(kfac.KFAC(resnet_cifar.resnet20()).layers) == 20
+    assert len(kfac.KFAC(resnet_cifar.resnet32()).layers) == 32
+    assert len(kfac.KFAC(resnet.resnet50()).layers) == 54
+
+
+def test_skip_layers():
+    m = resnet_cifar.resnet20()
+    assert len(kfac.KFAC(m, skip_layers='linear').layers) == 19
+    assert len(kfac.KFAC(resnet_cifar.resnet20(), skip_layers=['Conv2d']).layers) == 1
+    # skipping a container class stops recursion into it
+    assert len(kfac.KFAC(resnet_cifar.resnet20(), skip_layers=['sequential']).layers) == 2
+
+
+def test_embedding_must_be_skipped():
+    m = nn.Sequential(nn.Embedding(10, 4), nn.Linear(4, 2))
+    with pytest.raises(ValueError):
+        kfac.KFAC(m)
+    assert len(kfac.KFAC(m, skip_layers=['embedding']).layers) == 1
+
+
+def test_torch_lstmcell_rejected_and_kfac_lstm_registered():
+    with pytest.raises(TypeError):
+        kfac.KFAC(nn.Sequential(nn.LSTMCell(4, 4)), skip_layers=[])
+    lm = LSTMModel(50, 8, 8, 2, dropout=0.0)
+    pre = kfac.KFAC(lm, skip_layers=['embedding'])
+    # 2 layers x (ih, hh) LinearMulti + decoder Linear
+    assert len(pre.layers) == 5
+    names = [type(l).__name__ for l in pre.layers]
+    assert names.count('LinearMultiLayer') == 4
+
+
+def test_frozen_module_not_registered():
+    m = SmallNet()
+    for p in m.c2.parameters():
+        p.requires_grad_(False)
+    assert len(kfac.KFAC(m).layers) == 4
+
+
+def test_invalid_arguments():
+    m = SmallNet()
+    for kw in [dict(lr=-1), dict(factor_decay=0), dict(factor_decay=1.5), dict(damping=0),
+               dict(kl_clip=0), dict(factor_update_freq=0), dict(inv_update_freq=0),
+               dict(assignment_strategy='x')]:
+        with pytest.raises(ValueError):
+            kfac.KFAC(m, **kw)
+    with pytest.warns(UserWarning):
+        kfac.KFAC(m, factor_update_freq=3, inv_update_freq=10)
+
+
+def test_compute_factor_in_hook_bit_identical():
+    cfg = {'seed': 0, 'batch': 6, 'steps': 3}
+    outs = []
+    for in_hook in (False, True):
+        model, data = build_case(cfg)
+        pre = kfac.KFAC(model, factor_update_freq=1, inv_update_freq=2,
+                        compute_factor_in_hook=in_hook)
+        outs.append(run_steps(model, pre, data, cfg['steps']))
+    for a, b in zip(outs[0][0], outs[1][0]):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize('kw', [dict(precompute_outer_eigen=False), dict(use_eigen_decomp=False),
+                                dict(kl_clip=None), dict(factor_dtype=torch.float64),
+                                dict(inv_dtype=torch.float64), dict(accumulate_data=True)])
+def test_variants_run_and_change_grads(kw):
+    model, data = build_case({'seed': 0, 'batch': 6, 'steps': 3})
+    ref = copy.deepcopy(model)
+    pre = kfac.KFAC(model, factor_update_freq=1, inv_update_freq=1, **kw)
+    grads, _ = run_steps(model, pre, data, 3)
+    model.zero_grad()
+    nn.functional.cross_entropy(ref(data[0][0]), data[0][1]).backward()
+    plain = [p.grad for p in ref.parameters()]
+    assert all(torch.isfinite(g).all() for g in grads[0])
+    assert any(not torch.allclose(a, b) for a, b in zip(grads[0], plain))
+
+
+def test_state_dict_layout_and_roundtrip():
+    model, data = build_case({'seed': 0, 'batch': 6, 'steps': 3})
+    pre = kfac.KFAC(model, factor_update_freq=1, inv_update_freq=2)
+    sched = torch.optim.lr_scheduler.LambdaLR(pre, lambda e: 1.0)
+    run_steps(model, pre, data, 3)
+    sd = pre.state_dict()
+    assert set(sd) == {'state', 'param_groups', 'layers'}
+    g = sd['param_groups'][0]
+    for key in ('damping', 'factor_decay', 'factor_update_freq', 'inv_update_freq', 'kl_clip',
+                'lr', 'step', 'initial_lr'):
+        assert key in g
+    assert g['step'] == 3
+    assert all(set(l) == {'A', 'G'} for l in sd['layers'])
+    sd_inv = pre.state_dict(include_layer_inverses=True)
+    assert {'QA', 'QG', 'dGdA'} <= set(sd_inv['layers'][0])
+    model2, _ = build_case({'seed': 1, 'batch': 6, 'steps': 1})
+    pre2 = kfac.KFAC(model2, factor_update_freq=1, inv_update_freq=2)
+    pre2.load_state_dict(copy.deepcopy(sd))
+    assert pre2.param_groups[0]['step'] == 3
+    for a, b in zip(pre.layers, pre2.layers):
+        assert torch.equal(a.state['A'], b.state['A'])
+        assert torch.allclose(a.state['dGdA'], b.state['dGdA'])
+    bad = copy.deepcopy(sd)
+    bad['layers'] = bad['layers'][:-1]
+    with pytest.raises(ValueError):
+        pre2.load_state_dict(bad)
+    legacy = copy.deepcopy(sd)
+    legacy['layers'] = [{'A_factor': l['A'], 'G_factor': l['G']} for l in legacy['layers']]
+    pre2.load_state_dict(legacy)
+
+
+def test_checkpoint_file_roundtrip(tmp_path):
+    model, data = build_case({'seed': 0, 'batch': 6, 'steps': 2})
+    pre = kfac.KFAC(model, factor_update_freq=1, inv_update_freq=2)
+    sched = kfac.KFACParamScheduler(pre, damping_alpha=0.5, damping_schedule=[1])
+    run_steps(model, pre, data, 2)
+    path = tmp_path / 'ckpt.pt'
+    torch.save({'preconditioner': pre.state_dict(), 'schedulers': [sched.state_dict()]}, path)
+    blob = torch.load(path, weights_only=False)
+    pre.load_state_dict(blob['preconditioner'])
+    sched.load_state_dict(blob['schedulers'][0])
+
+
+def test_mem_opt_inverses_not_saved():
+    model, data = build_case({'seed': 0, 'batch': 6, 'steps': 1})
+    pre = kfac.KFAC(model, comm_method=kfac.CommMethod.MEM_OPT, factor_update_freq=1,
+                    inv_update_freq=1)
+    run_steps(model, pre, data, 1)
+    with pytest.warns(UserWarning):
+        sd = pre.state_dict(include_layer_inverses=True)
+    assert all(set(l) == {'A', 'G'} for l in sd['layers'])
+
+
+def test_param_scheduler():
+    pre = kfac.KFAC(SmallNet(), damping=0.01, factor_update_freq=10, inv_update_freq=100)
+    s = kfac.KFACParamScheduler(pre, damping_alpha=0.5, damping_schedule=[2, 4],
+                                update_freq_alpha=2, update_freq_schedule=[3])
+    s.step()  # 1
+    assert pre.param_groups[0]['damping'] == 0.01
+    s.step()  # 2
+    assert pre.param_groups[0]['damping'] == 0.005
+    s.step()  # 3
+    assert pre.param_groups[0]['factor_update_freq'] == 20
+    assert pre.param_groups[0]['inv_update_freq'] == 200
+    s.step(10)
+    assert pre.param_groups[0]['damping'] == 0.0025
+    sd = s.state_dict()
+    assert set(sd) == {'damping_base', 'damping_alpha', 'damping_schedule',
+                       'factor_update_freq_base', 'inv_update_freq_base', 'update_freq_alpha',
+                       'update_freq_schedule', '_step'}
+    s2 = kfac.KFACParamScheduler(pre)
+    s2.load_state_dict(sd)
+    assert s2._step == 10
+
+
+def test_shared_module_requires_accumulate():
+    lm = LSTMModel(20, 8, 8, 1, dropout=0.0, tie_weights=True)
+    pre = kfac.KFAC(lm, skip_layers=['embedding', 'linear'])
+    with pytest.raises(ValueError):
+        with warnings.catch_warnings():
+            warnings.simplefilter('ignore')
+            pre.register_shared_module(lm.decoder, lm.encoder)
+    pre2 = kfac.KFAC(lm, skip_layers=['embedding', 'linear'], accumulate_data=True)
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        pre2.register_shared_module(lm.decoder, lm.encoder, reverse_hooks=True)
+    assert len(pre2.layers) == 3
+
+
+def test_memory_usage_and_repr():
+    model, data = build_case({'seed': 0, 'batch': 6, 'steps': 1})
+    pre = kfac.KFAC(model, factor_update_freq=1, inv_update_freq=1)
+    run_steps(model, pre, data, 1)
+    assert pre.memory_usage() > 0
+    r = repr(pre)
+    assert 'registered_layers: 5' in r and 'damping' in r
+
+
+def test_inplace_relu_after_conv_hooks():
+    """Tensor hooks must see the gradient of the conv output, not of the
+    in-place ReLU that overwrote it (module full-backward hooks cannot even
+    run here: they forbid the in-place op)."""
+    torch.manual_seed(0)
+    conv = nn.Conv2d(3, 4, 3)
+    lin = nn.Linear(4 * 36, 2)
+    m = nn.Sequential(conv, nn.ReLU(inplace=True), nn.Flatten(), lin)
+    pre = kfac.KFAC(m, factor_update_freq=1, inv_update_freq=1)
+    x = torch.randn(2, 3, 8, 8)
+    y = torch.tensor([0, 1])
+    nn.functional.cross_entropy(m(x), y).backward()
+    out = conv(x)
+    out.retain_grad()
+    nn.functional.cross_entropy(lin(torch.relu(out).flatten(1)), y).backward()
+    assert torch.allclose(pre.layers[0].g_outputs[0], out.grad)
