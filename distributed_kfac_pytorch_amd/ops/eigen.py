@@ -75,6 +75,12 @@ def _library_eigh(mats, clip, n_workers=4):
     n > 192 (profiles/r1_eigh_concurrency.json; saturates at 4 = the HW queue
     count per process).  The caller's stream is ordered before and after."""
     dev = mats[0].device
+    if n_workers <= 1:
+        outs = []
+        for A in mats:
+            d, Q = torch.linalg.eigh(A)
+            outs.append((Q.contiguous(), d if clip is None else torch.clamp(d, min=clip)))
+        return outs
     cur = torch.cuda.current_stream(dev)
     k = min(n_workers, len(mats))
     pool = _side_streams(dev, k)
@@ -118,14 +124,15 @@ def symeig_many(mats, clip=0.0, solver='auto'):
             outs.append((Q, d))
         return outs
     small = [i for i, A in enumerate(mats)
-             if A.shape[0] <= SMALL_N and solver in ('auto', 'jacobi')]
+             if A.shape[0] <= SMALL_N and solver in ('auto', 'jacobi', 'serial')]
     large = [i for i in range(len(mats)) if i not in set(small)]
     outs = [None] * len(mats)
     if small:
         for i, r in zip(small, _jacobi_small([mats[i] for i in small], clip)):
             outs[i] = r
     if large:
-        for i, r in zip(large, _library_eigh([mats[i] for i in large], clip)):
+        workers = 1 if solver == 'serial' else 4
+        for i, r in zip(large, _library_eigh([mats[i] for i in large], clip, workers)):
             outs[i] = r
     return outs
 

@@ -70,7 +70,9 @@ def test_gpu_bf16_autocast_step_finite():
 
 
 def test_gpu_state_dict_roundtrip():
-    _, _, pre = _run('cuda')
+    # 3 steps with inv_update_freq=2: the last step recomputes the inverses
+    # from the final factors, which is what load_state_dict recomputes too
+    _, _, pre = _run('cuda', steps=3)
     sd = pre.state_dict(include_layer_inverses=True)
     model2 = SmallNet().cuda()
     pre2 = kfac.KFAC(model2, factor_update_freq=1, inv_update_freq=2, lr=0.05, damping=0.003)
