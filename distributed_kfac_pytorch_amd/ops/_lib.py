@@ -52,6 +52,8 @@ _SIGS = {
     'kfac_hadamard': [c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_f, c_int, c_vp],
     'kfac_eig_jacobi_small': [ctypes.POINTER(EigRecord), c_int, c_int, c_f, c_int, c_f, c_vp],
     'kfac_max_small_eig_n': [],
+    'kfac_syevd_batched': [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp],
+    'kfac_stedc': [c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
 }
 
 

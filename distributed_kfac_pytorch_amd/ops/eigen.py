@@ -3,9 +3,10 @@
 GPU path (MI355X):
   * n <= 192: every such factor of the step is solved by ONE launch of the
     batched LDS Jacobi kernel (csrc/eig_jacobi.hip), one workgroup per matrix.
-  * larger n: rocSOLVER through torch.linalg.eigh, issued on a small pool of
-    side streams so independent latency-bound solves overlap (each call is
-    dominated by serial panel steps at these sizes: profiles/r1_probe_baseline.json).
+  * larger n: grouped by size class, each class in ONE strided-batched
+    divide-and-conquer call (csrc/eig_library.hip); classes run concurrently
+    on a pool of side streams (each solve is dominated by serial panel steps
+    at these sizes: profiles/r1_rocsolver_variants.log).
 CPU path: torch.linalg.eigh (the reference semantics, kfac/layers/utils.py:45-74).
 
 Results: ascending eigenvalues clipped at `clip` (reference default 0.0),
@@ -68,45 +69,78 @@ def _thread_pool(k):
     return _pool
 
 
-def _library_eigh(mats, clip, n_workers=4):
-    """rocSOLVER syevd calls are host-latency bound (panel steps with host
-    round trips), so they are spread over a pool of host threads, each with
-    its own HIP stream: measured 1739 -> 610 ms for ResNet-50's 82 factors of
-    n > 192 (profiles/r1_eigh_concurrency.json; saturates at 4 = the HW queue
-    count per process).  The caller's stream is ordered before and after."""
+def _syevd_class(mats, clip, stream):
+    """Every matrix of one size n in ONE strided-batched divide-and-conquer
+    call (csrc/eig_library.hip) on `stream`."""
+    n = mats[0].shape[0]
     dev = mats[0].device
+    with torch.cuda.stream(stream):
+        A = torch.stack(mats) if len(mats) > 1 else mats[0].clone().unsqueeze(0)
+        b = A.shape[0]
+        D = torch.empty(b, n, dtype=torch.float32, device=dev)
+        E = torch.empty(b, n, dtype=torch.float32, device=dev)
+        info = torch.empty(b, dtype=torch.int32, device=dev)
+        _lib.check(_lib.lib().kfac_syevd_batched(_lib.ptr(A), n, b, _lib.ptr(D), _lib.ptr(E),
+                                                  _lib.ptr(info), _lib.c_vp(stream.cuda_stream)),
+                   'kfac_syevd_batched')
+        # column-major eigenvector k == row k of the row-major view
+        Q = A.transpose(1, 2).contiguous()
+        if clip is not None:
+            D.clamp_(min=clip)
+    return [(Q[i], D[i]) for i in range(b)]
+
+
+def _library_eigh(mats, clip, n_workers=4):
+    """Large factors, grouped by size class, one batched call per class; the
+    classes run concurrently on a pool of host threads, each with its own HIP
+    stream (the tridiagonal reduction is panel-latency bound, so independent
+    classes overlap well; 4 = the HW queue count per process).  The caller's
+    stream is ordered before and after."""
+    dev = mats[0].device
+    classes = {}
+    for i, A in enumerate(mats):
+        classes.setdefault(A.shape[0], []).append(i)
+    order = sorted(classes, key=lambda n: -n)
+    outs = [None] * len(mats)
     if n_workers <= 1:
-        outs = []
-        for A in mats:
-            d, Q = torch.linalg.eigh(A)
-            outs.append((Q.contiguous(), d if clip is None else torch.clamp(d, min=clip)))
+        cur = torch.cuda.current_stream(dev)
+        for n in order:
+            idx = classes[n]
+            for i, r in zip(idx, _syevd_class([mats[i] for i in idx], clip, cur)):
+                outs[i] = r
         return outs
     cur = torch.cuda.current_stream(dev)
-    k = min(n_workers, len(mats))
+    k = min(n_workers, len(order))
     pool = _side_streams(dev, k)
     for s in pool:
         s.wait_stream(cur)
-    order = sorted(range(len(mats)), key=lambda i: -mats[i].shape[0])
-    outs = [None] * len(mats)
+    # greedy LPT of the classes over the workers (cost ~ n^3, batch nearly free)
+    load = [0.0] * k
+    assign = [[] for _ in range(k)]
+    for n in order:
+        j = min(range(k), key=lambda w: load[w])
+        assign[j].append(n)
+        load[j] += float(n) ** 3 * (1.0 + 0.3 * (len(classes[n]) - 1))
 
     def work(j):
-        s = pool[j]
         torch.cuda.set_device(dev)
-        with torch.cuda.stream(s):
-            for i in order[j::k]:
-                d, Q = torch.linalg.eigh(mats[i])
-                Q = Q.contiguous()
-                if clip is not None:
-                    d = torch.clamp(d, min=clip)
-                outs[i] = (Q, d)
+        res = []
+        for n in assign[j]:
+            idx = classes[n]
+            res.append((idx, _syevd_class([mats[i] for i in idx], clip, pool[j])))
+        return res
 
-    list(_thread_pool(k).map(work, range(k)))
-    for j, s in enumerate(pool):
+    for res in _thread_pool(k).map(work, range(k)):
+        for idx, rs in res:
+            for i, r in zip(idx, rs):
+                outs[i] = r
+    for j, s in enumerate(pool[:k]):
         cur.wait_stream(s)
-        for i in order[j::k]:
-            mats[i].record_stream(s)
-            outs[i][0].record_stream(cur)
-            outs[i][1].record_stream(cur)
+        for n in assign[j]:
+            for i in classes[n]:
+                mats[i].record_stream(s)
+                outs[i][0].record_stream(cur)
+                outs[i][1].record_stream(cur)
     return outs
 
 

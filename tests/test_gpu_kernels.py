@@ -162,6 +162,26 @@ def test_symeig_large_path():
     assert resid < 1e-4
 
 
+@pytest.mark.parametrize('solver', ['auto', 'serial'])
+def test_symeig_size_classes(solver):
+    """Several factors per size class (strided batch) + several classes
+    (concurrent streams); order and per-matrix results must be preserved."""
+    torch.manual_seed(8)
+    mats = []
+    for n in (300, 256, 300, 520, 256, 300, 193):
+        X = torch.randn(n, n + 7, device=DEV)
+        mats.append(X @ X.t() / (n + 7) - 0.01 * torch.eye(n, device=DEV))
+    outs = eigen.symeig_many(mats, clip=0.0, solver=solver)
+    torch.cuda.synchronize()
+    for A, (Q, d) in zip(mats, outs):
+        assert Q.shape == A.shape and Q.is_contiguous()
+        d_ref = torch.linalg.eigvalsh(A.double())
+        assert torch.allclose(d.double(), d_ref.clamp(min=0), atol=1e-4)
+        dd = torch.linalg.eigvalsh(A.double()).float()   # unclipped for the residual
+        resid = (A @ Q - Q * dd).norm() / A.norm()
+        assert resid < 1e-4, resid
+
+
 def test_outer_recip_and_hadamard():
     torch.manual_seed(8)
     dG = torch.rand(37, device=DEV)
