@@ -38,6 +38,7 @@ from . import comm
 from . import layers as kfac_layers
 from .ops import precond as precond_ops
 from .ops import eigen as eigen_ops
+from .ops import precond_fused
 from .parallel.plan import ExecutionPlan
 from .parallel import collectives
 from .utils import distribution
@@ -81,7 +82,8 @@ class KFAC(optim.Optimizer):
                  grad_worker_fraction=0.25, factor_dtype=None, precompute_outer_eigen=True,
                  use_eigen_decomp=True, skip_layers=[], verbose=False,
                  bucket_cap_mb=64.0, symmetry_aware_comm=True, eigen_solver='auto',
-                 profile=False, use_hip_graphs=True):
+                 profile=False, use_hip_graphs=True, precond_precision='fp32',
+                 fused_precondition=True):
         if not 0.0 <= lr:
             raise ValueError('Invalid learning rate: {}'.format(lr))
         if not 0.0 < factor_decay <= 1:
@@ -145,6 +147,13 @@ class KFAC(optim.Optimizer):
         self.plan = None
         self.timer = PhaseTimer(enabled=profile)
         self.use_hip_graphs = use_hip_graphs
+        if precond_precision not in precond_fused.PRECISIONS:
+            raise ValueError('precond_precision must be one of {}'.format(
+                sorted(precond_fused.PRECISIONS)))
+        self.precond_precision = precond_precision
+        self.fused_precondition = fused_precondition
+        self.fused = None
+        self._fused_kl = None
         self._graph = None
         self._graph_sig = None
         self._graph_scale = None
@@ -244,6 +253,7 @@ class KFAC(optim.Optimizer):
             self.compute_inverses(damping=self.param_groups[0]['damping'])
             if self.comm_method in (CommMethod.COMM_OPT, CommMethod.HYBRID_OPT):
                 self.broadcast_inverses()
+            self._eigendata_updated()
 
     # ---------------------------------------------------------- registration
     def _layer_kwargs(self):
@@ -372,6 +382,7 @@ class KFAC(optim.Optimizer):
             if self.comm_method in (CommMethod.COMM_OPT, CommMethod.HYBRID_OPT):
                 with t('inverse_comm'):
                     self.broadcast_inverses()
+            self._eigendata_updated()
         if self._graph_eligible():
             with t('precondition'):
                 self._graph_replay()
@@ -508,10 +519,35 @@ class KFAC(optim.Optimizer):
             layer.update_A_factor(alpha=alpha)
             layer.update_G_factor(alpha=alpha)
 
+    def _eigendata_updated(self):
+        """New eigendata is in place: refresh the fused kernels' operand copies."""
+        if self.fused is not None:
+            self.fused.refresh_eigen()
+
+    def _build_fused(self):
+        """The grouped MFMA preconditioning chain (ops/precond_fused.py) for
+        every layer this rank preconditions, on the GPU eigen path."""
+        self.fused = None
+        if not (self.fused_precondition and self.use_eigen_decomp and self.layers and
+                self.inv_dtype == torch.float32):
+            return
+        if not self.layers[0].module.weight.is_cuda:
+            return
+        rank = comm.backend.rank()
+        mine = [l for l in self.layers if rank in l.compute_grad_ranks]
+        if mine:
+            self.fused = precond_fused.FusedPreconditioner(mine, self.precond_precision)
+            self._fused_all = len(mine) == len(self.layers)
+
     @torch.no_grad()
     def compute_preconditioned_gradients(self, damping=0.001):
+        self._fused_kl = None
+        if self.fused is not None:
+            self._fused_kl = self.fused.run(damping=damping, with_kl=self._fused_all)
+            return
         for layer in self.layers:
             layer.compute_preconditioned_gradient(damping=damping)
+
 
     def _grad_pairs(self):
         pairs = []
@@ -573,9 +609,12 @@ class KFAC(optim.Optimizer):
         self.plan = ExecutionPlan(self.layers, world, rank, a_locs, g_locs, allocator,
                                   self.use_eigen_decomp, self.precompute_outer_eigen,
                                   self.inv_dtype, build_eig_arena=True, device=device)
+        self._build_fused()
 
     def _compute_grad_scale(self):
         """sum_layers <v, g> * lr^2 -> KL-clip scale, kept on the device."""
         g = self.param_groups[0]
+        if self._fused_kl is not None:
+            return _DeviceKLScale(self._fused_kl, g['lr'], g['kl_clip'])
         vg = precond_ops.kl_dot(self._grad_pairs())
         return _DeviceKLScale(vg, g['lr'], g['kl_clip'])
