@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 import distributed_kfac_pytorch_amd as kfac  # noqa: E402
 from distributed_kfac_pytorch_amd.models import resnet  # noqa: E402
 from distributed_kfac_pytorch_amd.parallel import launch  # noqa: E402
+from distributed_kfac_pytorch_amd import graphs  # noqa: E402
 
 METRIC = 'images/sec (whole node) ResNet-50 K-FAC+SGD'
 
@@ -57,6 +58,9 @@ def parse():
     ap.add_argument('--channels-last', type=int, default=1)
     ap.add_argument('--eigen-solver', default='auto')
     ap.add_argument('--profile-phases', action='store_true')
+    ap.add_argument('--precond-precision', default='fp32', choices=['fp32', 'bf16x3'])
+    ap.add_argument('--graphs', type=int, default=-1,
+                    help='whole-step hipGraph capture (1/0); default: on for a single rank')
     return ap.parse_args()
 
 
@@ -85,14 +89,14 @@ def main():
                         inv_update_freq=args.kfac_update_freq, kl_clip=args.kl_clip, lr=base_lr,
                         comm_method=method, grad_worker_fraction=args.grad_worker_fraction,
                         distribute_layer_factors=False, eigen_solver=args.eigen_solver,
-                        profile=args.profile_phases)
+                        profile=args.profile_phases, precond_precision=args.precond_precision)
 
     B, S = args.batch_size, args.image_size
     g = torch.Generator(device=device).manual_seed(rank)
     x = torch.randn(B, 3, S, S, device=device, generator=g).to(memory_format=mf)
     y = torch.randint(0, 1000, (B,), device=device, generator=g)
 
-    def step():
+    def train_step():
         opt.zero_grad(set_to_none=False)
         with torch.autocast(device_type=device.type, dtype=torch.bfloat16):
             out = model(x)
@@ -103,8 +107,13 @@ def main():
         opt.step()
         return loss
 
+    use_graphs = args.graphs if args.graphs >= 0 else int(world == 1)
+    use_graphs = bool(use_graphs) and device.type == 'cuda' and not args.profile_phases
+    step = graphs.GraphedTrainStep(train_step, pre, [opt], enabled=use_graphs)
+
     for _ in range(args.warmup):
         step()
+    step.prepare()   # capture every graphed step kind outside the timed window
     if pre is not None:
         pre.param_groups[0]['step'] = 0
         pre.timer.reset()
@@ -150,7 +159,9 @@ def main():
                            'comm_method': args.comm_method,
                            'factor_update_freq': args.kfac_cov_update_freq,
                            'inv_update_freq': args.kfac_update_freq,
-                           'damping': args.damping, 'kl_clip': args.kl_clip},
+                           'damping': args.damping, 'kl_clip': args.kl_clip,
+                           'precond_precision': args.precond_precision},
+                       'hip_graphs': use_graphs,
                        'final_loss': round(float(loss.item()), 4)},
         }
         if phases is not None:

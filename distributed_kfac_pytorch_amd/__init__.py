@@ -17,6 +17,7 @@ from . import modules
 from . import layers
 from . import ops
 from . import parallel
+from . import graphs
 from .preconditioner import KFAC, CommMethod
 from .scheduler import KFACParamScheduler
 

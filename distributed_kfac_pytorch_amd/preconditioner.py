@@ -412,6 +412,8 @@ class KFAC(optim.Optimizer):
         COMM_OPT) and runs on a GPU."""
         if not self.use_hip_graphs or self.plan is None or not self.layers:
             return False
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            return False    # an outer whole-step graph (graphs.GraphedTrainStep) is capturing
         if not self.layers[0].module.weight.is_cuda:
             return False
         return comm.backend.size() == 1 or self.comm_method == CommMethod.COMM_OPT

@@ -1,0 +1,60 @@
+"""Whole-step hipGraph capture (graphs.GraphedTrainStep) vs eager execution."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import distributed_kfac_pytorch_amd as kfac
+from distributed_kfac_pytorch_amd import graphs
+from distributed_kfac_pytorch_amd.models import resnet_cifar
+
+pytestmark = pytest.mark.gpu
+
+
+def _train(use_graphs, steps=25, precision='fp32'):
+    torch.manual_seed(0)
+    m = resnet_cifar.resnet20().cuda().to(memory_format=torch.channels_last)
+    opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9)
+    pre = kfac.KFAC(m, factor_update_freq=2, inv_update_freq=10, lr=0.05,
+                    precond_precision=precision)
+    g = torch.Generator(device='cuda').manual_seed(3)
+    xs = [torch.randn(16, 3, 32, 32, device='cuda', generator=g) for _ in range(steps)]
+    ys = [torch.randint(0, 10, (16,), device='cuda', generator=g) for _ in range(steps)]
+    x = torch.empty_like(xs[0]).contiguous(memory_format=torch.channels_last)
+    y = torch.empty_like(ys[0])
+
+    def step_fn():
+        opt.zero_grad(set_to_none=False)
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            loss = F.cross_entropy(m(x), y)
+        loss.backward()
+        pre.step()
+        opt.step()
+        return loss
+
+    step = graphs.GraphedTrainStep(step_fn, pre, [opt], warmup=1, enabled=use_graphs)
+    losses = []
+    for i in range(steps):
+        x.copy_(xs[i])
+        y.copy_(ys[i])
+        losses.append(step().item())
+    return losses, [p.detach().clone() for p in m.parameters()], step
+
+
+def _pdiff(pa, pb):
+    num = sum((a - b).norm() ** 2 for a, b in zip(pa, pb)) ** 0.5
+    den = sum(a.norm() ** 2 for a in pa) ** 0.5
+    return (num / den).item()
+
+
+def test_graphed_matches_eager():
+    # 14 steps: eager inverse steps 0 and 10, factor steps, plain steps
+    le, pe, se = _train(False, steps=14)
+    le2, pe2, _ = _train(False, steps=14)     # run-to-run noise (f32 atomics in the SYRK)
+    lg, pg, sg = _train(True, steps=14)
+    assert sg.replays > 0 and len(sg.graphs) == 2      # 'plain' and 'factor' graphs
+    assert se.replays == 0
+    noise = _pdiff(pe, pe2)
+    diff = _pdiff(pe, pg)
+    for a, b in zip(le, lg):
+        assert abs(a - b) < 2e-2 * max(1.0, abs(a)), (le, lg)
+    assert diff < max(5e-3, 20 * noise), (diff, noise, le, lg)
