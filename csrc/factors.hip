@@ -266,6 +266,190 @@ __global__ __launch_bounds__(256) void syrk_patch_kernel(PatchArgs p) {
       }
 }
 
+// ---------------------------------------------------------------------------
+// syrk_vec: the channels-contiguous (NHWC / Linear) fast path of syrk_patch.
+// Columns are processed in the *internal* order (i, j, c) -- channel fastest,
+// which is the memory order of a channels_last activation -- so 8 consecutive
+// columns of one patch row are ONE 16-byte load.  Each thread gathers an 8x8
+// (rows x columns) block with 8 such loads, transposes it in registers and
+// stores 8 k-contiguous 16-byte rows into the [column][k] LDS image that the
+// MFMA fragments read with ds_read_b128.  The factor EMA kernel maps the
+// internal order back to the reference order (c, i, j) (factor_ema perm).
+// Requirements (checked on the host): 16-bit dtype, channel stride 1,
+// C % 8 == 0, every other stride % 8 == 0, 16-byte aligned base.
+constexpr int VBK = 64;                 // patch rows per k-step
+constexpr int VLDK = VBK + 8;           // 144-byte LDS rows: conflict-free b128 reads
+
+__device__ __forceinline__ uint32_t pack_lo(uint32_t a, uint32_t b) { return (a & 0xffffu) | (b << 16); }
+__device__ __forceinline__ uint32_t pack_hi(uint32_t a, uint32_t b) { return (a >> 16) | (b & 0xffff0000u); }
+__device__ __forceinline__ uint32_t u4get(const uint4& v, int i) {
+  return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void syrk_vec_kernel(PatchArgs p) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BT * VLDK];
+  uint16_t* sA = smem;
+  uint16_t* sB = smem + BT * VLDK;
+
+  int t = blockIdx.x, ti = 0, rem = p.ntiles;
+  while (t >= rem) { t -= rem; ++ti; --rem; }
+  const int tj = ti + t;
+  const bool diag = (ti == tj);
+
+  const long long r_begin = (long long)blockIdx.y * p.rows_per_split;
+  long long r_end = r_begin + p.rows_per_split;
+  if (r_end > p.M) r_end = p.M;
+  if (r_begin >= r_end) return;
+  const int nk = (int)((r_end - r_begin + VBK - 1) / VBK);
+
+  const uint16_t* x = (const uint16_t*)p.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  // loader role: operand (0 = A tile ti, 1 = B tile tj), row group, column chunk
+  const int op = tid >> 7;
+  const int rg = (tid & 127) >> 4;      // rows rg*8 .. rg*8+7 of the k-step
+  const int cc = tid & 15;              // columns cc*8 .. cc*8+7 of the tile
+  const bool loader = !(diag && op == 1);
+  const int gcol = (op ? tj : ti) * BT + cc * 8;
+  // chunk kind: 0 = data, 1 = bias (first column of the chunk is the ones column), 2 = zero
+  int kind = 2, coff = 0, di = 0, dj = 0;
+  if (gcol < p.kcols) {
+    const int rij = gcol / p.C, c0 = gcol - rij * p.C;
+    const int i = rij / p.kw, j = rij - i * p.kw;
+    di = i * p.dh; dj = j * p.dw;
+    coff = (int)(c0 + (long long)di * p.sh + (long long)dj * p.sw);
+    kind = 0;
+  } else if (gcol < p.ncols) {
+    kind = 1;
+  }
+  const uint16_t one = DTypeTraits<DT>::from_f32(1.0f);
+
+  uint4 blk[8];
+  auto load_step = [&](int k) {
+    const long long r0 = r_begin + (long long)k * VBK + rg * 8;
+    long long rs = r0 < r_end ? r0 : r_begin;
+    const long long ohw = (long long)p.OH * p.OW;
+    long long b = rs / ohw;
+    int rr = (int)(rs - b * ohw);
+    int oh = rr / p.OW, ow = rr - oh * p.OW;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (loader && (r0 + q) < r_end) {
+        if (kind == 0) {
+          const int h = oh * p.sth - p.ph + di, w = ow * p.stw - p.pw + dj;
+          if ((unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W) {
+            const long long off = b * p.sb + (long long)(oh * p.sth - p.ph) * p.sh +
+                                  (long long)(ow * p.stw - p.pw) * p.sw + coff;
+            v = *(const uint4*)(x + off);
+          }
+        } else if (kind == 1) {
+          v.x = one;
+        }
+      }
+      blk[q] = v;
+      if (++ow == p.OW) { ow = 0; if (++oh == p.OH) { oh = 0; ++b; } }
+    }
+  };
+  auto store_step = [&]() {
+    if (!loader) return;
+    uint16_t* dst = (op ? sB : sA) + (cc * 8) * VLDK + rg * 8;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int d = c >> 1;
+      uint4 o;
+      if (c & 1) {
+        o.x = pack_hi(u4get(blk[0], d), u4get(blk[1], d));
+        o.y = pack_hi(u4get(blk[2], d), u4get(blk[3], d));
+        o.z = pack_hi(u4get(blk[4], d), u4get(blk[5], d));
+        o.w = pack_hi(u4get(blk[6], d), u4get(blk[7], d));
+      } else {
+        o.x = pack_lo(u4get(blk[0], d), u4get(blk[1], d));
+        o.y = pack_lo(u4get(blk[2], d), u4get(blk[3], d));
+        o.z = pack_lo(u4get(blk[4], d), u4get(blk[5], d));
+        o.w = pack_lo(u4get(blk[6], d), u4get(blk[7], d));
+      }
+      *(uint4*)(dst + c * VLDK) = o;
+    }
+  };
+
+  const int wr = wave >> 1, wc = wave & 1;
+  const int lr = lane & 31, lh = lane >> 5;
+  f32x16_t acc[2][2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
+  const uint16_t* sBr = diag ? sA : sB;
+
+  load_step(0);
+  for (int k = 0; k < nk; ++k) {
+    store_step();
+    __syncthreads();
+    if (k + 1 < nk) load_step(k + 1);
+    typedef typename std::conditional<DT == KDT_BF16, bf16x8_t, f16x8_t>::type frag_t;
+#pragma unroll
+    for (int ks = 0; ks < VBK / 16; ++ks) {
+      frag_t a[2], bb[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+        a[m] = *(const frag_t*)(sA + (wr * 64 + m * 32 + lr) * VLDK + ks * 16 + lh * 8);
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+        bb[n] = *(const frag_t*)(sBr + (wc * 64 + n * 32 + lr) * VLDK + ks * 16 + lh * 8);
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          if constexpr (DT == KDT_BF16)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m], bb[n], acc[m][n], 0, 0, 0);
+          else
+            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[m], bb[n], acc[m][n], 0, 0, 0);
+        }
+    }
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int row = ti * BT + wr * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        int col = tj * BT + wc * 64 + n * 32 + lr;
+        if (row < p.ncols && col < p.ncols && (!diag || row <= col))
+          atomicAdd(p.ws + (long long)row * p.ldw + col, p.scale * acc[m][n][r]);
+      }
+}
+
+// Reference column order (c, i, j) -> internal order (i, j, c) of syrk_vec.
+__device__ __forceinline__ int perm_col(int x, int kcols, int C, int kk) {
+  if (x >= kcols || kk == 1) return x;
+  const int c = x / kk, r = x - c * kk;
+  return r * C + c;
+}
+
+// EMA with the internal->reference column permutation (see syrk_vec).
+template <int SDT>
+__global__ __launch_bounds__(256) void factor_ema_perm_kernel(
+    typename DTypeTraits<SDT>::raw_t* __restrict__ state, const float* __restrict__ ws,
+    int n, int ldw, float a1, float a2, int mode, int kcols, int C, int kk) {
+  typedef DTypeTraits<SDT> Tr;
+  const int i = blockIdx.y;
+  const int pi = perm_col(i, kcols, C, kk);
+  for (int j = blockIdx.x * 256 + threadIdx.x; j < n; j += gridDim.x * 256) {
+    const int pj = perm_col(j, kcols, C, kk);
+    const float w = (pi <= pj) ? ws[(long long)pi * ldw + pj] : ws[(long long)pj * ldw + pi];
+    const long long o = (long long)i * n + j;
+    const float s = (mode == 0) ? (Tr::to_f32(state[o]) * a1 + w) * a2 : w;
+    state[o] = Tr::from_f32(s);
+  }
+}
+
 // state = a2 * (a1 * state + ws_sym)   (mode 0: EMA, a1 = alpha/(1-alpha), a2 = 1-alpha)
 // state = ws_sym                       (mode 1: assign)
 // The workspace holds only the upper triangle; (i, j) with i > j reads ws[j][i].
@@ -377,6 +561,63 @@ KFAC_API int kfac_syrk_patch(int dtype, const void* x, long long sb, long long s
   } else {
     return -1;
   }
+  return (int)hipGetLastError();
+}
+
+// Fast path entry: returns 1 when syrk_vec ran (columns in internal order),
+// 0 when the inputs do not qualify (caller falls back to kfac_syrk_patch).
+KFAC_API int kfac_syrk_vec(int dtype, const void* x, long long sb, long long sc, long long sh,
+                           long long sw, int B, int C, int H, int W, int kh, int kw, int sth,
+                           int stw, int ph, int pw, int dh, int dw, int has_bias, float scale,
+                           float* ws, int ldw, int max_blocks, hipStream_t stream) {
+  if (!(dtype == KDT_BF16 || dtype == KDT_F16)) return 0;
+  if (sc != 1 || (C % 8) || (sb % 8) || (H > 1 && (sh % 8)) || (W > 1 && (sw % 8)) ||
+      (((uintptr_t)x) & 15))
+    return 0;
+  PatchArgs p;
+  p.x = x; p.sb = sb; p.sc = sc; p.sh = sh; p.sw = sw;
+  p.B = B; p.C = C; p.H = H; p.W = W;
+  p.kh = kh; p.kw = kw; p.sth = sth; p.stw = stw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
+  p.OH = (H + 2 * ph - dh * (kh - 1) - 1) / sth + 1;
+  p.OW = (W + 2 * pw - dw * (kw - 1) - 1) / stw + 1;
+  p.kcols = C * kh * kw;
+  p.ncols = p.kcols + (has_bias ? 1 : 0);
+  p.M = (long long)B * p.OH * p.OW;
+  p.ntiles = (p.ncols + BT - 1) / BT;
+  p.scale = scale; p.ws = ws; p.ldw = ldw;
+  if (p.M <= 0 || p.OH <= 0 || p.OW <= 0) return 1;
+  const int tiles = p.ntiles * (p.ntiles + 1) / 2;
+  if (max_blocks <= 0) max_blocks = 2048;
+  long long ksteps = (p.M + VBK - 1) / VBK;
+  long long splits = (max_blocks + tiles - 1) / tiles;
+  if (splits < 1) splits = 1;
+  if (splits > ksteps) splits = ksteps;
+  long long steps_per = (ksteps + splits - 1) / splits;
+  p.rows_per_split = steps_per * VBK;
+  splits = (p.M + p.rows_per_split - 1) / p.rows_per_split;
+  dim3 grid(tiles, (unsigned)splits), block(256);
+  if (dtype == KDT_BF16)
+    hipLaunchKernelGGL(syrk_vec_kernel<KDT_BF16>, grid, block, 0, stream, p);
+  else
+    hipLaunchKernelGGL(syrk_vec_kernel<KDT_F16>, grid, block, 0, stream, p);
+  int err = (int)hipGetLastError();
+  return err ? -err : 1;
+}
+
+KFAC_API int kfac_factor_ema_perm(int sdtype, void* state, const float* ws, int n, int ldw,
+                                  float alpha, int mode, int kcols, int C, int kk,
+                                  hipStream_t stream) {
+  float a1 = 0.f, a2 = 1.f;
+  if (mode == 0) { a1 = alpha / (1.f - alpha); a2 = 1.f - alpha; }
+  dim3 grid((n + 255) / 256 < 8 ? (n + 255) / 256 : 8, n), block(256);
+  if (sdtype == KDT_F32)
+    hipLaunchKernelGGL(factor_ema_perm_kernel<KDT_F32>, grid, block, 0, stream, (float*)state, ws, n, ldw, a1, a2, mode, kcols, C, kk);
+  else if (sdtype == KDT_BF16)
+    hipLaunchKernelGGL(factor_ema_perm_kernel<KDT_BF16>, grid, block, 0, stream, (uint16_t*)state, ws, n, ldw, a1, a2, mode, kcols, C, kk);
+  else if (sdtype == KDT_F16)
+    hipLaunchKernelGGL(factor_ema_perm_kernel<KDT_F16>, grid, block, 0, stream, (uint16_t*)state, ws, n, ldw, a1, a2, mode, kcols, C, kk);
+  else
+    return -1;
   return (int)hipGetLastError();
 }
 

@@ -44,6 +44,11 @@ _SIGS = {
                         c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_vp, c_int,
                         c_int, c_vp],
     'kfac_factor_ema': [c_int, c_vp, c_vp, c_int, c_int, c_f, c_int, c_vp],
+    'kfac_syrk_vec': [c_int, c_vp, c_ll, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_int, c_int,
+                      c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_vp, c_int,
+                      c_int, c_vp],
+    'kfac_factor_ema_perm': [c_int, c_vp, c_vp, c_int, c_int, c_f, c_int, c_int, c_int, c_int,
+                             c_vp],
     'kfac_triu_pack': [c_int, c_vp, c_vp, c_int, c_vp],
     'kfac_triu_unpack': [c_int, c_vp, c_vp, c_int, c_f, c_vp],
     'kfac_grouped_kl_dot': [ctypes.POINTER(MatRecord), c_int, c_vp, c_vp],

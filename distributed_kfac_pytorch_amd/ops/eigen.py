@@ -83,11 +83,26 @@ def _syevd_class(mats, clip, stream):
         _lib.check(_lib.lib().kfac_syevd_batched(_lib.ptr(A), n, b, _lib.ptr(D), _lib.ptr(E),
                                                   _lib.ptr(info), _lib.c_vp(stream.cuda_stream)),
                    'kfac_syevd_batched')
+        _INFOS.append(info)
         # column-major eigenvector k == row k of the row-major view
         Q = A.transpose(1, 2).contiguous()
         if clip is not None:
             D.clamp_(min=clip)
     return [(Q[i], D[i]) for i in range(b)]
+
+
+_INFOS = []
+
+
+def check_solver_status():
+    """Host-side check of every divide-and-conquer call issued since the last
+    check (info != 0 -> the solver did not converge).  Syncs; call once per
+    inverse step, not in the hot path."""
+    global _INFOS
+    infos, _INFOS = _INFOS, []
+    bad = [int(i.abs().max().item()) for i in infos if (i != 0).any().item()]
+    if bad:
+        raise RuntimeError('symmetric eigensolver failed to converge (info={})'.format(bad))
 
 
 def _library_eigh(mats, clip, n_workers=4):

@@ -60,11 +60,46 @@ def linear_source(a2d, has_bias):
     return FactorSource(x4, POINTWISE, has_bias, 1.0)
 
 
-def accumulate_sources(sources, ws):
-    """ws (n x n f32, zeroed) += sum_s scale_s * P_s^T P_s  (upper triangle only)."""
+def _vec_eligible(s):
+    """Mirror of kfac_syrk_vec's checks (channel-contiguous 16-bit data)."""
+    x = s.x
+    if x.dtype not in (torch.bfloat16, torch.float16):
+        return False
+    sb, sc, sh, sw = x.stride()
+    _, C, H, W = x.shape
+    return (sc == 1 and C % 8 == 0 and sb % 8 == 0 and (H == 1 or sh % 8 == 0) and
+            (W == 1 or sw % 8 == 0) and x.data_ptr() % 16 == 0)
+
+
+def accumulate_sources(sources, ws, allow_vec=True):
+    """ws (n x n f32, zeroed) += sum_s scale_s * P_s^T P_s  (upper triangle only).
+
+    Returns None when ws is in the reference column order (c, kh, kw), or
+    (kcols, C, kh*kw) when the channels-contiguous fast path filled it in the
+    internal order (kh, kw, c) -- `kfac_factor_ema_perm` maps it back."""
     L = _lib.lib()
     stream = _lib.stream(ws.device)
     n = ws.shape[0]
+    if allow_vec and all(_vec_eligible(s) for s in sources):
+        order = None
+        for s in sources:
+            x = s.x
+            B, C, H, W = x.shape
+            sb, sc, sh, sw = x.stride()
+            g = s.geom
+            if s.ncols != n:
+                raise ValueError('factor source has {} columns, workspace {}'.format(s.ncols, n))
+            r = L.kfac_syrk_vec(_lib.DTYPE_CODE[x.dtype], _lib.ptr(x), sb, sc, sh, sw, B, C, H, W,
+                                g.kh, g.kw, g.sh, g.sw, g.ph, g.pw, g.dh, g.dw, int(s.has_bias),
+                                s.scale, _lib.ptr(ws), ws.stride(0), 0, stream)
+            if r != 1:
+                raise RuntimeError('kfac_syrk_vec failed ({})'.format(r))
+            kk = g.kh * g.kw
+            o = (C * kk, C, kk)
+            if order is not None and order != o:
+                raise ValueError('factor sources disagree on the patch geometry')
+            order = o
+        return None if order[2] == 1 else order
     for s in sources:
         x = s.x
         if x.dtype not in (torch.float32, torch.bfloat16, torch.float16):
@@ -80,6 +115,21 @@ def accumulate_sources(sources, ws):
             _lib.DTYPE_CODE[x.dtype], _lib.ptr(x), sb, sc, sh, sw, B, C, H, W,
             g.kh, g.kw, g.sh, g.sw, g.ph, g.pw, g.dh, g.dw, int(s.has_bias), s.scale,
             _lib.ptr(ws), ws.stride(0), 0, stream), 'kfac_syrk_patch')
+    return None
+
+
+def _ema(state, ws, n, alpha, mode, order):
+    L = _lib.lib()
+    dev = ws.device
+    if order is None:
+        _lib.check(L.kfac_factor_ema(_lib.DTYPE_CODE[state.dtype], _lib.ptr(state), _lib.ptr(ws),
+                                     n, n, float(alpha), mode, _lib.stream(dev)),
+                   'kfac_factor_ema')
+    else:
+        kcols, C, kk = order
+        _lib.check(L.kfac_factor_ema_perm(_lib.DTYPE_CODE[state.dtype], _lib.ptr(state),
+                                          _lib.ptr(ws), n, n, float(alpha), mode, kcols, C, kk,
+                                          _lib.stream(dev)), 'kfac_factor_ema_perm')
 
 
 def update_factor(state, sources, alpha, out_dtype):
@@ -98,10 +148,8 @@ def update_factor(state, sources, alpha, out_dtype):
         return state
     ws = _lib.workspace(dev, n * n).view(n, n)
     ws.zero_()
-    accumulate_sources(sources, ws)
-    L = _lib.lib()
-    _lib.check(L.kfac_factor_ema(_lib.DTYPE_CODE[state.dtype], _lib.ptr(state), _lib.ptr(ws), n,
-                                 n, float(alpha), 0, _lib.stream(dev)), 'kfac_factor_ema')
+    order = accumulate_sources(sources, ws)
+    _ema(state, ws, n, alpha, 0, order)
     return state
 
 
@@ -111,8 +159,7 @@ def compute_cov(sources, out_dtype=torch.float32):
     dev = sources[0].x.device
     ws = _lib.workspace(dev, n * n).view(n, n)
     ws.zero_()
-    accumulate_sources(sources, ws)
+    order = accumulate_sources(sources, ws)
     out = torch.empty(n, n, dtype=out_dtype, device=dev)
-    _lib.check(_lib.lib().kfac_factor_ema(_lib.DTYPE_CODE[out_dtype], _lib.ptr(out), _lib.ptr(ws),
-                                          n, n, 0.0, 1, _lib.stream(dev)), 'kfac_factor_ema')
+    _ema(out, ws, n, 0.0, 1, order)
     return out

@@ -143,6 +143,8 @@ class KFAC(optim.Optimizer):
         self.bucket_cap_mb = bucket_cap_mb
         self.symmetry_aware_comm = symmetry_aware_comm
         self.eigen_solver = eigen_solver
+        # host-checks the eigensolver status once per inverse step (one sync)
+        self.check_solver = True
         self.workers_assigned = False
         self.plan = None
         self.timer = PhaseTimer(enabled=profile)
@@ -506,6 +508,8 @@ class KFAC(optim.Optimizer):
         mats = [l.state[w].to(torch.float32) for l, w in jobs]
         if self.use_eigen_decomp:
             results = eigen_ops.symeig_many(mats, clip=0.0, solver=self.eigen_solver)
+            if self.check_solver:
+                eigen_ops.check_solver_status()
             results = [(Q.to(l.inv_dtype), d.to(l.inv_dtype))
                        for (l, _), (Q, d) in zip(jobs, results)]
         else:

@@ -1,0 +1,85 @@
+"""Summarise a rocprofv3 kernel trace restricted to the bench's timed window.
+
+    python scripts/prof_window.py <kernel_trace.csv> [steps]
+
+The bench (KFAC_PROFILE_MARKER=1) launches torch.cuda._sleep just before the
+timed window; every dispatch after it is attributed to a category and the
+per-step GPU time is printed (busy time and sum of kernel durations).
+"""
+import collections
+import csv
+import sys
+
+
+def category(name):
+    n = name
+    if 'pgemm_kernel' in n:
+        return 'kfac: precondition GEMM chain'
+    if 'gather_grad' in n or 'grouped_apply' in n or 'grouped_kl' in n:
+        return 'kfac: grad gather / KL / apply'
+    if 'split_copy' in n:
+        return 'kfac: eigendata split (inverse step)'
+    if 'syrk_patch' in n or 'factor_ema' in n:
+        return 'kfac: factor SYRK + EMA'
+    if 'jacobi' in n:
+        return 'kfac: small-n Jacobi eigensolver'
+    if 'rocsolver' in n or 'rocblas' in n or n.startswith('Cijk'):
+        return 'rocSOLVER/rocBLAS (large-n eigensolver)'
+    if 'triu' in n:
+        return 'kfac: triu pack/unpack'
+    if 'BatchNorm' in n or 'bn_' in n.lower():
+        return 'model: batchnorm'
+    if 'conv' in n.lower() or 'ck::' in n or 'igemm' in n.lower():
+        return 'model: conv (MIOpen/CK)'
+    if 'elementwise' in n or 'vectorized' in n or 'reduce' in n.lower():
+        return 'model/optim: elementwise'
+    return 'other'
+
+
+def main():
+    path = sys.argv[1]
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda r: int(r['Start_Timestamp']))
+    start = None
+    for r in rows:
+        if 'sleep' in r['Kernel_Name'].lower() or 'spin' in r['Kernel_Name'].lower():
+            start = int(r['Start_Timestamp'])
+    if start is None:
+        print('marker kernel not found; using the whole trace')
+        start = int(rows[0]['Start_Timestamp'])
+    win = [r for r in rows if int(r['Start_Timestamp']) > start]
+    tot = collections.Counter()
+    cnt = collections.Counter()
+    names = collections.defaultdict(collections.Counter)
+    for r in win:
+        d = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e6
+        c = category(r['Kernel_Name'])
+        tot[c] += d
+        cnt[c] += 1
+        names[c][r['Kernel_Name'][:90]] += d
+    span = (int(win[-1]['End_Timestamp']) - int(win[0]['Start_Timestamp'])) / 1e6
+    # busy time = union of kernel intervals
+    iv = sorted((int(r['Start_Timestamp']), int(r['End_Timestamp'])) for r in win)
+    busy, cs, ce = 0, iv[0][0], iv[0][1]
+    for s, e in iv[1:]:
+        if s > ce:
+            busy += ce - cs
+            cs, ce = s, e
+        else:
+            ce = max(ce, e)
+    busy += ce - cs
+    print('window: %d dispatches, span %.2f ms, GPU busy %.2f ms, %d steps -> %.3f ms/step busy'
+          % (len(win), span, busy / 1e6, steps, busy / 1e6 / steps))
+    print('%-44s %10s %8s %10s' % ('category', 'ms total', 'calls', 'ms/step'))
+    for c, v in tot.most_common():
+        print('%-44s %10.2f %8d %10.3f' % (c, v, cnt[c], v / steps))
+    print()
+    for c, v in tot.most_common(6):
+        print('[%s]' % c)
+        for n, d in names[c].most_common(4):
+            print('   %9.2f ms  %s' % (d, n))
+
+
+if __name__ == '__main__':
+    main()

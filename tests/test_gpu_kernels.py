@@ -33,6 +33,12 @@ def _cov_patches_ref(x, k, s, p, d, bias):
     (5, 12, 12, 3, 1, 2, 2, True),
     (3, 20, 20, 7, 2, 3, 1, False),
     (64, 7, 7, 3, 1, 1, 1, False),    # ncols 576 -> several 128 tiles
+    # channel counts % 8 == 0: the NHWC 16-bit inputs take the vectorised
+    # syrk_vec path (internal (kh, kw, c) order, permuted back by the EMA)
+    (16, 9, 9, 3, 2, 1, 1, True),
+    (24, 10, 12, 3, 1, 2, 2, True),
+    (136, 6, 6, 3, 1, 1, 1, True),    # ncols 1225: 10 tiles, bias chunk
+    (48, 14, 14, 1, 2, 0, 1, False),
 ])
 def test_syrk_patch_matches_unfold(dtype, layout, geom):
     C, H, W, k, s, p, d, bias = geom
@@ -43,13 +49,21 @@ def test_syrk_patch_matches_unfold(dtype, layout, geom):
     ref = _cov_patches_ref(x.float(), k, s, p, d, bias)
     src = factors.FactorSource(x, factors.Geometry(k, k, s, s, p, p, d, d), bias, 1.0)
     n = src.ncols
-    ws = torch.zeros(n, n, device=DEV)
-    factors.accumulate_sources([src], ws)
-    got = torch.triu(ws).double()
-    want = torch.triu(ref)
+    got = factors.compute_cov([src], torch.float32).double()
+    want = ref
+    assert torch.equal(got, got.t())
     tol = 1e-4 if dtype == torch.float32 else 2e-3
     err = (got - want).abs().max().item() / max(1.0, want.abs().max().item())
     assert err < tol, err
+
+
+def test_syrk_vec_path_is_taken():
+    x = torch.randn(2, 16, 5, 5, device=DEV).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    src = factors.FactorSource(x, factors.Geometry(3, 3, 1, 1, 1, 1, 1, 1), True, 1.0)
+    assert factors._vec_eligible(src)
+    ws = torch.zeros(src.ncols, src.ncols, device=DEV)
+    assert factors.accumulate_sources([src], ws) == (144, 16, 9)
 
 
 @pytest.mark.parametrize('rows', [1, 37, 1000, 70000])
