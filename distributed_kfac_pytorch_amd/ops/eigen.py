@@ -12,6 +12,8 @@ CPU path: torch.linalg.eigh (the reference semantics, kfac/layers/utils.py:45-74
 Results: ascending eigenvalues clipped at `clip` (reference default 0.0),
 Q row-major contiguous with eigenvector k in column k.
 """
+import os
+
 import torch
 
 from . import _lib
@@ -19,6 +21,7 @@ from . import _lib
 __all__ = ['symeig_many', 'inverse_many', 'SMALL_N']
 
 SMALL_N = 192
+SPLIT_N = 1 << 30   # never split: batched big classes beat concurrent singles (r1_eigh_split.log)
 _streams = {}
 
 
@@ -105,45 +108,66 @@ def check_solver_status():
         raise RuntimeError('symmetric eigensolver failed to converge (info={})'.format(bad))
 
 
-def _library_eigh(mats, clip, n_workers=4):
-    """Large factors, grouped by size class, one batched call per class; the
-    classes run concurrently on a pool of host threads, each with its own HIP
-    stream (the tridiagonal reduction is panel-latency bound, so independent
-    classes overlap well; 4 = the HW queue count per process).  The caller's
-    stream is ordered before and after."""
-    dev = mats[0].device
+def eigh_workers():
+    """Concurrent solver streams; each needs a HW queue to really overlap, so
+    the default follows GPU_MAX_HW_QUEUES (HIP's default 4)."""
+    env = os.environ.get('KFAC_EIGH_WORKERS')
+    if env:
+        return max(1, int(env))
+    return max(1, min(16, int(os.environ.get('GPU_MAX_HW_QUEUES', '4'))))
+
+
+def _jobs(mats):
+    """Size classes; large classes are split into single-matrix jobs (a
+    strided batch of big matrices is nearly serial: r1_rocsolver_variants.log
+    n=4608 x3 228 ms vs 124 ms for one), small ones stay batched."""
     classes = {}
     for i, A in enumerate(mats):
         classes.setdefault(A.shape[0], []).append(i)
-    order = sorted(classes, key=lambda n: -n)
+    jobs = []
+    for n, idx in classes.items():
+        if n >= SPLIT_N:
+            jobs += [[i] for i in idx]
+        else:
+            jobs.append(idx)
+    jobs.sort(key=lambda j: -(mats[j[0]].shape[0] ** 3) * (1.0 + 0.3 * (len(j) - 1)))
+    return jobs
+
+
+def _library_eigh(mats, clip, n_workers=None):
+    """Large factors as divide-and-conquer jobs (one strided batch per small
+    size class, one call per big matrix) spread over `n_workers` host threads,
+    each with its own HIP stream: the tridiagonal reduction is panel-latency
+    bound, so independent jobs overlap almost perfectly as long as each stream
+    has its own hardware queue.  The caller's stream is ordered before and
+    after."""
+    if n_workers is None:
+        n_workers = eigh_workers()
+    dev = mats[0].device
+    jobs = _jobs(mats)
     outs = [None] * len(mats)
     if n_workers <= 1:
         cur = torch.cuda.current_stream(dev)
-        for n in order:
-            idx = classes[n]
+        for idx in jobs:
             for i, r in zip(idx, _syevd_class([mats[i] for i in idx], clip, cur)):
                 outs[i] = r
         return outs
     cur = torch.cuda.current_stream(dev)
-    k = min(n_workers, len(order))
+    k = min(n_workers, len(jobs))
     pool = _side_streams(dev, k)
     for s in pool:
         s.wait_stream(cur)
-    # greedy LPT of the classes over the workers (cost ~ n^3, batch nearly free)
+    # greedy LPT of the jobs over the workers (cost ~ n^3, a batch nearly free)
     load = [0.0] * k
     assign = [[] for _ in range(k)]
-    for n in order:
+    for idx in jobs:
         j = min(range(k), key=lambda w: load[w])
-        assign[j].append(n)
-        load[j] += float(n) ** 3 * (1.0 + 0.3 * (len(classes[n]) - 1))
+        assign[j].append(idx)
+        load[j] += float(mats[idx[0]].shape[0]) ** 3 * (1.0 + 0.3 * (len(idx) - 1))
 
     def work(j):
         torch.cuda.set_device(dev)
-        res = []
-        for n in assign[j]:
-            idx = classes[n]
-            res.append((idx, _syevd_class([mats[i] for i in idx], clip, pool[j])))
-        return res
+        return [(idx, _syevd_class([mats[i] for i in idx], clip, pool[j])) for idx in assign[j]]
 
     for res in _thread_pool(k).map(work, range(k)):
         for idx, rs in res:
@@ -151,8 +175,8 @@ def _library_eigh(mats, clip, n_workers=4):
                 outs[i] = r
     for j, s in enumerate(pool[:k]):
         cur.wait_stream(s)
-        for n in assign[j]:
-            for i in classes[n]:
+        for idx in assign[j]:
+            for i in idx:
                 mats[i].record_stream(s)
                 outs[i][0].record_stream(cur)
                 outs[i][1].record_stream(cur)
@@ -180,7 +204,7 @@ def symeig_many(mats, clip=0.0, solver='auto'):
         for i, r in zip(small, _jacobi_small([mats[i] for i in small], clip)):
             outs[i] = r
     if large:
-        workers = 1 if solver == 'serial' else 4
+        workers = 1 if solver == 'serial' else None
         for i, r in zip(large, _library_eigh([mats[i] for i in large], clip, workers)):
             outs[i] = r
     return outs
