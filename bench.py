@@ -35,6 +35,7 @@ import distributed_kfac_pytorch_amd as kfac  # noqa: E402
 from distributed_kfac_pytorch_amd.models import resnet  # noqa: E402
 from distributed_kfac_pytorch_amd.parallel import launch  # noqa: E402
 from distributed_kfac_pytorch_amd import graphs  # noqa: E402
+from distributed_kfac_pytorch_amd.parallel import grad_sync as grad_sync_mod  # noqa: E402
 
 METRIC = 'images/sec (whole node) ResNet-50 K-FAC+SGD'
 
@@ -63,8 +64,10 @@ def parse():
     ap.add_argument('--precond-precision', default='bf16x3', choices=['fp32', 'bf16x3'],
                     help='fused preconditioning GEMM precision (library default: fp32; '
                          'bf16x3 = split-bf16 MFMA, ~1e-5 relative error)')
-    ap.add_argument('--graphs', type=int, default=-1,
-                    help='whole-step hipGraph capture (1/0); default: on for a single rank')
+    ap.add_argument('--graphs', type=int, default=1,
+                    help='hipGraph capture of the training step (1/0)')
+    ap.add_argument('--ddp', action='store_true',
+                    help='eager torch DDP instead of the graphed flat-arena all-reduce')
     return ap.parse_args()
 
 
@@ -81,7 +84,13 @@ def main():
     model = resnet.get_model(args.model).to(device)
     mf = torch.channels_last if args.channels_last else torch.contiguous_format
     model = model.to(memory_format=mf)
-    model = launch.wrap_ddp(model, device, broadcast_buffers=False)
+    use_graphs = bool(args.graphs) and device.type == 'cuda' and not args.profile_phases
+    grad_sync = None
+    if args.ddp or not use_graphs:
+        model = launch.wrap_ddp(model, device, broadcast_buffers=False)
+    elif world > 1:
+        # one flat-arena all-reduce between graph replays (parallel/grad_sync.py)
+        grad_sync = grad_sync_mod.GradientAllreduce(model)
     base_lr = 0.0125 * world
     opt = torch.optim.SGD(model.parameters(), lr=base_lr, momentum=0.9, weight_decay=5e-5)
     pre = None
@@ -93,27 +102,38 @@ def main():
                         inv_update_freq=args.kfac_update_freq, kl_clip=args.kl_clip, lr=base_lr,
                         comm_method=method, grad_worker_fraction=args.grad_worker_fraction,
                         distribute_layer_factors=False, eigen_solver=args.eigen_solver,
-                        profile=args.profile_phases, precond_precision=args.precond_precision)
+                        profile=args.profile_phases, precond_precision=args.precond_precision,
+                        compute_factor_in_hook=grad_sync is not None)
 
     B, S = args.batch_size, args.image_size
     g = torch.Generator(device=device).manual_seed(rank)
     x = torch.randn(B, 3, S, S, device=device, generator=g).to(memory_format=mf)
     y = torch.randint(0, 1000, (B,), device=device, generator=g)
 
-    def train_step():
+    def forward_backward():
         opt.zero_grad(set_to_none=False)
         with torch.autocast(device_type=device.type, dtype=torch.bfloat16):
             out = model(x)
             loss = F.cross_entropy(out, y, label_smoothing=0.1)
         loss.backward()
+        return loss
+
+    def update():
         if pre is not None:
             pre.step()
         opt.step()
+
+    def train_step():
+        loss = forward_backward()
+        update()
         return loss
 
-    use_graphs = args.graphs if args.graphs >= 0 else int(world == 1)
-    use_graphs = bool(use_graphs) and device.type == 'cuda' and not args.profile_phases
-    step = graphs.GraphedTrainStep(train_step, pre, [opt], enabled=use_graphs)
+    if grad_sync is not None:
+        step = graphs.GraphedTrainStep(None, pre, [opt], enabled=use_graphs,
+                                       forward_backward=forward_backward,
+                                       communicate=grad_sync, update=update)
+    else:
+        step = graphs.GraphedTrainStep(train_step, pre, [opt], enabled=use_graphs)
 
     for _ in range(args.warmup):
         step()
@@ -170,6 +190,8 @@ def main():
                            'damping': args.damping, 'kl_clip': args.kl_clip,
                            'precond_precision': args.precond_precision},
                        'hip_graphs': use_graphs,
+                       'grad_allreduce': 'ddp' if grad_sync is None and world > 1 else
+                                         ('flat-arena' if world > 1 else None),
                        'final_loss': round(float(loss.item()), 4)},
         }
         if phases is not None:

@@ -14,7 +14,7 @@
 // 16-byte loads and read back as MFMA fragments with ds_read_b128; a
 // transposed result is produced by swapping the operands (S2), never by a
 // strided epilogue.  Operand buffers are zero-padded along k to a multiple
-// of 32 by construction (ops/precond_fused.py), so the k-loop is unmasked.
+// of 64 by construction (ops/precond_fused.py), so the k-loop is unmasked.
 //
 // Precision modes:
 //   PREC_BF16X3  operands stored as bf16 (hi, lo) planes (x ~= hi + lo), three
@@ -34,9 +34,6 @@ namespace {
 enum { PREC_F32 = 0, PREC_BF16X3 = 1 };
 enum { EPI_STORE = 0, EPI_HADAMARD = 1, EPI_HADAMARD_VEC = 2, EPI_FINAL = 3 };
 
-constexpr int TM = 128, TN = 128, TK = 32;
-constexpr int LDB16 = TK + 8;   // 80-byte rows: conflict-free ds_read_b128 (guide: LDS banking)
-constexpr int LDF32 = TK + 4;   // 144-byte rows, 16-byte aligned chunk writes
 
 struct PGemm {
   const void* a_hi; const void* a_lo; long long lda;
@@ -65,129 +62,144 @@ __device__ __forceinline__ void split_bf16(float x, uint16_t& h, uint16_t& l) {
   l = f32_to_bf16_bits(x - bf16_bits_to_f32(h));
 }
 
-template <int PREC>
-__global__ __launch_bounds__(256) void pgemm_kernel(const PGemm* __restrict__ table, int count,
-                                                    double* __restrict__ kl) {
+// Tile geometry: BM x BN output tile per workgroup of WM x WN waves (each
+// wave owns a (BM/WM) x (BN/WN) sub-tile of 32x32 MFMA tiles), TK = 32 deep
+// k-steps staged through one LDS image with the next k-step's global loads in
+// flight under the MFMAs.  Two instantiations are launched per stage:
+//   big   256 x 256, 8 waves (2 x 4), 128 x 64 per wave: half the operand
+//         traffic per FLOP of the small tile -- the stage is bound by operand
+//         bandwidth (measured 5 TB/s at 128 x 128, profiles/r1_pgemm_variants.log)
+//   small 128 x 128, 4 waves (2 x 2), 64 x 64 per wave, for problems with a
+//         dimension below 256 (layers with 64..192 channels)
+constexpr int TK = 32;
+
+template <int PREC, int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void pgemm_kernel(const PGemm* __restrict__ table,
+                                                             int count, double* __restrict__ kl) {
   constexpr bool X3 = (PREC == PREC_BF16X3);
+  constexpr int NT = 64 * WM * WN;                // threads
+  constexpr int MI = BM / WM / 32, NJ = BN / WN / 32;
+  constexpr int LDB16 = TK + 8;   // 80-byte rows: conflict-free ds_read_b128 (guide: LDS banking)
+  constexpr int LDF32 = TK + 4;   // 16-byte aligned chunk writes
   // one LDS array (guide: a second __shared__ object can de-pipeline loads)
-  constexpr int LDS_BYTES = X3 ? (4 * TM * LDB16 * 2) : (2 * TM * LDF32 * 4);
+  constexpr int LDS_BYTES = X3 ? (2 * (BM + BN) * LDB16 * 2) : ((BM + BN) * LDF32 * 4);
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
 
   const int pi = find_problem(table, count, blockIdx.x);
   const PGemm& P = table[pi];
   const int local = blockIdx.x - P.tile_begin;
   const int tm = local / P.tiles_n, tn = local - tm * P.tiles_n;
-  const int m0 = tm * TM, n0 = tn * TN;
+  const int m0 = tm * BM, n0 = tn * BN;
   const int M = P.M, N = P.N;
   const int ksteps = (P.K + TK - 1) / TK;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
+  const int wr = wave / WN, wc = wave % WN;
   const int lr = lane & 31, lh = lane >> 5;
 
-  // ---- loader: 4 x 16 B per operand per thread per k-step
-  // bf16 planes: chunk c in [0,1024): plane = c>>9, row = (c & 511) >> 2, kc = c & 3 (8 elems)
-  // f32:         chunk c in [0,1024): row = c >> 3, kc = c & 7 (4 elems)
-  uint4 ra[4], rb[4];
+  // ---- loader: 16-byte chunks.  bf16 planes: per operand 2 planes x rows x 4
+  // chunks (8 elements); f32: rows x 8 chunks (4 elements)
+  constexpr int CPR = X3 ? TK / 8 : TK / 4;       // chunks per row and plane
+  constexpr int PL = X3 ? 2 : 1;                  // planes
+  constexpr int CA = PL * BM * CPR, CB = PL * BN * CPR;
+  constexpr int QA = CA / NT, QB = CB / NT;
+  static_assert(CA % NT == 0 && CB % NT == 0, "loader split");
+  constexpr int ESZ = X3 ? 2 : 4;
+  uint4 ra[QA], rb[QB];
   auto load = [&](int k0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int c = tid + 256 * q;
-      int row, kof, plane;
-      if (X3) { plane = c >> 9; row = (c & 511) >> 2; kof = (c & 3) * 8; }
-      else { plane = 0; row = c >> 3; kof = (c & 7) * 4; }
-      const int esz = X3 ? 2 : 4;
-      {
-        const int gm = m0 + row;
-        const unsigned char* base = (const unsigned char*)(plane ? P.a_lo : P.a_hi);
-        ra[q] = (gm < M) ? *(const uint4*)(base + ((long long)gm * P.lda + k0 + kof) * esz)
-                         : make_uint4(0, 0, 0, 0);
-      }
-      {
-        const int gn = n0 + row;
-        const unsigned char* base = (const unsigned char*)(plane ? P.b_lo : P.b_hi);
-        rb[q] = (gn < N) ? *(const uint4*)(base + ((long long)gn * P.ldb + k0 + kof) * esz)
-                         : make_uint4(0, 0, 0, 0);
-      }
+    for (int q = 0; q < QA; ++q) {
+      const int c = tid + NT * q;
+      const int plane = c / (BM * CPR), row = (c % (BM * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
+      const int gm = m0 + row;
+      const unsigned char* base = (const unsigned char*)(plane ? P.a_lo : P.a_hi);
+      ra[q] = (gm < M) ? *(const uint4*)(base + ((long long)gm * P.lda + k0 + kof) * ESZ)
+                       : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < QB; ++q) {
+      const int c = tid + NT * q;
+      const int plane = c / (BN * CPR), row = (c % (BN * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
+      const int gn = n0 + row;
+      const unsigned char* base = (const unsigned char*)(plane ? P.b_lo : P.b_hi);
+      rb[q] = (gn < N) ? *(const uint4*)(base + ((long long)gn * P.ldb + k0 + kof) * ESZ)
+                       : make_uint4(0, 0, 0, 0);
     }
   };
+  // LDS image: [A hi | A lo | B hi | B lo] rows of LDB16 bf16 (X3) or [A | B] rows of LDF32 f32
   auto store = [&]() {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int c = tid + 256 * q;
-      if (X3) {
-        const int plane = c >> 9, row = (c & 511) >> 2, kof = (c & 3) * 8;
-        uint16_t* sAp = (uint16_t*)smem + (plane * TM) * LDB16;            // A hi | A lo
-        uint16_t* sBp = (uint16_t*)smem + (2 * TM + plane * TM) * LDB16;   // B hi | B lo
-        *(uint4*)(sAp + row * LDB16 + kof) = ra[q];
-        *(uint4*)(sBp + row * LDB16 + kof) = rb[q];
-      } else {
-        const int row = c >> 3, kof = (c & 7) * 4;
-        float* sA = (float*)smem;
-        float* sB = (float*)smem + TM * LDF32;
-        *(uint4*)(sA + row * LDF32 + kof) = ra[q];
-        *(uint4*)(sB + row * LDF32 + kof) = rb[q];
-      }
+    for (int q = 0; q < QA; ++q) {
+      const int c = tid + NT * q;
+      const int plane = c / (BM * CPR), row = (c % (BM * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
+      if (X3) *(uint4*)((uint16_t*)smem + (plane * BM + row) * LDB16 + kof) = ra[q];
+      else *(uint4*)((float*)smem + row * LDF32 + kof) = ra[q];
+    }
+#pragma unroll
+    for (int q = 0; q < QB; ++q) {
+      const int c = tid + NT * q;
+      const int plane = c / (BN * CPR), row = (c % (BN * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
+      if (X3) *(uint4*)((uint16_t*)smem + (2 * BM + plane * BN + row) * LDB16 + kof) = rb[q];
+      else *(uint4*)((float*)smem + (BM + row) * LDF32 + kof) = rb[q];
     }
   };
 
-  f32x16_t acc[2][2];
+  f32x16_t acc[MI][NJ];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  const int arow0 = wr * (BM / WM), brow0 = wc * (BN / WN);
   load(0);
   for (int ks = 0; ks < ksteps; ++ks) {
     store();
     __syncthreads();
-    if (ks + 1 < ksteps) load((ks + 1) * TK);
+    if (ks + 1 < ksteps) load((ks + 1) * TK);   // global loads in flight under the MFMAs
     if constexpr (X3) {
       const uint16_t* sAh = (const uint16_t*)smem;
-      const uint16_t* sAl = sAh + TM * LDB16;
-      const uint16_t* sBh = sAh + 2 * TM * LDB16;
-      const uint16_t* sBl = sAh + 3 * TM * LDB16;
+      const uint16_t* sAl = sAh + BM * LDB16;
+      const uint16_t* sBh = sAh + 2 * BM * LDB16;
+      const uint16_t* sBl = sBh + BN * LDB16;
 #pragma unroll
       for (int kk = 0; kk < TK / 16; ++kk) {
-        bf16x8_t ah[2], al[2], bh[2], bl[2];
+        bf16x8_t bh[NJ], bl[NJ];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int off = (wr * 64 + i * 32 + lr) * LDB16 + kk * 16 + lh * 8;
-          ah[i] = *(const bf16x8_t*)(sAh + off);
-          al[i] = *(const bf16x8_t*)(sAl + off);
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int off = (wc * 64 + j * 32 + lr) * LDB16 + kk * 16 + lh * 8;
+        for (int j = 0; j < NJ; ++j) {
+          const int off = (brow0 + j * 32 + lr) * LDB16 + kk * 16 + lh * 8;
           bh[j] = *(const bf16x8_t*)(sBh + off);
           bl[j] = *(const bf16x8_t*)(sBl + off);
         }
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < MI; ++i) {
+          const int off = (arow0 + i * 32 + lr) * LDB16 + kk * 16 + lh * 8;
+          const bf16x8_t ah = *(const bf16x8_t*)(sAh + off);
+          const bf16x8_t al = *(const bf16x8_t*)(sAl + off);
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < NJ; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[j], acc[i][j], 0, 0, 0);
           }
+        }
       }
     } else {
       const float* sA = (const float*)smem;
-      const float* sB = sA + TM * LDF32;
+      const float* sB = sA + BM * LDF32;
 #pragma unroll
       for (int kk = 0; kk < TK / 2; ++kk) {
-        float a[2], b[2];
+        float b[NJ];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) a[i] = sA[(wr * 64 + i * 32 + lr) * LDF32 + kk * 2 + lh];
+        for (int j = 0; j < NJ; ++j) b[j] = sB[(brow0 + j * 32 + lr) * LDF32 + kk * 2 + lh];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) b[j] = sB[(wc * 64 + j * 32 + lr) * LDF32 + kk * 2 + lh];
+        for (int i = 0; i < MI; ++i) {
+          const float a = sA[(arow0 + i * 32 + lr) * LDF32 + kk * 2 + lh];
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b[j], acc[i][j], 0, 0, 0);
+        }
       }
     }
     __syncthreads();
@@ -196,13 +208,13 @@ __global__ __launch_bounds__(256) void pgemm_kernel(const PGemm* __restrict__ ta
   // ---- epilogue (C/D map of 32x32 MFMA: row = (r&3) + 8*(r>>2) + 4*lh, col = lr)
   float kl_part = 0.f;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wr * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        const int n = n0 + wc * 64 + j * 32 + lr;
+        const int m = m0 + arow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const int n = n0 + brow0 + j * 32 + lr;
         if (m >= M || n >= N) continue;
         float v = acc[i][j][r];
         if (P.epi == EPI_HADAMARD) v *= P.dmat[(long long)m * P.ldd + n];
@@ -350,16 +362,22 @@ KFAC_API int kfac_pgemm_record_size() { return (int)sizeof(PGemm); }
 KFAC_API int kfac_gather_record_size() { return (int)sizeof(GatherJob); }
 KFAC_API int kfac_split_record_size() { return (int)sizeof(SplitJob); }
 
-KFAC_API int kfac_pgemm(int prec, const void* dev_table, int count, int total_tiles, double* kl,
-                        hipStream_t stream) {
+// tile: 0 = small (128 x 128, 256 threads), 1 = big (256 x 256, 512 threads);
+// the table (ops/precond_fused.py) holds the problems of that tile class.
+KFAC_API int kfac_pgemm(int prec, int tile, const void* dev_table, int count, int total_tiles,
+                        double* kl, hipStream_t stream) {
   if (count <= 0 || total_tiles <= 0) return 0;
   const PGemm* t = (const PGemm*)dev_table;
-  if (prec == PREC_BF16X3)
-    hipLaunchKernelGGL(pgemm_kernel<PREC_BF16X3>, dim3(total_tiles), dim3(256), 0, stream, t, count, kl);
-  else if (prec == PREC_F32)
-    hipLaunchKernelGGL(pgemm_kernel<PREC_F32>, dim3(total_tiles), dim3(256), 0, stream, t, count, kl);
-  else
+  dim3 g(total_tiles);
+  if (prec == PREC_BF16X3) {
+    if (tile) hipLaunchKernelGGL((pgemm_kernel<PREC_BF16X3, 256, 256, 2, 4>), g, dim3(512), 0, stream, t, count, kl);
+    else hipLaunchKernelGGL((pgemm_kernel<PREC_BF16X3, 128, 128, 2, 2>), g, dim3(256), 0, stream, t, count, kl);
+  } else if (prec == PREC_F32) {
+    if (tile) hipLaunchKernelGGL((pgemm_kernel<PREC_F32, 256, 256, 2, 4>), g, dim3(512), 0, stream, t, count, kl);
+    else hipLaunchKernelGGL((pgemm_kernel<PREC_F32, 128, 128, 2, 2>), g, dim3(256), 0, stream, t, count, kl);
+  } else {
     return -1;
+  }
   return (int)hipGetLastError();
 }
 

@@ -2,30 +2,38 @@
 
 On MI355X a ResNet-50 step at per-GPU batch 32 is host-launch bound when run
 eagerly: ~14 ms of Python/ATen dispatch for ~9 ms of GPU work
-(profiles/r1_graph_step_probe.log).  `GraphedTrainStep` captures the whole
-step -- forward, backward, K-FAC factor SYRKs, the fused preconditioning
-chain, the device-side KL clip and the optimizer update -- into hipGraphs and
-replays them, one graph per *step kind* (this is the MI355X replacement for a
-tracing compiler):
+(profiles/r1_graph_step_probe.log).  `GraphedTrainStep` captures the step --
+forward, backward, K-FAC factor SYRKs, the fused preconditioning chain, the
+device-side KL clip and the optimizer update -- into hipGraphs and replays
+them, one graph per *step kind* (the MI355X replacement for a tracing
+compiler):
 
-  'plain'   no factor update, no inverse update       -> replayed graph
-  'factor'  factor update (hooks + SYRK + EMA)         -> replayed graph
+  'plain'   no factor update, no inverse update       -> replayed graph(s)
+  'factor'  factor update (hooks + SYRK + EMA)         -> replayed graph(s)
   'eager'   inverse-update steps (rocSOLVER D&C with host-side work, eigendata
             broadcast) and the very first steps        -> run eagerly
 
+Two modes:
+  single-segment  `step_fn` does everything (one process): one graph per kind.
+  segmented       `forward_backward`, `communicate`, `update`: the forward +
+                  backward segment is a graph per kind; `communicate` (the
+                  data-parallel gradient all-reduce, parallel/grad_sync.py)
+                  runs eagerly between replays -- no collective is ever
+                  captured; `update` (preconditioner.step() + optimizer.step())
+                  is a graph only when it issues no collective for that kind
+                  (one rank, or K-FAC COMM_OPT plain steps), else eager.
+
 Step kinds follow the K-FAC schedule (`factor_update_freq`, `inv_update_freq`,
-reference kfac/preconditioner.py:494-514); the K-FAC step counter that the
-graph cannot advance is advanced here.  Python-level hyper-parameters baked
-into a graph (learning rates, damping, KL clip, frequencies) form the graph
-key, so a scheduler that changes them triggers a re-capture instead of a stale
+reference kfac/preconditioner.py:494-514); the K-FAC step counter that a graph
+cannot advance is advanced here.  Python-level hyper-parameters baked into a
+graph (learning rates, damping, KL clip, frequencies) are part of the graph
+key, so a scheduler that changes them triggers a re-capture, never a stale
 replay.
 
-Contract for `step_fn`: it reads its inputs from tensors whose storage does
-not change between calls (copy each batch into them), calls
-`optimizer.zero_grad(set_to_none=False)`, runs forward/backward,
-`preconditioner.step()` and `optimizer.step()`, and returns a tensor (the
-loss).  Eager fallback: `enabled=False`, a CPU device, or an exception during
-capture (warned once).
+Contract: inputs are read from tensors whose storage does not change between
+calls (copy each batch into them); `optimizer.zero_grad(set_to_none=False)`;
+the step returns a tensor (the loss).  Eager fallback: `enabled=False`, no
+GPU, or an exception during capture (warned once).
 """
 import warnings
 
@@ -35,9 +43,20 @@ __all__ = ['GraphedTrainStep']
 
 
 class GraphedTrainStep(object):
-    def __init__(self, step_fn, preconditioner=None, optimizers=(), warmup=2, enabled=True):
+    def __init__(self, step_fn=None, preconditioner=None, optimizers=(), warmup=2, enabled=True,
+                 forward_backward=None, communicate=None, update=None):
+        if step_fn is None and (forward_backward is None or update is None):
+            raise ValueError('give step_fn, or forward_backward and update')
         self.step_fn = step_fn
+        self.fb, self.comm, self.update = forward_backward, communicate, update
+        self.segmented = step_fn is None
         self.pre = preconditioner
+        if self.segmented and preconditioner is not None and \
+                not preconditioner.compute_factor_in_hook:
+            # a replayed forward/backward graph runs no Python hooks, so the
+            # factors must be computed INSIDE the captured hooks
+            raise ValueError('segmented GraphedTrainStep needs '
+                             'KFAC(compute_factor_in_hook=True)')
         self.optimizers = list(optimizers) if isinstance(optimizers, (list, tuple)) \
             else [optimizers]
         self.warmup = warmup
@@ -51,6 +70,7 @@ class GraphedTrainStep(object):
         # AccumulateGrad nodes created in warm-up live on the capture stream
         self.side = torch.cuda.Stream() if self.enabled else None
 
+    # ------------------------------------------------------------ schedule
     def _kind(self):
         pre = self.pre
         if pre is None:
@@ -62,7 +82,7 @@ class GraphedTrainStep(object):
             return 'factor'
         return 'plain'
 
-    def _key(self, kind):
+    def _key(self, seg, kind):
         hp = []
         for opt in self.optimizers:
             for g in opt.param_groups:
@@ -72,34 +92,97 @@ class GraphedTrainStep(object):
             p = self.pre.param_groups[0]
             hp.append((p['lr'], p['damping'], p['kl_clip'], p['factor_decay'],
                        p['factor_update_freq'], p['inv_update_freq']))
-        return (kind, tuple(hp))
+        return (seg, kind, tuple(hp))
 
     def _advance(self):
         if self.pre is not None:
             self.pre.param_groups[0]['step'] += 1
 
+    def _update_capturable(self, kind):
+        """update = preconditioner.step() + optimizer.step(): capturable when
+        it issues no collective (one rank, or COMM_OPT plain steps)."""
+        pre = self.pre
+        if pre is None:
+            return True
+        from . import comm
+        if comm.backend is None or comm.backend.size() == 1:
+            return True
+        from .preconditioner import CommMethod
+        return kind == 'plain' and pre.comm_method == CommMethod.COMM_OPT
+
+    # ------------------------------------------------------------ execution
     def __call__(self):
         kind = self._kind()
         if not self.enabled or kind == 'eager':
             self.eager_steps += 1
+            return self._eager()
+        if not self.segmented:
+            return self._run_segment('step', kind, self.step_fn, advances=True)
+        loss = self._run_segment('fb', kind, self.fb, advances=False)
+        if self.comm is not None:
+            self.comm()
+        if self._update_capturable(kind):
+            self._run_segment('update', kind, self.update, advances=True)
+        else:
+            self.update()
+        return loss
+
+    def _eager(self):
+        if not self.segmented:
             return self.step_fn()
-        key = self._key(kind)
+        loss = self.fb()
+        if self.comm is not None:
+            self.comm()
+        self.update()
+        return loss
+
+    def _run_segment(self, seg, kind, fn, advances):
+        key = self._key(seg, kind)
         g = self.graphs.get(key)
         if g is not None:
             g.replay()
-            self._advance()
+            if advances:
+                self._advance()
             self.replays += 1
             return self.outputs[key]
         if self._warm.get(key, 0) < self.warmup:
             self._warm[key] = self._warm.get(key, 0) + 1
-            self.eager_steps += 1
             cur = torch.cuda.current_stream()
             self.side.wait_stream(cur)
             with torch.cuda.stream(self.side):
-                out = self.step_fn()
+                out = fn()
             cur.wait_stream(self.side)
             return out
-        return self._capture(key)
+        return self._capture(key, fn, advances)
+
+    def _capture(self, key, fn, advances):
+        step0 = self.pre.param_groups[0]['step'] if self.pre is not None else None
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        try:
+            # a private memory pool per graph: segments and kinds replay in
+            # any order, so one graph's outputs must never alias another's
+            # temporaries
+            with torch.cuda.graph(g, stream=self.side):
+                out = fn()
+        except Exception as e:  # pragma: no cover - depends on the HIP runtime
+            warnings.warn('hipGraph capture of the training step failed ({}); running '
+                          'eagerly from now on'.format(e))
+            self.enabled = False
+            if self.pre is not None:
+                self.pre.param_groups[0]['step'] = step0
+            return fn()
+        if self.pre is not None:
+            # capture recorded the work without running it; a captured
+            # preconditioner.step() advanced the step counter: rewind
+            self.pre.param_groups[0]['step'] = step0
+        self.graphs[key] = g
+        self.outputs[key] = out
+        g.replay()
+        if advances:
+            self._advance()
+        self.replays += 1
+        return out
 
     def prepare(self):
         """Warm up and capture every graphed step kind now (e.g. before a timed
@@ -130,30 +213,3 @@ class GraphedTrainStep(object):
                 p['step'] = s
                 self()
         p['step'] = saved
-
-    def _capture(self, key):
-        step0 = self.pre.param_groups[0]['step'] if self.pre is not None else None
-        torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        try:
-            # a private memory pool per graph: step kinds replay in any order,
-            # so one graph's outputs must never alias another's temporaries
-            with torch.cuda.graph(g, stream=self.side):
-                out = self.step_fn()
-        except Exception as e:  # pragma: no cover - depends on the HIP runtime
-            warnings.warn('hipGraph capture of the training step failed ({}); running '
-                          'eagerly from now on'.format(e))
-            self.enabled = False
-            if self.pre is not None:
-                self.pre.param_groups[0]['step'] = step0
-            return self.step_fn()
-        if self.pre is not None:
-            # capture recorded the work without running it; the step counter
-            # was advanced by the captured preconditioner.step(): rewind
-            self.pre.param_groups[0]['step'] = step0
-        self.graphs[key] = g
-        self.outputs[key] = out
-        g.replay()
-        self._advance()
-        self.replays += 1
-        return out

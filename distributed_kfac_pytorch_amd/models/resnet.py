@@ -14,7 +14,7 @@ kernels prefer on gfx950 (measured in profiles/).
 import torch
 import torch.nn as nn
 
-__all__ = ['ResNet', 'Bottleneck', 'BasicBlock', 'resnet18', 'resnet34',
+__all__ = ['ResNet', 'Bottleneck', 'BasicBlock', 'resnet_tiny', 'resnet18', 'resnet34',
            'resnet50', 'resnet101', 'resnet152', 'get_model']
 
 
@@ -68,19 +68,20 @@ class Bottleneck(nn.Module):
 
 
 class ResNet(nn.Module):
-    def __init__(self, block, layers, num_classes=1000, zero_init_residual=False):
+    def __init__(self, block, layers, num_classes=1000, zero_init_residual=False, width=64):
         super().__init__()
-        self.inplanes = 64
-        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
-        self.bn1 = nn.BatchNorm2d(64)
+        w = width
+        self.inplanes = w
+        self.conv1 = nn.Conv2d(3, w, 7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(w)
         self.relu = nn.ReLU(inplace=True)
         self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
-        self.layer1 = self._make_layer(block, 64, layers[0])
-        self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
-        self.layer3 = self._make_layer(block, 256, layers[2], stride=2)
-        self.layer4 = self._make_layer(block, 512, layers[3], stride=2)
+        self.layer1 = self._make_layer(block, w, layers[0])
+        self.layer2 = self._make_layer(block, 2 * w, layers[1], stride=2)
+        self.layer3 = self._make_layer(block, 4 * w, layers[2], stride=2)
+        self.layer4 = self._make_layer(block, 8 * w, layers[3], stride=2)
         self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
-        self.fc = nn.Linear(512 * block.expansion, num_classes)
+        self.fc = nn.Linear(8 * w * block.expansion, num_classes)
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode='fan_out', nonlinearity='relu')
@@ -133,8 +134,15 @@ def resnet152(**kw):
     return ResNet(Bottleneck, [3, 8, 36, 3], **kw)
 
 
+def resnet_tiny(**kw):
+    """Bottleneck ResNet, one block per stage, width 8: the ResNet-50 layer
+    types at test-sized factors (CPU tests of the bench / examples)."""
+    kw.setdefault('width', 8)
+    return ResNet(Bottleneck, [1, 1, 1, 1], **kw)
+
+
 _MODELS = {'resnet18': resnet18, 'resnet34': resnet34, 'resnet50': resnet50,
-           'resnet101': resnet101, 'resnet152': resnet152}
+           'resnet101': resnet101, 'resnet152': resnet152, 'resnet_tiny': resnet_tiny}
 
 
 def get_model(name, **kw):

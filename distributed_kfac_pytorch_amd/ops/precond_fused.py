@@ -32,7 +32,18 @@ __all__ = ['FusedPreconditioner', 'PRECISIONS']
 
 PRECISIONS = {'fp32': 0, 'bf16x3': 1}
 EPI_STORE, EPI_HADAMARD, EPI_HADAMARD_VEC, EPI_FINAL = 0, 1, 2, 3
-TILE = 128
+TILE = 128        # small tile class (csrc/precond_gemm.hip)
+BIG_TILE = 256    # big tile class: half the operand traffic per FLOP
+
+
+BIG_TILES = False  # measured 2.7x slower on ResNet-50 (profiles/r1_pgemm_variants.log)
+
+
+def _tile_class(M, N):
+    """1 = 256 x 256 tiles, 0 = 128 x 128 tiles.  The chain is latency bound
+    (few tiles in flight per CU), so the small tile with 4x the tile count
+    wins; the big class stays available for experiments."""
+    return 1 if (BIG_TILES and M >= 256 and N >= 256) else 0
 
 
 class PGemmRec(ctypes.Structure):
@@ -64,7 +75,8 @@ class SplitRec(ctypes.Structure):
 
 
 def _pad32(n):
-    return (n + 31) // 32 * 32
+    """k-padding of every MFMA operand: a multiple of the kernel's TK (64)."""
+    return (n + 63) // 64 * 64
 
 
 def _cdiv(a, b):
@@ -182,15 +194,21 @@ class FusedPreconditioner(object):
                     r.c_hi, r.c_lo, r.ldc = C.hi, C.lo, C.ld
                 r.M, r.N, r.K = M, N, K
                 probs.append(r)
-            # longest k-loops first: their tiles are dispatched first
-            probs.sort(key=lambda r: -r.K)
-            tiles = 0
-            for r in probs:
-                r.tiles_n = _cdiv(r.N, TILE)
-                r.tile_begin = tiles
-                tiles += _cdiv(r.M, TILE) * r.tiles_n
-            arr = (PGemmRec * len(probs))(*probs)
-            stages.append((_upload(arr, self.device), len(probs), tiles))
+            launches = []
+            for tile, size in ((1, BIG_TILE), (0, TILE)):
+                sel = [r for r in probs if _tile_class(r.M, r.N) == tile]
+                if not sel:
+                    continue
+                # longest k-loops first: their tiles are dispatched first
+                sel.sort(key=lambda r: -r.K)
+                tiles = 0
+                for r in sel:
+                    r.tiles_n = _cdiv(r.N, size)
+                    r.tile_begin = tiles
+                    tiles += _cdiv(r.M, size) * r.tiles_n
+                arr = (PGemmRec * len(sel))(*sel)
+                launches.append((tile, _upload(arr, self.device), len(sel), tiles))
+            stages.append(launches)
         self._stage_tables = stages
 
     def refresh_eigen(self):
@@ -303,10 +321,11 @@ class FusedPreconditioner(object):
                    'kfac_gather_grad')
         if with_kl:
             self.kl.zero_()
-        for i, (table, count, tiles) in enumerate(self._stage_tables):
+        for i, launches in enumerate(self._stage_tables):
             kl = _lib.ptr(self.kl) if (with_kl and i == 3) else None
-            _lib.check(L.kfac_pgemm(self.prec, _lib.ptr(table), count, tiles, kl, stream),
-                       'kfac_pgemm')
+            for tile, table, count, tiles in launches:
+                _lib.check(L.kfac_pgemm(self.prec, tile, _lib.ptr(table), count, tiles, kl,
+                                        stream), 'kfac_pgemm')
         for b in self.bufs:
             b.layer.preconditioned_gradient = b.layer._split_pgrad(b.layer._pgrad_matrix())
         return self.kl if with_kl else None

@@ -1,0 +1,88 @@
+"""Worker bodies for the multi-process (gloo, CPU) tests in test_distributed.py.
+
+Each function runs inside one spawned rank, writes its results with
+torch.save into `out_dir`, and never raises silently (an exception in a rank
+makes torch.multiprocessing.spawn fail the test).
+"""
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def _init(rank, world, port):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    os.environ['RANK'] = str(rank)
+    os.environ['WORLD_SIZE'] = str(world)
+    os.environ['LOCAL_RANK'] = str(rank)
+    torch.set_num_threads(1)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from distributed_kfac_pytorch_amd import comm
+    comm.reset_comm_backend()
+    comm.init_comm_backend()
+
+
+def kfac_strategy(rank, world, port, out_dir, cfg):
+    """Identical data on every rank: the K-FAC result must equal world=1."""
+    _init(rank, world, port)
+    import distributed_kfac_pytorch_amd as kfac
+    from tests._oracle_common import build_case, run_steps
+    model, data = build_case({'seed': 0, 'batch': 6, 'steps': cfg['steps']})
+    method = getattr(kfac.CommMethod, cfg['method'])
+    pre = kfac.KFAC(model, factor_update_freq=1, inv_update_freq=cfg.get('inv_freq', 2),
+                    lr=0.05, damping=0.003, comm_method=method,
+                    grad_worker_fraction=cfg.get('fraction', 0.25),
+                    distribute_layer_factors=cfg.get('distribute', False),
+                    precompute_outer_eigen=cfg.get('prediv', True),
+                    use_eigen_decomp=cfg.get('eigen', True))
+    grads, factors = run_steps(model, pre, data, cfg['steps'])
+    torch.save({'grads': grads, 'factors': factors},
+               os.path.join(out_dir, 'rank{}.pt'.format(rank)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def grad_allreduce(rank, world, port, out_dir, cfg):
+    """Different data per rank; GradientAllreduce must average gradients and
+    start every rank from rank 0's parameters."""
+    _init(rank, world, port)
+    import torch.nn as nn
+    from distributed_kfac_pytorch_amd.parallel.grad_sync import GradientAllreduce
+    torch.manual_seed(100 + rank)     # deliberately different initialisation
+    model = nn.Sequential(nn.Conv2d(3, 8, 3), nn.ReLU(), nn.Flatten(), nn.Linear(8 * 6 * 6, 5))
+    model[0].to(memory_format=torch.channels_last)
+    sync = GradientAllreduce(model)
+    params0 = [p.detach().clone() for p in model.parameters()]
+    g = torch.Generator().manual_seed(rank)
+    x = torch.randn(4, 3, 8, 8, generator=g)
+    model.zero_grad(set_to_none=False)
+    model(x).square().mean().backward()
+    local = [p.grad.detach().clone() for p in model.parameters()]
+    sync()
+    avg = [p.grad.detach().clone() for p in model.parameters()]
+    views_ok = all(p.grad.data_ptr() >= sync.arenas[0].data_ptr() for p in model.parameters())
+    torch.save({'params0': params0, 'local': local, 'avg': avg, 'views_ok': views_ok},
+               os.path.join(out_dir, 'rank{}.pt'.format(rank)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def bench_cpu(rank, world, port, out_dir, cfg):
+    """bench.py's distributed path end to end on CPU/gloo (tiny model)."""
+    _init(rank, world, port)
+    import subprocess  # noqa: F401  (keeps the import surface identical to the GPU run)
+    sys.argv = ['bench.py'] + cfg['argv']
+    import runpy
+    from contextlib import redirect_stdout
+    import io
+    buf = io.StringIO()
+    with redirect_stdout(buf):
+        runpy.run_path(os.path.join(ROOT, 'bench.py'), run_name='__main__')
+    with open(os.path.join(out_dir, 'rank{}.txt'.format(rank)), 'w') as f:
+        f.write(buf.getvalue())

@@ -1,0 +1,121 @@
+"""Multi-process K-FAC on CPU with gloo (world 2 and 4), 127.0.0.1 rendezvous.
+
+Strategy equivalence: with identical data on
+every rank, COMM_OPT / MEM_OPT / HYBRID_OPT must reproduce the single-process
+preconditioned gradients and factors BIT-FOR-BIT on every rank (the reference
+achieves this once its eigenvector-contiguity bug is fixed).  Also covers the
+flat-arena gradient all-reduce used by the graphed bench and bench.py's
+distributed path end to end.
+"""
+import json
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+import distributed_kfac_pytorch_amd as kfac
+from tests import _dist_worker
+from tests._oracle_common import build_case, run_steps
+
+
+def _port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _spawn(fn, world, tmp_path, cfg):
+    mp.spawn(fn, args=(world, _port(), str(tmp_path), cfg), nprocs=world, join=True)
+
+
+def _single(cfg):
+    # the ranks run single-threaded; the BLAS reduction order (and so the last
+    # bit of every matmul) depends on the thread count
+    threads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        return _single_run(cfg)
+    finally:
+        torch.set_num_threads(threads)
+
+
+def _single_run(cfg):
+    model, data = build_case({'seed': 0, 'batch': 6, 'steps': cfg['steps']})
+    pre = kfac.KFAC(model, factor_update_freq=1, inv_update_freq=cfg.get('inv_freq', 2),
+                    lr=0.05, damping=0.003, precompute_outer_eigen=cfg.get('prediv', True),
+                    use_eigen_decomp=cfg.get('eigen', True))
+    return run_steps(model, pre, data, cfg['steps'])
+
+
+CASES = [
+    (2, {'method': 'COMM_OPT'}),
+    (2, {'method': 'MEM_OPT'}),
+    (4, {'method': 'HYBRID_OPT', 'fraction': 0.5}),
+    (4, {'method': 'HYBRID_OPT', 'fraction': 0.25}),
+    (4, {'method': 'COMM_OPT', 'prediv': False}),
+    (2, {'method': 'COMM_OPT', 'eigen': False}),
+    (4, {'method': 'MEM_OPT', 'eigen': False}),
+]
+
+
+@pytest.mark.parametrize('world,cfg', CASES,
+                         ids=['-'.join([str(w)] + ['{}={}'.format(k, v) for k, v in c.items()])
+                              for w, c in CASES])
+def test_strategy_equivalence(tmp_path, world, cfg):
+    cfg = dict(cfg, steps=4)
+    ref_grads, ref_factors = _single(cfg)
+    _spawn(_dist_worker.kfac_strategy, world, tmp_path, cfg)
+    for r in range(world):
+        res = torch.load(os.path.join(str(tmp_path), 'rank{}.pt'.format(r)), weights_only=True)
+        for step, (gs, rs) in enumerate(zip(res['grads'], ref_grads)):
+            for a, b in zip(gs, rs):
+                assert torch.equal(a, b), (r, step, (a - b).abs().max().item())
+        for (a, g), (ra, rg) in zip(res['factors'], ref_factors):
+            assert torch.equal(a, ra) and torch.equal(g, rg)
+
+
+def test_distribute_layer_factors_without_prediv(tmp_path):
+    """A and G of a layer on different ranks (reference default for COMM_OPT
+    once prediv is off): still bit-identical."""
+    cfg = {'method': 'COMM_OPT', 'prediv': False, 'distribute': True, 'steps': 3}
+    ref_grads, _ = _single(cfg)
+    _spawn(_dist_worker.kfac_strategy, 2, tmp_path, cfg)
+    for r in range(2):
+        res = torch.load(os.path.join(str(tmp_path), 'rank{}.pt'.format(r)), weights_only=True)
+        for gs, rs in zip(res['grads'], ref_grads):
+            for a, b in zip(gs, rs):
+                assert torch.equal(a, b)
+
+
+def test_gradient_allreduce(tmp_path):
+    world = 2
+    _spawn(_dist_worker.grad_allreduce, world, tmp_path, {})
+    res = [torch.load(os.path.join(str(tmp_path), 'rank{}.pt'.format(r)), weights_only=True)
+           for r in range(world)]
+    for r in range(world):
+        assert res[r]['views_ok']
+        for p, p0 in zip(res[r]['params0'], res[0]['params0']):
+            assert torch.equal(p, p0)        # broadcast from rank 0
+        for a, l0, l1 in zip(res[r]['avg'], res[0]['local'], res[1]['local']):
+            assert torch.allclose(a, (l0 + l1) / 2, atol=1e-7, rtol=1e-6)
+
+
+@pytest.mark.parametrize('method', ['comm-opt', 'hybrid-opt'])
+def test_bench_distributed_cpu(tmp_path, method):
+    """bench.py prints ONE JSON line on rank 0 with the whole-job throughput."""
+    argv = ['--gpus', '2', '--steps', '2', '--warmup', '1', '--model', 'resnet_tiny',
+            '--batch-size', '2', '--image-size', '32', '--comm-method', method,
+            '--kfac-update-freq', '2', '--kfac-cov-update-freq', '1']
+    _spawn(_dist_worker.bench_cpu, 2, tmp_path, {'argv': argv})
+    out0 = open(os.path.join(str(tmp_path), 'rank0.txt')).read().strip().splitlines()
+    out1 = open(os.path.join(str(tmp_path), 'rank1.txt')).read().strip()
+    assert out1 == ''
+    assert len(out0) == 1
+    rec = json.loads(out0[0])
+    assert rec['n_gpus'] == 2 and rec['steps'] == 2 and rec['warmup'] == 1
+    assert rec['config']['global_batch'] == 4
+    assert rec['value'] > 0 and rec['config']['parallelism'] == 'dp2'

@@ -10,12 +10,12 @@ from distributed_kfac_pytorch_amd.models import resnet_cifar
 pytestmark = pytest.mark.gpu
 
 
-def _train(use_graphs, steps=25, precision='fp32'):
+def _train(use_graphs, steps=25, precision='fp32', segmented=False):
     torch.manual_seed(0)
     m = resnet_cifar.resnet20().cuda().to(memory_format=torch.channels_last)
     opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9)
     pre = kfac.KFAC(m, factor_update_freq=2, inv_update_freq=10, lr=0.05,
-                    precond_precision=precision)
+                    precond_precision=precision, compute_factor_in_hook=segmented)
     g = torch.Generator(device='cuda').manual_seed(3)
     xs = [torch.randn(16, 3, 32, 32, device='cuda', generator=g) for _ in range(steps)]
     ys = [torch.randint(0, 10, (16,), device='cuda', generator=g) for _ in range(steps)]
@@ -31,7 +31,22 @@ def _train(use_graphs, steps=25, precision='fp32'):
         opt.step()
         return loss
 
-    step = graphs.GraphedTrainStep(step_fn, pre, [opt], warmup=1, enabled=use_graphs)
+    if segmented:
+        def fb():
+            opt.zero_grad(set_to_none=False)
+            with torch.autocast('cuda', dtype=torch.bfloat16):
+                loss = F.cross_entropy(m(x), y)
+            loss.backward()
+            return loss
+
+        def update():
+            pre.step()
+            opt.step()
+        step = graphs.GraphedTrainStep(None, pre, [opt], warmup=1, enabled=use_graphs,
+                                       forward_backward=fb, communicate=lambda: None,
+                                       update=update)
+    else:
+        step = graphs.GraphedTrainStep(step_fn, pre, [opt], warmup=1, enabled=use_graphs)
     losses = []
     for i in range(steps):
         x.copy_(xs[i])
@@ -58,3 +73,16 @@ def test_graphed_matches_eager():
     for a, b in zip(le, lg):
         assert abs(a - b) < 2e-2 * max(1.0, abs(a)), (le, lg)
     assert diff < max(5e-3, 20 * noise), (diff, noise, le, lg)
+
+
+def test_segmented_graphs_match_eager():
+    """forward/backward graph + eager communicate + update graph (the
+    multi-rank bench layout), factors computed inside the captured hooks."""
+    le, pe, _ = _train(False, steps=14, segmented=True)
+    le2, pe2, _ = _train(False, steps=14, segmented=True)
+    ls, ps, ss = _train(True, steps=14, segmented=True)
+    assert ss.replays > 0 and len(ss.graphs) == 4      # fb/update x plain/factor
+    for a, b in zip(le, ls):
+        assert abs(a - b) < 2e-2 * max(1.0, abs(a)), (le, ls)
+    noise, diff = _pdiff(pe, pe2), _pdiff(pe, ps)
+    assert diff < max(1e-2, 20 * noise), (diff, noise)
