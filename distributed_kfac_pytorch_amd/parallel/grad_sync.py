@@ -59,12 +59,10 @@ class GradientAllreduce(object):
         if self.world <= 1:
             return
         for arena in self.arenas:
-            if self.average and arena.is_cuda:
-                dist.all_reduce(arena, op=dist.ReduceOp.AVG, group=self.group)
-            else:
-                dist.all_reduce(arena, op=dist.ReduceOp.SUM, group=self.group)
-                if self.average:
-                    arena.div_(self.world)
+            # SUM + scale (ReduceOp.AVG needs ncclAvg support in the RCCL build)
+            dist.all_reduce(arena, op=dist.ReduceOp.SUM, group=self.group)
+            if self.average:
+                arena.mul_(1.0 / self.world)
 
 
 def _dense_strides(t):

@@ -1,0 +1,105 @@
+"""Train / test loops for the CNN examples (reference: examples/cnn_utils/engine.py:1-125).
+
+Per loader batch: `batches_per_allreduce` micro-batches, all but the last
+under `model.no_sync()` (DDP), optional mixed precision (bf16 autocast on the
+GPU; fp16 + GradScaler when `--fp16`), then `preconditioner.step()` between
+the gradient all-reduce and `optimizer.step()`.  Metrics stay on the device
+(examples/utils.Metric) and are reduced once per epoch.
+"""
+import contextlib
+import time
+
+import torch
+
+from examples.utils import Metric, accuracy
+
+__all__ = ['train', 'test']
+
+try:
+    from tqdm import tqdm
+except ImportError:  # pragma: no cover
+    tqdm = None
+
+
+def _autocast(args):
+    if not args.cuda:
+        return contextlib.nullcontext()
+    if getattr(args, 'fp16', False):
+        return torch.autocast('cuda', dtype=torch.float16)
+    if getattr(args, 'bf16', True):
+        return torch.autocast('cuda', dtype=torch.bfloat16)
+    return contextlib.nullcontext()
+
+
+def train(epoch, model, optimizer, preconditioner, loss_func, train_sampler, train_loader, args,
+          log_writer=None):
+    model.train()
+    train_sampler.set_epoch(epoch)
+    train_loss, train_acc = Metric('train_loss'), Metric('train_accuracy')
+    scaler = getattr(args, 'grad_scaler', None)
+    bar = None
+    if tqdm is not None and getattr(args, 'verbose', False):
+        bar = tqdm(total=len(train_loader), desc='Epoch {:3d}/{:3d}'.format(epoch, args.epochs),
+                   bar_format='{l_bar}{bar:10}{r_bar}')
+    t0 = time.time()
+    for data, target in train_loader:
+        if args.cuda:
+            data, target = data.cuda(non_blocking=True), target.cuda(non_blocking=True)
+            if getattr(args, 'channels_last', False):
+                data = data.contiguous(memory_format=torch.channels_last)
+        optimizer.zero_grad(set_to_none=False)
+        starts = list(range(0, len(data), args.batch_size))
+        for i in starts:
+            xb, yb = data[i:i + args.batch_size], target[i:i + args.batch_size]
+            sync = i == starts[-1] or not hasattr(model, 'no_sync')
+            ctx = contextlib.nullcontext() if sync else model.no_sync()
+            with ctx:
+                with _autocast(args):
+                    out = model(xb)
+                    loss = loss_func(out, yb) / len(starts)
+                with torch.no_grad():
+                    train_loss.update(loss * len(starts))
+                    train_acc.update(accuracy(out, yb))
+                if scaler is not None:
+                    scaler.scale(loss).backward()
+                else:
+                    loss.backward()
+        if preconditioner is not None:
+            if scaler is not None:
+                scaler.unscale_(optimizer)
+            preconditioner.step()
+        if scaler is not None:
+            scaler.step(optimizer)
+            scaler.update()
+        else:
+            optimizer.step()
+        if bar is not None:
+            bar.update(1)
+    if bar is not None:
+        bar.close()
+    loss_avg, acc_avg = train_loss.avg, train_acc.avg
+    if log_writer is not None:
+        log_writer.add_scalar('train/loss', loss_avg, epoch)
+        log_writer.add_scalar('train/accuracy', acc_avg, epoch)
+        log_writer.add_scalar('train/lr', optimizer.param_groups[0]['lr'], epoch)
+    return {'loss': float(loss_avg), 'accuracy': float(acc_avg), 'time': time.time() - t0}
+
+
+def test(epoch, model, loss_func, val_loader, args, log_writer=None):
+    model.eval()
+    val_loss, val_acc = Metric('val_loss'), Metric('val_accuracy')
+    with torch.no_grad():
+        for data, target in val_loader:
+            if args.cuda:
+                data, target = data.cuda(non_blocking=True), target.cuda(non_blocking=True)
+                if getattr(args, 'channels_last', False):
+                    data = data.contiguous(memory_format=torch.channels_last)
+            with _autocast(args):
+                out = model(data)
+            val_loss.update(loss_func(out.float(), target))
+            val_acc.update(accuracy(out, target))
+    loss_avg, acc_avg = val_loss.avg, val_acc.avg
+    if log_writer is not None:
+        log_writer.add_scalar('val/loss', loss_avg, epoch)
+        log_writer.add_scalar('val/accuracy', acc_avg, epoch)
+    return {'loss': float(loss_avg), 'accuracy': float(acc_avg)}
