@@ -286,18 +286,19 @@ __device__ __forceinline__ uint32_t u4get(const uint4& v, int i) {
   return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
 }
 
+// One (upper-triangular tile pair, row split) work item of syrk_vec.
 template <int DT>
-__global__ __launch_bounds__(256) void syrk_vec_kernel(PatchArgs p) {
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BT * VLDK];
+__device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int split,
+                                              uint16_t* smem) {
   uint16_t* sA = smem;
   uint16_t* sB = smem + BT * VLDK;
 
-  int t = blockIdx.x, ti = 0, rem = p.ntiles;
+  int t = tile, ti = 0, rem = p.ntiles;
   while (t >= rem) { t -= rem; ++ti; --rem; }
   const int tj = ti + t;
   const bool diag = (ti == tj);
 
-  const long long r_begin = (long long)blockIdx.y * p.rows_per_split;
+  const long long r_begin = (long long)split * p.rows_per_split;
   long long r_end = r_begin + p.rows_per_split;
   if (r_end > p.M) r_end = p.M;
   if (r_begin >= r_end) return;
@@ -426,6 +427,55 @@ __global__ __launch_bounds__(256) void syrk_vec_kernel(PatchArgs p) {
       }
 }
 
+template <int DT>
+__global__ __launch_bounds__(256) void syrk_vec_kernel(PatchArgs p) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BT * VLDK];
+  syrk_vec_tile<DT>(p, blockIdx.x, blockIdx.y, smem);
+}
+
+// Grouped form: every channels-contiguous factor of a K-FAC factor step in
+// ONE launch (each problem owns `blocks` = tile pairs x row splits blocks
+// starting at `block_begin`), so the small factors no longer run as
+// under-filled launches of their own.
+struct SyrkProblem {
+  PatchArgs p;
+  int block_begin, blocks, dtype, pad;
+};
+
+// Tables travel BY VALUE in the kernel arguments (< 4 KB), so a launch is
+// capturable into a hipGraph with its problem pointers baked in (no H2D copy).
+constexpr int MAX_SYRK_PROBLEMS = 24;
+struct SyrkBatch {
+  int count, pad[3];
+  SyrkProblem prob[MAX_SYRK_PROBLEMS];
+};
+
+template <int DT>
+__global__ __launch_bounds__(256) void syrk_vec_grouped_kernel(SyrkBatch batch) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BT * VLDK];
+  const SyrkProblem* t = batch.prob;
+  const int count = batch.count;
+  int lo = 0, hi = count - 1;
+  const int b = blockIdx.x;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (t[mid].block_begin <= b) lo = mid; else hi = mid - 1;
+  }
+  const SyrkProblem& P = t[lo];
+  const int local = b - P.block_begin;
+  const int tiles = P.p.ntiles * (P.p.ntiles + 1) / 2;
+  syrk_vec_tile<DT>(P.p, local % tiles, local / tiles, smem);
+}
+
+// Grouped EMA (with the internal->reference permutation): one block row per
+// (factor, row i).
+struct EmaJob {
+  void* state; const float* ws;
+  int n, ldw, kcols, C, kk, sdtype, row_begin, pad;
+  float a1, a2;
+  int mode, pad2;
+};
+
 // Reference column order (c, i, j) -> internal order (i, j, c) of syrk_vec.
 __device__ __forceinline__ int perm_col(int x, int kcols, int C, int kk) {
   if (x >= kcols || kk == 1) return x;
@@ -448,6 +498,42 @@ __global__ __launch_bounds__(256) void factor_ema_perm_kernel(
     const float s = (mode == 0) ? (Tr::to_f32(state[o]) * a1 + w) * a2 : w;
     state[o] = Tr::from_f32(s);
   }
+}
+
+template <int SDT>
+__device__ __forceinline__ void ema_perm_row(const EmaJob& J, int i) {
+  typedef DTypeTraits<SDT> Tr;
+  typename Tr::raw_t* state = (typename Tr::raw_t*)J.state;
+  const int pi = perm_col(i, J.kcols, J.C, J.kk);
+  for (int j = threadIdx.x; j < J.n; j += 256) {
+    const int pj = perm_col(j, J.kcols, J.C, J.kk);
+    const float w = (pi <= pj) ? J.ws[(long long)pi * J.ldw + pj] : J.ws[(long long)pj * J.ldw + pi];
+    const long long o = (long long)i * J.n + j;
+    const float v = (J.mode == 0) ? (Tr::to_f32(state[o]) * J.a1 + w) * J.a2 : w;
+    state[o] = Tr::from_f32(v);
+  }
+}
+
+constexpr int MAX_EMA_JOBS = 60;
+struct EmaBatch {
+  int count, pad[3];
+  EmaJob job[MAX_EMA_JOBS];
+};
+
+__global__ __launch_bounds__(256) void factor_ema_grouped_kernel(EmaBatch batch) {
+  const EmaJob* t = batch.job;
+  const int count = batch.count;
+  int lo = 0, hi = count - 1;
+  const int b = blockIdx.x;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (t[mid].row_begin <= b) lo = mid; else hi = mid - 1;
+  }
+  const EmaJob& J = t[lo];
+  const int i = b - J.row_begin;
+  if (J.sdtype == KDT_F32) ema_perm_row<KDT_F32>(J, i);
+  else if (J.sdtype == KDT_BF16) ema_perm_row<KDT_BF16>(J, i);
+  else ema_perm_row<KDT_F16>(J, i);
 }
 
 // state = a2 * (a1 * state + ws_sym)   (mode 0: EMA, a1 = alpha/(1-alpha), a2 = 1-alpha)
@@ -664,4 +750,91 @@ KFAC_API int kfac_triu_unpack(int dtype, const void* packed, void* a, int n, flo
   else
     return -1;
   return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------ grouped API
+KFAC_API int kfac_syrk_problem_size() { return (int)sizeof(SyrkProblem); }
+KFAC_API int kfac_ema_job_size() { return (int)sizeof(EmaJob); }
+
+// Fill the derived fields of a SyrkProblem from the user fields (host side):
+// returns the number of blocks, or 0 when the input does not qualify for the
+// channels-contiguous path.  split_rows: target patch rows per block.
+KFAC_API int kfac_syrk_problem_init(SyrkProblem* P, int block_begin, int dtype, const void* x,
+                                    long long sb,
+                                    long long sc, long long sh, long long sw, int B, int C, int H,
+                                    int W, int kh, int kw, int sth, int stw, int ph, int pw, int dh,
+                                    int dw, int has_bias, float scale, float* ws, int ldw,
+                                    long long split_rows) {
+  if (!(dtype == KDT_BF16 || dtype == KDT_F16)) return 0;
+  if (sc != 1 || (C % 8) || (sb % 8) || (H > 1 && (sh % 8)) || (W > 1 && (sw % 8)) ||
+      (((uintptr_t)x) & 15))
+    return 0;
+  PatchArgs& p = P->p;
+  p.x = x; p.sb = sb; p.sc = sc; p.sh = sh; p.sw = sw;
+  p.B = B; p.C = C; p.H = H; p.W = W;
+  p.kh = kh; p.kw = kw; p.sth = sth; p.stw = stw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
+  p.OH = (H + 2 * ph - dh * (kh - 1) - 1) / sth + 1;
+  p.OW = (W + 2 * pw - dw * (kw - 1) - 1) / stw + 1;
+  p.kcols = C * kh * kw;
+  p.ncols = p.kcols + (has_bias ? 1 : 0);
+  p.M = (long long)B * p.OH * p.OW;
+  p.ntiles = (p.ncols + BT - 1) / BT;
+  p.scale = scale; p.ws = ws; p.ldw = ldw;
+  if (p.M <= 0) return 0;
+  if (split_rows < VBK) split_rows = VBK;
+  split_rows = (split_rows + VBK - 1) / VBK * VBK;
+  long long splits = (p.M + split_rows - 1) / split_rows;
+  p.rows_per_split = (p.M + splits - 1) / splits;
+  p.rows_per_split = (p.rows_per_split + VBK - 1) / VBK * VBK;
+  splits = (p.M + p.rows_per_split - 1) / p.rows_per_split;
+  P->dtype = dtype;
+  P->block_begin = block_begin;
+  P->pad = 0;
+  P->blocks = (int)(splits * (p.ntiles * (p.ntiles + 1) / 2));
+  return P->blocks;
+}
+
+// host_table: `count` SyrkProblem records (block_begin relative to the
+// first); launched in batches of MAX_SYRK_PROBLEMS.
+KFAC_API int kfac_syrk_grouped(const void* host_table, int count, int dtype, hipStream_t stream) {
+  const SyrkProblem* t = (const SyrkProblem*)host_table;
+  for (int base = 0; base < count; base += MAX_SYRK_PROBLEMS) {
+    SyrkBatch b;
+    b.count = count - base < MAX_SYRK_PROBLEMS ? count - base : MAX_SYRK_PROBLEMS;
+    int blocks = 0;
+    for (int k = 0; k < b.count; ++k) {
+      b.prob[k] = t[base + k];
+      b.prob[k].block_begin = blocks;
+      blocks += b.prob[k].blocks;
+    }
+    if (blocks == 0) continue;
+    if (dtype == KDT_BF16)
+      hipLaunchKernelGGL(syrk_vec_grouped_kernel<KDT_BF16>, dim3(blocks), dim3(256), 0, stream, b);
+    else if (dtype == KDT_F16)
+      hipLaunchKernelGGL(syrk_vec_grouped_kernel<KDT_F16>, dim3(blocks), dim3(256), 0, stream, b);
+    else
+      return -1;
+    int err = (int)hipGetLastError();
+    if (err) return err;
+  }
+  return 0;
+}
+
+KFAC_API int kfac_ema_grouped(const void* host_table, int count, hipStream_t stream) {
+  const EmaJob* t = (const EmaJob*)host_table;
+  for (int base = 0; base < count; base += MAX_EMA_JOBS) {
+    EmaBatch b;
+    b.count = count - base < MAX_EMA_JOBS ? count - base : MAX_EMA_JOBS;
+    int rows = 0;
+    for (int k = 0; k < b.count; ++k) {
+      b.job[k] = t[base + k];
+      b.job[k].row_begin = rows;
+      rows += b.job[k].n;
+    }
+    if (rows == 0) continue;
+    hipLaunchKernelGGL(factor_ema_grouped_kernel, dim3(rows), dim3(256), 0, stream, b);
+    int err = (int)hipGetLastError();
+    if (err) return err;
+  }
+  return 0;
 }

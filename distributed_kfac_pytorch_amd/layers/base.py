@@ -381,15 +381,47 @@ class KFACLayer(object):
     def _factor_out_dtype(self, x):
         return self.factor_dtype if self.factor_dtype is not None else x.dtype
 
+    def take_factor_job(self, which):
+        """Consume the saved hook data of factor `which` ('A' or 'G') and
+        return (sources, out_dtype) for the GPU factor kernels, or None when
+        there is nothing to add.  G applies the AMP unscale / non-finite
+        filter of the reference (base.py:392-417) to the source scales."""
+        if which == 'A':
+            if len(self.a_inputs) == 0:
+                return None
+            inputs, self.a_inputs = self.a_inputs, []
+            return self._a_sources(inputs), self._factor_out_dtype(inputs[0])
+        kept, unscale = self._take_g_outputs()
+        if not kept:
+            return None
+        srcs = self._g_sources(kept)
+        for s, u in zip(srcs, unscale):
+            s.scale /= (u * u)
+        return srcs, self._factor_out_dtype(kept[0])
+
+    def _take_g_outputs(self):
+        outputs, self.g_outputs = self.g_outputs, []
+        if self.grad_scaler is None:
+            return outputs, [1.0] * len(outputs)
+        kept, unscale = [], []
+        for g, s in outputs:
+            if torch.isfinite(g).all():
+                kept.append(g)
+                unscale.append(float(s))
+        if len(kept) != len(outputs):
+            warnings.warn('Some gradients were discarded when computing G because they '
+                          'were unable to be unscaled. Note this can degrade KFAC '
+                          'performance if too many gradients are discarded.')
+        return kept, unscale
+
     def update_A_factor(self, alpha=0.95):
         if len(self.a_inputs) == 0:
             return
-        inputs, self.a_inputs = self.a_inputs, []
-        if _lib.use_native(inputs[0]):
-            self.state['A'] = factor_ops.update_factor(
-                self.state['A'], self._a_sources(inputs), alpha,
-                self._factor_out_dtype(inputs[0]))
+        if _lib.use_native(self.a_inputs[0]):
+            srcs, dtype = self.take_factor_job('A')
+            self.state['A'] = factor_ops.update_factor(self.state['A'], srcs, alpha, dtype)
             return
+        inputs, self.a_inputs = self.a_inputs, []
         if self.factor_dtype is not None:
             inputs = [x.to(self.factor_dtype) for x in inputs]
         A_new = self._get_A_factor(inputs)
@@ -398,27 +430,16 @@ class KFACLayer(object):
         lutils.update_running_avg(A_new, self.state['A'], alpha=alpha)
 
     def update_G_factor(self, alpha=0.95):
-        outputs, self.g_outputs = self.g_outputs, []
-        if self.grad_scaler is not None:
-            kept, unscale = [], []
-            for g, s in outputs:
-                if torch.isfinite(g).all():
-                    kept.append(g)
-                    unscale.append(float(s))
-            if len(kept) != len(outputs):
-                warnings.warn('Some gradients were discarded when computing G because they '
-                              'were unable to be unscaled. Note this can degrade KFAC '
-                              'performance if too many gradients are discarded.')
-        else:
-            kept, unscale = outputs, [1.0] * len(outputs)
-        if len(kept) == 0:
+        if len(self.g_outputs) == 0:
             return
-        if _lib.use_native(kept[0]):
-            srcs = self._g_sources(kept)
-            for s, u in zip(srcs, unscale):
-                s.scale /= (u * u)
-            self.state['G'] = factor_ops.update_factor(
-                self.state['G'], srcs, alpha, self._factor_out_dtype(kept[0]))
+        first = self.g_outputs[0]
+        if _lib.use_native(first[0] if isinstance(first, tuple) else first):
+            job = self.take_factor_job('G')
+            if job is not None:
+                self.state['G'] = factor_ops.update_factor(self.state['G'], job[0], alpha, job[1])
+            return
+        kept, unscale = self._take_g_outputs()
+        if len(kept) == 0:
             return
         if self.factor_dtype is not None:
             kept = [g.to(self.factor_dtype) for g in kept]

@@ -11,6 +11,7 @@ Reference math being reproduced: kfac/layers/conv.py:24-70,
 kfac/layers/linear.py:12-59, kfac/layers/utils.py:13-43,164-178.
 """
 import collections
+import ctypes
 
 import torch
 
@@ -162,4 +163,98 @@ def compute_cov(sources, out_dtype=torch.float32):
     order = accumulate_sources(sources, ws)
     out = torch.empty(n, n, dtype=out_dtype, device=dev)
     _ema(out, ws, n, 0.0, 1, order)
+    return out
+
+
+# ---------------------------------------------------------------- grouped
+class EmaJob(ctypes.Structure):
+    _fields_ = [('state', ctypes.c_void_p), ('ws', ctypes.c_void_p),
+                ('n', ctypes.c_int), ('ldw', ctypes.c_int), ('kcols', ctypes.c_int),
+                ('C', ctypes.c_int), ('kk', ctypes.c_int), ('sdtype', ctypes.c_int),
+                ('row_begin', ctypes.c_int), ('pad', ctypes.c_int),
+                ('a1', ctypes.c_float), ('a2', ctypes.c_float),
+                ('mode', ctypes.c_int), ('pad2', ctypes.c_int)]
+
+
+SPLIT_ROWS = 2048   # patch rows per block of the grouped SYRK
+
+
+def update_factors_grouped(items, alpha):
+    """Running-average update of MANY factors in a fixed number of launches.
+
+    items: list of (state_or_None, sources, out_dtype).  Returns the list of
+    updated states (new identity-initialised tensors where state was None).
+    Every factor whose sources all qualify for the channels-contiguous path
+    goes through ONE grouped SYRK launch per input dtype plus ONE grouped EMA
+    launch; the rest fall back to the per-factor path.  One memset zeroes the
+    shared f32 workspace arena.
+    """
+    if not items:
+        return []
+    L = _lib.lib()
+    dev = items[0][1][0].x.device
+    stream = _lib.stream(dev)
+    out = [None] * len(items)
+    grouped, rest = [], []
+    for k, (state, sources, out_dtype) in enumerate(items):
+        if alpha != 1 and all(_vec_eligible(s) for s in sources) and \
+                len({(s.x.dtype, s.x.shape[1], s.geom.kh * s.geom.kw) for s in sources}) == 1:
+            grouped.append(k)
+        else:
+            rest.append(k)
+    for k in rest:
+        state, sources, out_dtype = items[k]
+        out[k] = update_factor(state, sources, alpha, out_dtype)
+    if not grouped:
+        return out
+    sizes = [items[k][1][0].ncols for k in grouped]
+    total = sum(n * n for n in sizes)
+    arena = _lib.workspace(dev, total, tag='syrk_grouped')
+    arena.zero_()
+    psize = L.kfac_syrk_problem_size()
+    by_dtype = {}
+    ws_of = {}
+    off = 0
+    for k, n in zip(grouped, sizes):
+        ws_of[k] = (off, n)
+        off += n * n
+        for s in items[k][1]:
+            by_dtype.setdefault(s.x.dtype, []).append((k, s))
+    for dtype, probs in by_dtype.items():
+        raw = ctypes.create_string_buffer(psize * len(probs))
+        blocks = 0
+        for i, (k, s) in enumerate(probs):
+            x = s.x
+            B, C, H, W = x.shape
+            sb, sc, sh, sw = x.stride()
+            g = s.geom
+            woff, n = ws_of[k]
+            ws_ptr = arena.data_ptr() + 4 * woff
+            nb = L.kfac_syrk_problem_init(
+                ctypes.byref(raw, i * psize), blocks, _lib.DTYPE_CODE[dtype], _lib.ptr(x),
+                sb, sc, sh, sw, B, C, H, W, g.kh, g.kw, g.sh, g.sw, g.ph, g.pw, g.dh, g.dw,
+                int(s.has_bias), s.scale, _lib.c_vp(ws_ptr), n, SPLIT_ROWS)
+            if nb <= 0:
+                raise RuntimeError('grouped SYRK rejected an eligible source')
+            blocks += nb
+        _lib.check(L.kfac_syrk_grouped(raw, len(probs), _lib.DTYPE_CODE[dtype], stream),
+                   'kfac_syrk_grouped')
+    jobs = (EmaJob * len(grouped))()
+    a1, a2 = alpha / (1.0 - alpha), 1.0 - alpha
+    for j, k in enumerate(grouped):
+        state, sources, out_dtype = items[k]
+        n = sizes[j]
+        if state is None:
+            state = torch.eye(n, dtype=out_dtype, device=dev)
+        out[k] = state
+        s0 = sources[0]
+        kk = s0.geom.kh * s0.geom.kw
+        C = s0.x.shape[1]
+        woff, _ = ws_of[k]
+        J = jobs[j]
+        J.state, J.ws = state.data_ptr(), arena.data_ptr() + 4 * woff
+        J.n, J.ldw, J.kcols, J.C, J.kk = n, n, C * kk, C, kk
+        J.sdtype = _lib.DTYPE_CODE[state.dtype]
+        J.a1, J.a2, J.mode = a1, a2, 0
+    _lib.check(L.kfac_ema_grouped(jobs, len(grouped), stream), 'kfac_ema_grouped')
     return out

@@ -39,6 +39,7 @@ from . import layers as kfac_layers
 from .ops import precond as precond_ops
 from .ops import eigen as eigen_ops
 from .ops import precond_fused
+from .ops import factors as factor_ops
 from .parallel.plan import ExecutionPlan
 from .parallel import collectives
 from .utils import distribution
@@ -154,6 +155,8 @@ class KFAC(optim.Optimizer):
                 sorted(precond_fused.PRECISIONS)))
         self.precond_precision = precond_precision
         self.fused_precondition = fused_precondition
+        # all factors of a step in a few grouped launches (GPU)
+        self.grouped_factors = True
         self.fused = None
         self._fused_kl = None
         self._graph = None
@@ -521,6 +524,20 @@ class KFAC(optim.Optimizer):
 
     @torch.no_grad()
     def compute_factors(self, alpha=0.95):
+        """Update every layer's A and G.  On the GPU all factors of the step go
+        through a handful of grouped SYRK + EMA launches (ops/factors.py
+        update_factors_grouped) instead of ~3 launches per factor."""
+        if self.layers and self.layers[0].module.weight.is_cuda and self.grouped_factors:
+            items, refs = [], []
+            for layer in self.layers:
+                for which in ('A', 'G'):
+                    job = layer.take_factor_job(which)
+                    if job is not None:
+                        items.append((layer.state[which], job[0], job[1]))
+                        refs.append((layer, which))
+            for (layer, which), st in zip(refs, factor_ops.update_factors_grouped(items, alpha)):
+                layer.state[which] = st
+            return
         for layer in self.layers:
             layer.update_A_factor(alpha=alpha)
             layer.update_G_factor(alpha=alpha)
