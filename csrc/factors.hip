@@ -449,6 +449,7 @@ struct SyrkBatch {
   int count, pad[3];
   SyrkProblem prob[MAX_SYRK_PROBLEMS];
 };
+static_assert(sizeof(SyrkBatch) <= 4096, "kernel arguments are limited to 4 KB");
 
 template <int DT>
 __global__ __launch_bounds__(256) void syrk_vec_grouped_kernel(SyrkBatch batch) {
@@ -519,6 +520,7 @@ struct EmaBatch {
   int count, pad[3];
   EmaJob job[MAX_EMA_JOBS];
 };
+static_assert(sizeof(EmaBatch) <= 4096, "kernel arguments are limited to 4 KB");
 
 __global__ __launch_bounds__(256) void factor_ema_grouped_kernel(EmaBatch batch) {
   const EmaJob* t = batch.job;

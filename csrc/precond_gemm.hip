@@ -261,9 +261,21 @@ __device__ __forceinline__ float load_any(const void* p, long long i, int dt) {
   return f16_bits_to_f32(((const uint16_t*)p)[i]);
 }
 
+// The job table travels BY VALUE (kernel arguments): the .grad pointers are
+// baked into each launch, so a graph-captured launch and an eager one never
+// share a mutable table (with zero_grad(set_to_none=True) every eager step
+// allocates new gradients while the captured graph keeps its own).
+constexpr int MAX_GATHER = 36;   // 36 x 104 B: the batch stays under the 4 KB kernel-argument limit
+struct GatherBatch {
+  int count, pad[3];
+  GatherJob job[MAX_GATHER];
+};
+static_assert(sizeof(GatherBatch) <= 4096, "kernel arguments are limited to 4 KB");
+
 template <int PREC>
-__global__ __launch_bounds__(256) void gather_grad_kernel(const GatherJob* __restrict__ jobs,
-                                                          int count) {
+__global__ __launch_bounds__(256) void gather_grad_kernel(GatherBatch batch) {
+  const GatherJob* jobs = batch.job;
+  const int count = batch.count;
   __shared__ float tile[64][65];
   int lo = 0, hi = count - 1;
   while (lo < hi) {
@@ -381,15 +393,28 @@ KFAC_API int kfac_pgemm(int prec, int tile, const void* dev_table, int count, in
   return (int)hipGetLastError();
 }
 
-KFAC_API int kfac_gather_grad(int prec, const void* dev_jobs, int count, int total_tiles,
-                              hipStream_t stream) {
-  if (count <= 0 || total_tiles <= 0) return 0;
-  const GatherJob* j = (const GatherJob*)dev_jobs;
-  if (prec == PREC_BF16X3)
-    hipLaunchKernelGGL(gather_grad_kernel<PREC_BF16X3>, dim3(total_tiles), dim3(256), 0, stream, j, count);
-  else
-    hipLaunchKernelGGL(gather_grad_kernel<PREC_F32>, dim3(total_tiles), dim3(256), 0, stream, j, count);
-  return (int)hipGetLastError();
+// host_jobs: `count` GatherJob records (tile_begin/tiles_g filled in here).
+KFAC_API int kfac_gather_grad(int prec, const void* host_jobs, int count, hipStream_t stream) {
+  const GatherJob* t = (const GatherJob*)host_jobs;
+  for (int base = 0; base < count; base += MAX_GATHER) {
+    GatherBatch b;
+    b.count = count - base < MAX_GATHER ? count - base : MAX_GATHER;
+    int tiles = 0;
+    for (int k = 0; k < b.count; ++k) {
+      b.job[k] = t[base + k];
+      b.job[k].tiles_g = (b.job[k].nG + 63) / 64;
+      b.job[k].tile_begin = tiles;
+      tiles += ((b.job[k].nA + 63) / 64) * b.job[k].tiles_g;
+    }
+    if (tiles == 0) continue;
+    if (prec == PREC_BF16X3)
+      hipLaunchKernelGGL(gather_grad_kernel<PREC_BF16X3>, dim3(tiles), dim3(256), 0, stream, b);
+    else
+      hipLaunchKernelGGL(gather_grad_kernel<PREC_F32>, dim3(tiles), dim3(256), 0, stream, b);
+    int err = (int)hipGetLastError();
+    if (err) return err;
+  }
+  return 0;
 }
 
 KFAC_API int kfac_split_copy(int prec, const void* dev_jobs, int count, int total_tiles,

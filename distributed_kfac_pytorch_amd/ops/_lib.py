@@ -67,7 +67,7 @@ _SIGS = {
     'kfac_syevd_batched': [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp],
     'kfac_stedc': [c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
     'kfac_pgemm': [c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp],
-    'kfac_gather_grad': [c_int, c_vp, c_int, c_int, c_vp],
+    'kfac_gather_grad': [c_int, c_vp, c_int, c_vp],
     'kfac_split_copy': [c_int, c_vp, c_int, c_int, c_vp],
     'kfac_pgemm_record_size': [],
     'kfac_gather_record_size': [],

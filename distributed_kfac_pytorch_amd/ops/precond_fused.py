@@ -18,9 +18,11 @@ Precision (`precision=`):
             ~5x the fp32 MFMA rate.
   'fp32'    fp32 operands on the exact f32 MFMA (the reference's fp32 math).
 
-Static tables (all pointers are arena/buffer pointers that never move) are
-uploaded once; the gather table is rebuilt only if a `.grad` tensor is
-re-allocated (e.g. `zero_grad(set_to_none=True)`).
+Static GEMM tables (all pointers are arena/buffer pointers that never move)
+are uploaded once; the .grad gather table is passed by value in the kernel
+arguments and rebuilt on the host whenever a `.grad` tensor moved (e.g.
+`zero_grad(set_to_none=True)`), so graph-captured and eager launches never
+share a mutable table.
 """
 import ctypes
 
@@ -262,6 +264,9 @@ class FusedPreconditioner(object):
             t.record_stream(cur)
 
     def _gather_table(self):
+        """Host-side job table for the .grad gather, rebuilt only when a .grad
+        tensor moved; launched BY VALUE (no device table to go stale between
+        graph-captured and eager launches)."""
         sig = []
         for b in self.bufs:
             g = b.layer._get_weight_grad()
@@ -274,11 +279,9 @@ class FusedPreconditioner(object):
         sig = tuple(sig)
         if sig == self._gather_sig:
             return self._gather
-        recs = []
-        tiles = 0
-        for b in self.bufs:
+        recs = (GatherRec * len(self.bufs))()
+        for r, b in zip(recs, self.bufs):
             g = b.layer._get_weight_grad()
-            r = GatherRec()
             r.w = g.data_ptr()
             st = g.stride()
             if g.dim() == 4:
@@ -295,13 +298,9 @@ class FusedPreconditioner(object):
                 r.bias, r.bdtype = bias.data_ptr(), _lib.DTYPE_CODE[bias.dtype]
             r.o_hi, r.o_lo, r.ldo = b.Gct.hi, b.Gct.lo, b.Gct.ld
             r.nG, r.nA = b.nG, b.nA
-            r.tiles_g = _cdiv(b.nG, 64)
-            r.tile_begin = tiles
-            tiles += _cdiv(b.nA, 64) * r.tiles_g
-            recs.append(r)
-        self._gather = (_upload((GatherRec * len(recs))(*recs), self.device), len(recs), tiles)
+        self._gather = recs
         self._gather_sig = sig
-        return self._gather
+        return recs
 
     # ---------------------------------------------------------------- run
     def run(self, damping=0.0, with_kl=True):
@@ -316,9 +315,8 @@ class FusedPreconditioner(object):
             self._build_stage_tables()
         L = _lib.lib()
         stream = _lib.stream(self.device)
-        gt, gc, gtiles = self._gather_table()
-        _lib.check(L.kfac_gather_grad(self.prec, _lib.ptr(gt), gc, gtiles, stream),
-                   'kfac_gather_grad')
+        recs = self._gather_table()
+        _lib.check(L.kfac_gather_grad(self.prec, recs, len(recs), stream), 'kfac_gather_grad')
         if with_kl:
             self.kl.zero_()
         for i, launches in enumerate(self._stage_tables):

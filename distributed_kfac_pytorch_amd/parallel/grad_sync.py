@@ -50,6 +50,11 @@ class GradientAllreduce(object):
                 for t in list(model.parameters()) + list(model.buffers()):
                     dist.broadcast(t.data, src=broadcast_from, group=group)
 
+    def zero_grad(self):
+        """One fill per arena instead of one per parameter."""
+        for arena in self.arenas:
+            arena.zero_()
+
     def check_views(self):
         """True while every .grad is still a view of the arena (an optimizer
         `zero_grad(set_to_none=True)` breaks this)."""

@@ -1,6 +1,5 @@
 set -o pipefail
-export TMPDIR=/tmp
-KFAC_PROFILE_MARKER=1 timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/p2 -o run --output-format csv -- python3 bench.py --steps 12 --warmup 10 --check-finite --graphs 0 > gpurun_out/nan_prof_nog.log 2>&1 || { tail gpurun_out/nan_prof_nog.log; exit 1; }
-grep -c nan gpurun_out/nan_prof_nog.log; grep "^step" gpurun_out/nan_prof_nog.log | head -4
-KFAC_PROFILE_MARKER=1 timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/p3 -o run --output-format csv -- python3 bench.py --steps 12 --warmup 10 --check-finite --eigen-solver serial > gpurun_out/nan_prof_serial.log 2>&1 || { tail gpurun_out/nan_prof_serial.log; exit 1; }
-grep -c nan gpurun_out/nan_prof_serial.log; grep "^step" gpurun_out/nan_prof_serial.log | head -4
+KFAC_NO_TAIL_GRAPH=1 timeout -k 10 200 python bench.py --steps 12 --warmup 10 --check-finite > gpurun_out/nan_a.log 2>&1 || exit 1
+echo "no tail graph: $(grep -c nan gpurun_out/nan_a.log) nan lines"; grep "^step" gpurun_out/nan_a.log | head -4
+timeout -k 10 200 python bench.py --steps 12 --warmup 10 --check-finite --precond-precision fp32 > gpurun_out/nan_b.log 2>&1 || exit 1
+echo "fp32: $(grep -c nan gpurun_out/nan_b.log) nan lines"

@@ -50,6 +50,6 @@ for i, launches in enumerate(fz._stage_tables):
     t = timeit(stage)
     desc = ' '.join('%s:%d' % ('big' if tl else 'small', n) for tl, _, _, n in launches)
     print('  stage %d: %.3f ms  %6.1f GFLOP  %6.1f TFLOP/s  tiles %s' % (i + 1, t, flops[i] / 1e9, flops[i] / t / 1e9, desc))
-gt, gc, gtiles = fz._gather_table()
-t = timeit(lambda: L.kfac_gather_grad(fz.prec, _lib.ptr(gt), gc, gtiles, stream))
+recs = fz._gather_table()
+t = timeit(lambda: L.kfac_gather_grad(fz.prec, recs, len(recs), stream))
 print('  gather: %.3f ms' % t)

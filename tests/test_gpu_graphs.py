@@ -10,7 +10,7 @@ from distributed_kfac_pytorch_amd.models import resnet_cifar
 pytestmark = pytest.mark.gpu
 
 
-def _train(use_graphs, steps=25, precision='fp32', segmented=False):
+def _train(use_graphs, steps=25, precision='fp32', segmented=False, set_to_none=False):
     torch.manual_seed(0)
     m = resnet_cifar.resnet20().cuda().to(memory_format=torch.channels_last)
     opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9)
@@ -23,7 +23,7 @@ def _train(use_graphs, steps=25, precision='fp32', segmented=False):
     y = torch.empty_like(ys[0])
 
     def step_fn():
-        opt.zero_grad(set_to_none=False)
+        opt.zero_grad(set_to_none=set_to_none)
         with torch.autocast('cuda', dtype=torch.bfloat16):
             loss = F.cross_entropy(m(x), y)
         loss.backward()
@@ -86,3 +86,16 @@ def test_segmented_graphs_match_eager():
         assert abs(a - b) < 2e-2 * max(1.0, abs(a)), (le, ls)
     noise, diff = _pdiff(pe, pe2), _pdiff(pe, ps)
     assert diff < max(1e-2, 20 * noise), (diff, noise)
+
+
+def test_graphed_set_to_none_matches_eager():
+    """zero_grad(set_to_none=True): the graph owns its gradients; eager
+    inverse steps allocate their own; K-FAC gathers by value from either."""
+    le, pe, _ = _train(False, steps=14, set_to_none=True)
+    le2, pe2, _ = _train(False, steps=14, set_to_none=True)
+    lg, pg, sg = _train(True, steps=14, set_to_none=True)
+    assert sg.replays > 0
+    for a, b in zip(le, lg):
+        assert abs(a - b) < 2e-2 * max(1.0, abs(a)), (le, lg)
+    noise, diff = _pdiff(pe, pe2), _pdiff(pe, pg)
+    assert diff < max(5e-3, 20 * noise), (diff, noise)
