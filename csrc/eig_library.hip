@@ -63,3 +63,25 @@ KFAC_API int kfac_stedc(float* D, float* E, float* C, int n, int* info, hipStrea
   rocblas_status st = rocsolver_sstedc(h, rocblas_evect_tridiagonal, n, D, E, C, n, info);
   return st == rocblas_status_success ? 0 : 1000 + (int)st;
 }
+
+// Householder tridiagonalisation only (strided batch, lower/upper per `lower`):
+// d, e (batch x n), tau (batch x n).  Pure kernel launches: capturable.
+KFAC_API int kfac_sytrd_batched(float* A, int n, int batch, float* D, float* E, float* tau,
+                                int lower, hipStream_t stream) {
+  rocblas_handle h = handle_for(stream);
+  if (!h) return -2;
+  const rocblas_stride nn = (rocblas_stride)n * n;
+  rocblas_status st = rocsolver_ssytrd_strided_batched(
+      h, lower ? rocblas_fill_lower : rocblas_fill_upper, n, A, n, nn, D, n, E, n, tau, n, batch);
+  return st == rocblas_status_success ? 0 : 1000 + (int)st;
+}
+
+// C <- Q C with Q from kfac_sytrd_batched (single matrix).
+KFAC_API int kfac_ormtr(float* A, float* tau, float* C, int n, int lower, hipStream_t stream) {
+  rocblas_handle h = handle_for(stream);
+  if (!h) return -2;
+  rocblas_status st = rocsolver_sormtr(h, rocblas_side_left,
+                                       lower ? rocblas_fill_lower : rocblas_fill_upper,
+                                       rocblas_operation_none, n, n, A, n, tau, C, n);
+  return st == rocblas_status_success ? 0 : 1000 + (int)st;
+}

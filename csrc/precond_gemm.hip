@@ -374,22 +374,33 @@ KFAC_API int kfac_pgemm_record_size() { return (int)sizeof(PGemm); }
 KFAC_API int kfac_gather_record_size() { return (int)sizeof(GatherJob); }
 KFAC_API int kfac_split_record_size() { return (int)sizeof(SplitJob); }
 
-// tile: 0 = small (128 x 128, 256 threads), 1 = big (256 x 256, 512 threads);
+// tile: 0 = 128 x 128 (4 waves), 1 = 256 x 256 (8 waves), 2 = 64 x 64 (4 waves),
+// 3 = 128 x 128 (8 waves), 4 = 128 x 64 (4 waves);
 // the table (ops/precond_fused.py) holds the problems of that tile class.
 KFAC_API int kfac_pgemm(int prec, int tile, const void* dev_table, int count, int total_tiles,
                         double* kl, hipStream_t stream) {
   if (count <= 0 || total_tiles <= 0) return 0;
   const PGemm* t = (const PGemm*)dev_table;
   dim3 g(total_tiles);
+#define KFAC_PGEMM_LAUNCH(P)                                                                          \
+  switch (tile) {                                                                                     \
+    case 1: hipLaunchKernelGGL((pgemm_kernel<P, 256, 256, 2, 4>), g, dim3(512), 0, stream, t, count, kl); break; \
+    case 2: hipLaunchKernelGGL((pgemm_kernel<P, 64, 64, 2, 2>), g, dim3(256), 0, stream, t, count, kl); break;   \
+    case 3: hipLaunchKernelGGL((pgemm_kernel<P, 128, 128, 4, 2>), g, dim3(512), 0, stream, t, count, kl); break; \
+    case 4: hipLaunchKernelGGL((pgemm_kernel<P, 128, 64, 2, 2>), g, dim3(256), 0, stream, t, count, kl); break;  \
+    case 5: hipLaunchKernelGGL((pgemm_kernel<P, 128, 128, 4, 4>), g, dim3(1024), 0, stream, t, count, kl); break; \
+    case 6: hipLaunchKernelGGL((pgemm_kernel<P, 256, 128, 4, 2>), g, dim3(512), 0, stream, t, count, kl); break; \
+    case 7: hipLaunchKernelGGL((pgemm_kernel<P, 128, 256, 2, 4>), g, dim3(512), 0, stream, t, count, kl); break; \
+    default: hipLaunchKernelGGL((pgemm_kernel<P, 128, 128, 2, 2>), g, dim3(256), 0, stream, t, count, kl); break; \
+  }
   if (prec == PREC_BF16X3) {
-    if (tile) hipLaunchKernelGGL((pgemm_kernel<PREC_BF16X3, 256, 256, 2, 4>), g, dim3(512), 0, stream, t, count, kl);
-    else hipLaunchKernelGGL((pgemm_kernel<PREC_BF16X3, 128, 128, 2, 2>), g, dim3(256), 0, stream, t, count, kl);
+    KFAC_PGEMM_LAUNCH(PREC_BF16X3)
   } else if (prec == PREC_F32) {
-    if (tile) hipLaunchKernelGGL((pgemm_kernel<PREC_F32, 256, 256, 2, 4>), g, dim3(512), 0, stream, t, count, kl);
-    else hipLaunchKernelGGL((pgemm_kernel<PREC_F32, 128, 128, 2, 2>), g, dim3(256), 0, stream, t, count, kl);
+    KFAC_PGEMM_LAUNCH(PREC_F32)
   } else {
     return -1;
   }
+#undef KFAC_PGEMM_LAUNCH
   return (int)hipGetLastError();
 }
 

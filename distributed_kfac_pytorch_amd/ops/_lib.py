@@ -66,6 +66,8 @@ _SIGS = {
     'kfac_max_small_eig_n': [],
     'kfac_syevd_batched': [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp],
     'kfac_stedc': [c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
+    'kfac_sytrd_batched': [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp],
+    'kfac_ormtr': [c_vp, c_vp, c_vp, c_int, c_int, c_vp],
     'kfac_pgemm': [c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp],
     'kfac_gather_grad': [c_int, c_vp, c_int, c_vp],
     'kfac_split_copy': [c_int, c_vp, c_int, c_int, c_vp],

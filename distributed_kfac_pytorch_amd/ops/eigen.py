@@ -87,6 +87,7 @@ def _syevd_class(mats, clip, stream):
                                                   _lib.ptr(info), _lib.c_vp(stream.cuda_stream)),
                    'kfac_syevd_batched')
         _INFOS.append(info)
+        del _INFOS[:-256]   # bounded when nobody checks
         # column-major eigenvector k == row k of the row-major view
         Q = A.transpose(1, 2).contiguous()
         if clip is not None:

@@ -39,13 +39,24 @@ BIG_TILE = 256    # big tile class: half the operand traffic per FLOP
 
 
 BIG_TILES = False  # measured 2.7x slower on ResNet-50 (profiles/r1_pgemm_variants.log)
+# kernel tile configurations of csrc/precond_gemm.hip: id -> (BM, BN)
+TILE_SHAPES = {0: (128, 128), 1: (256, 256), 2: (64, 64), 3: (128, 128), 4: (128, 64),
+               5: (128, 128), 6: (256, 128), 7: (128, 256)}
+# tile configuration of every problem not in the big class, per precision
+# (profiles/r1_pgemm_variants.md: bf16x3 128x128 with 8 waves 1.64 ms vs 1.94
+# ms with 4 waves; fp32 128x128 with 16 waves 2.98 ms vs 3.55 ms)
+TILE_CFG_DEFAULT = {'bf16x3': 3, 'fp32': 5}
+TILE_CFG = None    # None: per-precision default
 
 
-def _tile_class(M, N):
-    """1 = 256 x 256 tiles, 0 = 128 x 128 tiles.  The chain is latency bound
-    (few tiles in flight per CU), so the small tile with 4x the tile count
-    wins; the big class stays available for experiments."""
-    return 1 if (BIG_TILES and M >= 256 and N >= 256) else 0
+def _tile_class(M, N, precision):
+    """1 = 256 x 256 tiles, else the 128 x 128 configuration.  The chain is
+    latency bound (few k-steps in flight per CU): 128 x 128 tiles with more
+    waves per tile win over bigger tiles; the big class stays available for
+    experiments."""
+    if BIG_TILES and M >= 256 and N >= 256:
+        return 1
+    return TILE_CFG if TILE_CFG is not None else TILE_CFG_DEFAULT[precision]
 
 
 class PGemmRec(ctypes.Structure):
@@ -197,17 +208,19 @@ class FusedPreconditioner(object):
                 r.M, r.N, r.K = M, N, K
                 probs.append(r)
             launches = []
-            for tile, size in ((1, BIG_TILE), (0, TILE)):
-                sel = [r for r in probs if _tile_class(r.M, r.N) == tile]
+            classes = sorted({_tile_class(r.M, r.N, self.precision) for r in probs})
+            for tile in classes:
+                bm, bn = TILE_SHAPES[tile]
+                sel = [r for r in probs if _tile_class(r.M, r.N, self.precision) == tile]
                 if not sel:
                     continue
                 # longest k-loops first: their tiles are dispatched first
                 sel.sort(key=lambda r: -r.K)
                 tiles = 0
                 for r in sel:
-                    r.tiles_n = _cdiv(r.N, size)
+                    r.tiles_n = _cdiv(r.N, bn)
                     r.tile_begin = tiles
-                    tiles += _cdiv(r.M, size) * r.tiles_n
+                    tiles += _cdiv(r.M, bm) * r.tiles_n
                 arr = (PGemmRec * len(sel))(*sel)
                 launches.append((tile, _upload(arr, self.device), len(sel), tiles))
             stages.append(launches)

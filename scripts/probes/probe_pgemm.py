@@ -40,6 +40,14 @@ for b in fz.bufs:
     flops[1] += 2.0 * nA * nG * nA
     flops[2] += 2.0 * nG * nA * nG
     flops[3] += 2.0 * nG * nA * nA
+from distributed_kfac_pytorch_amd.ops import precond_fused as pf
+for cfg in (0, 3, 5, 6, 7):
+    pf.TILE_CFG = cfg
+    fz._build_stage_tables()
+    t = timeit(lambda: fz.run(damping=0.001))
+    print('tile cfg %d %s: chain %.3f ms' % (cfg, pf.TILE_SHAPES[cfg], t), flush=True)
+pf.TILE_CFG = int(os.environ['TILE_CFG']) if 'TILE_CFG' in os.environ else None
+fz._build_stage_tables()
 tot = timeit(lambda: fz.run(damping=0.001))
 print('%s: full chain %.3f ms  (%.1f GFLOP real, %.1f TFLOP/s)' % (prec, tot, sum(flops) / 1e9, sum(flops) / tot / 1e9))
 for i, launches in enumerate(fz._stage_tables):
