@@ -132,13 +132,20 @@ def check(err, name):
 
 
 _ws = {}
+_retired = []
 
 
 def workspace(device, numel, dtype=torch.float32, tag='main'):
-    """A grow-only scratch buffer per (device, tag, dtype); stream-ordered reuse."""
+    """A grow-only scratch buffer per (device, tag, dtype); stream-ordered reuse.
+
+    A buffer that is outgrown is retired but never freed: a hipGraph captured
+    earlier may still address it, and freeing it would let the allocator hand
+    that memory to another tensor while the graph keeps writing into it."""
     key = (str(device), tag, dtype)
     buf = _ws.get(key)
     if buf is None or buf.numel() < numel:
+        if buf is not None:
+            _retired.append(buf)
         buf = torch.empty(max(numel, 1), dtype=dtype, device=device)
         _ws[key] = buf
     return buf[:numel]

@@ -169,11 +169,15 @@ class FusedPreconditioner(object):
         self.kl = torch.zeros((), dtype=torch.float64, device=self.device)
         self._gather_sig = None
         self._stage_tables = None
+        # superseded device tables stay alive: a captured graph may use them
+        self._retired_tables = []
         self.damping = 0.0
         self._build_stage_tables()
 
     # ------------------------------------------------------------- tables
     def _build_stage_tables(self):
+        if self._stage_tables is not None:
+            self._retired_tables.append(self._stage_tables)
         stages = []
         for stage in range(4):
             probs = []
