@@ -36,7 +36,10 @@ def init_distributed(backend=None, no_cuda=False, timeout_s=1800):
         torch.cuda.set_device(device)
     if is_distributed() and not dist.is_initialized():
         if backend is None:
-            backend = 'nccl' if device.type == 'cuda' else 'gloo'
+            # KFAC_DIST_BACKEND=gloo rehearses the multi-rank GPU path with
+            # several ranks sharing one GPU (RCCL refuses duplicate devices)
+            backend = os.environ.get('KFAC_DIST_BACKEND') or \
+                ('nccl' if device.type == 'cuda' else 'gloo')
         kw = {}
         if backend == 'nccl' and device.type == 'cuda':
             kw['device_id'] = device
