@@ -159,7 +159,8 @@ def main():
     for i in range(args.steps):
         loss = step()
         if args.check_finite:
-            print('step', i, 'loss', float(loss.item()), flush=True)
+            kl = float(pre.fused.kl) if (pre is not None and pre.fused is not None) else 0.0
+            print('step', i, 'loss', float(loss.item()), 'kl', kl, flush=True)
     if device.type == 'cuda':
         torch.cuda.synchronize()
     if dist.is_initialized():

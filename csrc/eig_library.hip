@@ -12,10 +12,13 @@
 // Reference semantics: kfac/layers/utils.py:45-74 (symeig, ascending
 // eigenvalues); the row-major <-> column-major flip is harmless for the
 // symmetric input and handled for the eigenvectors on the Python side.
-#include "common.h"
+#include "pgemm.h"
 
+#include <cstring>
 #include <map>
 #include <mutex>
+#include <tuple>
+#include <vector>
 #include <rocblas/rocblas.h>
 #include <rocsolver/rocsolver.h>
 
@@ -66,7 +69,7 @@ KFAC_API int kfac_stedc(float* D, float* E, float* C, int n, int* info, hipStrea
 
 // Householder tridiagonalisation only (strided batch, lower/upper per `lower`):
 // d, e (batch x n), tau (batch x n).  Pure kernel launches: capturable.
-KFAC_API int kfac_sytrd_batched(float* A, int n, int batch, float* D, float* E, float* tau,
+KFAC_API int kfac_rocsolver_sytrd_batched(float* A, int n, int batch, float* D, float* E, float* tau,
                                 int lower, hipStream_t stream) {
   rocblas_handle h = handle_for(stream);
   if (!h) return -2;
@@ -74,6 +77,312 @@ KFAC_API int kfac_sytrd_batched(float* A, int n, int batch, float* D, float* E, 
   rocblas_status st = rocsolver_ssytrd_strided_batched(
       h, lower ? rocblas_fill_lower : rocblas_fill_upper, n, A, n, nn, D, n, E, n, tau, n, batch);
   return st == rocblas_status_success ? 0 : 1000 + (int)st;
+}
+
+// Tail of the hand-written reduction path (csrc/eig_tridiag.hip): for every
+// matrix of the batch, the tridiagonal divide and conquer (eigenvalues
+// ascending in d, tridiagonal eigenvectors into Z, column-major) and the
+// back-transformation Z <- Q Z with the reflectors left in A (LAPACK lower,
+// column-major == our row-major upper rows).
+KFAC_API int kfac_stedc_ormtr_batched(float* A, int lda, long long strideA, float* d, float* e,
+                                      float* tau, float* Z, int ldz, long long strideZ, int n,
+                                      int batch, int* info, hipStream_t stream) {
+  rocblas_handle h = handle_for(stream);
+  if (!h) return -2;
+  for (int b = 0; b < batch; ++b) {
+    rocblas_status st = rocsolver_sstedc(h, rocblas_evect_tridiagonal, n, d + (long long)b * n,
+                                         e + (long long)b * n, Z + b * strideZ, ldz, info + b);
+    if (st != rocblas_status_success) return 1000 + (int)st;
+    st = rocsolver_sormtr(h, rocblas_side_left, rocblas_fill_lower, rocblas_operation_none, n, n,
+                          A + b * strideA, lda, tau + (long long)b * n, Z + b * strideZ, ldz);
+    if (st != rocblas_status_success) return 2000 + (int)st;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Batched blocked back-transformation Z <- Q Z for the hand-written reduction
+// (replaces one rocSOLVER ormtr call per matrix, 13 ms at n = 4608).
+// Q = H_0 H_1 ... H_{n-2} is applied as compact-WY blocks of BT reflectors,
+// last block first:  Z[j0:, :] -= V_k (T_k (V_k^T Z[j0:, :])).  Every GEMM is
+// the grouped MFMA kernel of csrc/precond_gemm.hip (exact f32 MFMA) over all
+// matrices of the size class; the long-K product V_k^T Z is split over K with
+// f32-atomic accumulation.  The whole sequence (~5 launches per block) is
+// captured once per buffer set into a hipGraph (no library GEMM, nothing on
+// the legacy stream).
+//
+// Layouts (all fp32): A row j = reflector j (made explicit: zeros up to j, 1
+// at j+1); Z column-major (row `col` of the row-major view = eigenvector
+// `col`); lda = ldz a multiple of 64 with zero padding past n, so every GEMM
+// operand is k-contiguous and zero-padded to the kernel's 64-wide k-steps.
+//   S1  W1t[col][c] = sum_{i>=j0} Z[col][i] V_k[c][i]     (split-K, atomic)
+//   S2  W2t[col][c] = sum_c' W1t[col][c'] T_k[c][c']
+//   S3  Z[col][j0+i] -= sum_c W2t[col][c] Vt_k[i][c]       (Vt_k = V_k^T copy)
+namespace {
+
+constexpr int BT = 128;       // reflectors per block
+constexpr int KCH = 512;      // split-K chunk of S1
+constexpr int TILE_F32 = 5;   // pgemm 128 x 128 fp32 tile configuration
+
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// Zero fill as a kernel (captured memset nodes misbehaved for multi-matrix
+// batches on ROCm 7.2: tests/test_gpu_eig_tridiag.py).
+__global__ __launch_bounds__(256) void zero_kernel(float4* p, long long n4) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256)
+    p[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// Row j of the reduced matrix (== reflector j in column-major) made explicit:
+// zeros up to j, the implicit 1 at j+1, v[1:] after.
+__global__ __launch_bounds__(256) void make_v_kernel(float* A, int lda, long long sA, int n) {
+  float* row = A + blockIdx.y * sA + (long long)blockIdx.x * lda;
+  const int j = blockIdx.x;
+  for (int i = threadIdx.x; i <= j + 1 && i < n; i += 256) row[i] = (i == j + 1) ? 1.f : 0.f;
+}
+
+// T_k (upper triangular, ROW-major BT x BT, zero beyond kb) from
+// G_k = V_k V_k^T (row-major, ld BT) and tau (LAPACK larft, forward /
+// columnwise): T(i,i) = tau_i, T(0:i, i) = -tau_i T(0:i, 0:i) G(0:i, i).
+__global__ __launch_bounds__(BT) void larft_kernel(const float* G, float* T, const float* tau,
+                                                   int n, int nblk) {
+  __shared__ float sT[BT][BT + 1];
+  __shared__ float sG[BT][BT + 1];
+  const int k = blockIdx.x, mat = blockIdx.y, r = threadIdx.x;
+  const long long off = ((long long)mat * nblk + k) * BT * BT;
+  const int j0 = k * BT;
+  const int kb = (n - j0) < BT ? (n - j0) : BT;
+  for (int i = 0; i < BT; ++i) {
+    sG[r][i] = (r < kb && i < kb) ? G[off + (long long)r * BT + i] : 0.f;
+    sT[r][i] = 0.f;
+  }
+  __syncthreads();
+  const float* tj = tau + (long long)mat * n + j0;
+  for (int i = 0; i < kb; ++i) {
+    const float ti = tj[i];
+    float acc = 0.f;
+    if (r < i)
+      for (int q = r; q < i; ++q) acc += sT[r][q] * sG[q][i];
+    __syncthreads();
+    if (r < i) sT[r][i] = -ti * acc;
+    else if (r == i) sT[r][i] = ti;
+    __syncthreads();
+  }
+  for (int i = 0; i < BT; ++i) T[off + (long long)r * BT + i] = sT[r][i];
+}
+
+struct BtArgs {
+  float* A; int lda; long long sA; const float* tau; float* Z; int ldz; long long sZ; int n;
+  int batch; float* Tbuf; float* W1; float* W2; float* Vt;
+};
+
+// One recorded operation of the back-transformation.
+struct BtOp {
+  int kind;              // 0 pgemm, 1 split copy, 2 memset, 3 make_v, 4 larft
+  size_t off; int count; int tiles;    // table offset (bytes) / records / tiles
+  void* ptr; size_t bytes;             // memset
+};
+
+struct BtPlan {
+  std::vector<BtOp> ops;
+  void* tables = nullptr;
+  hipGraphExec_t exec = nullptr;
+};
+
+void add_pgemm(std::vector<unsigned char>& host, std::vector<BtOp>& ops, std::vector<PGemm>& recs) {
+  int tiles = 0;
+  for (auto& r : recs) {
+    r.tiles_n = cdiv(r.N, 128);
+    r.tile_begin = tiles;
+    tiles += cdiv(r.M, 128) * r.tiles_n;
+  }
+  BtOp op{0, host.size(), (int)recs.size(), tiles, nullptr, 0};
+  const unsigned char* p = (const unsigned char*)recs.data();
+  host.insert(host.end(), p, p + recs.size() * sizeof(PGemm));
+  while (host.size() % 256) host.push_back(0);
+  ops.push_back(op);
+  recs.clear();
+}
+
+PGemm rec(const float* a, long long lda, const float* b, long long ldb, float* c, long long ldc,
+          int M, int N, int K, int epi) {
+  PGemm r;
+  memset(&r, 0, sizeof(r));
+  r.a_hi = r.a_lo = a; r.lda = lda;
+  r.b_hi = r.b_lo = b; r.ldb = ldb;
+  r.c_hi = r.c_lo = c; r.ldc = ldc;
+  r.M = M; r.N = N; r.K = K; r.epi = epi;
+  return r;
+}
+
+// Host-side plan: the op list and every GEMM / copy table of the sequence.
+void build_plan(const BtArgs& a, BtPlan& plan, std::vector<unsigned char>& host) {
+  const int n = a.n, b = a.batch, nblk = cdiv(n, BT);
+  const long long tstride = (long long)nblk * BT * BT;
+  float* G = a.Tbuf;
+  float* T = a.Tbuf + tstride * b;
+  const long long w1s = (long long)n * BT, vts = (long long)a.lda * BT;
+  std::vector<PGemm> recs;
+  plan.ops.push_back(BtOp{3, 0, 0, 0, nullptr, 0});
+  // G_k = V_k V_k^T for every block of every matrix (one grouped launch)
+  for (int m = 0; m < b; ++m)
+    for (int k = 0; k < nblk; ++k) {
+      const int j0 = k * BT, kb = n - j0 < BT ? n - j0 : BT;
+      const float* Vk = a.A + m * a.sA + (long long)j0 * a.lda + j0;
+      recs.push_back(rec(Vk, a.lda, Vk, a.lda, G + m * tstride + (long long)k * BT * BT, BT, kb,
+                         kb, a.lda - j0, EPI_STORE));
+    }
+  add_pgemm(host, plan.ops, recs);
+  plan.ops.push_back(BtOp{4, 0, 0, 0, nullptr, 0});
+  for (int k = nblk - 1; k >= 0; --k) {
+    const int j0 = k * BT, kb = n - j0 < BT ? n - j0 : BT, Kn = a.lda - j0;
+    if (kb < BT) {   // partial block: stale columns >= kb must read as zero
+      plan.ops.push_back(BtOp{2, 0, 0, 0, a.W2, (size_t)b * w1s * 4});
+      plan.ops.push_back(BtOp{2, 0, 0, 0, a.Vt, (size_t)b * vts * 4});
+    }
+    plan.ops.push_back(BtOp{2, 0, 0, 0, a.W1, (size_t)b * w1s * 4});
+    for (int m = 0; m < b; ++m) {
+      const float* Zm = a.Z + m * a.sZ;
+      const float* Vk = a.A + m * a.sA + (long long)j0 * a.lda;
+      for (int k0 = 0; k0 < Kn; k0 += KCH) {
+        const int kc = Kn - k0 < KCH ? Kn - k0 : KCH;
+        recs.push_back(rec(Zm + j0 + k0, a.ldz, Vk + j0 + k0, a.lda, a.W1 + m * w1s, BT, n, kb, kc,
+                           EPI_ATOMIC));
+      }
+    }
+    add_pgemm(host, plan.ops, recs);
+    for (int m = 0; m < b; ++m)
+      recs.push_back(rec(a.W1 + m * w1s, BT, T + m * tstride + (long long)k * BT * BT, BT,
+                         a.W2 + m * w1s, BT, n, kb, BT, EPI_STORE));
+    add_pgemm(host, plan.ops, recs);
+    {  // Vt_k = V_k^T (rows j0.., kb columns)
+      std::vector<SplitJob> jobs(b);
+      int tiles = 0;
+      for (int m = 0; m < b; ++m) {
+        SplitJob& J = jobs[m];
+        J.src = a.A + m * a.sA + (long long)j0 * a.lda + j0; J.lds = a.lda;
+        J.o_hi = J.o_lo = a.Vt + m * vts; J.ldo = BT;
+        J.rows = kb; J.cols = n - j0; J.trans = 1;
+        J.tiles_c = cdiv(J.cols, 64); J.tile_begin = tiles;
+        tiles += cdiv(J.rows, 64) * J.tiles_c;
+      }
+      BtOp op{1, host.size(), b, tiles, nullptr, 0};
+      const unsigned char* p = (const unsigned char*)jobs.data();
+      host.insert(host.end(), p, p + jobs.size() * sizeof(SplitJob));
+      while (host.size() % 256) host.push_back(0);
+      plan.ops.push_back(op);
+    }
+    for (int m = 0; m < b; ++m)
+      recs.push_back(rec(a.W2 + m * w1s, BT, a.Vt + m * vts, BT, a.Z + m * a.sZ + j0, a.ldz, n,
+                         n - j0, BT, EPI_SUB));
+    add_pgemm(host, plan.ops, recs);
+  }
+}
+
+int run_plan(const BtArgs& a, const BtPlan& plan, hipStream_t stream) {
+  const int nblk = cdiv(a.n, BT);
+  const long long tstride = (long long)nblk * BT * BT;
+  for (const BtOp& op : plan.ops) {
+    int err = 0;
+    const unsigned char* t = (const unsigned char*)plan.tables + op.off;
+    switch (op.kind) {
+      case 0: err = kfac_pgemm(PREC_F32, TILE_F32, t, op.count, op.tiles, nullptr, stream); break;
+      case 1: err = kfac_split_copy(PREC_F32, t, op.count, op.tiles, stream); break;
+      case 2: {
+        const long long n4 = (long long)(op.bytes / 16);
+        const int grid = (int)((n4 + 255) / 256 < 2048 ? (n4 + 255) / 256 : 2048);
+        hipLaunchKernelGGL(zero_kernel, dim3(grid), dim3(256), 0, stream, (float4*)op.ptr, n4);
+        err = (int)hipGetLastError();
+        break;
+      }
+      case 3:
+        hipLaunchKernelGGL(make_v_kernel, dim3(a.n, a.batch), dim3(256), 0, stream, a.A, a.lda,
+                           a.sA, a.n);
+        err = (int)hipGetLastError();
+        break;
+      default:
+        hipLaunchKernelGGL(larft_kernel, dim3(nblk, a.batch), dim3(BT), 0, stream, a.Tbuf,
+                           a.Tbuf + tstride * a.batch, a.tau, a.n, nblk);
+        err = (int)hipGetLastError();
+    }
+    if (err) return err;
+  }
+  return 0;
+}
+
+typedef std::tuple<float*, float*, int, int, float*, float*, float*, float*> BtKey;
+std::mutex g_bt_mu;
+std::map<BtKey, BtPlan> g_bt;
+
+// The plan (tables uploaded, graph captured on a private non-blocking
+// stream) of this buffer set; built on first use.  Call it from one thread
+// while no other thread issues library work (kfac_backtransform_prepare).
+BtPlan* plan_for(const BtArgs& a, int* err) {
+  const BtKey key(a.A, a.Z, a.n, a.batch, a.Tbuf, a.W1, a.W2, a.Vt);
+  std::lock_guard<std::mutex> lk(g_bt_mu);
+  auto it = g_bt.find(key);
+  if (it != g_bt.end()) return &it->second;
+  BtPlan plan;
+  std::vector<unsigned char> host;
+  build_plan(a, plan, host);
+  if ((*err = (int)hipMalloc(&plan.tables, host.size())) != 0) return nullptr;
+  if ((*err = (int)hipMemcpy(plan.tables, host.data(), host.size(), hipMemcpyHostToDevice)) != 0)
+    return nullptr;
+  static hipStream_t cap = nullptr;
+  if (!cap && hipStreamCreateWithFlags(&cap, hipStreamNonBlocking) != hipSuccess) cap = nullptr;
+  if (cap && hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal) == hipSuccess) {
+    hipGraph_t graph = nullptr;
+    const int e1 = run_plan(a, plan, cap);
+    const hipError_t e2 = hipStreamEndCapture(cap, &graph);
+    if (!e1 && e2 == hipSuccess && graph &&
+        hipGraphInstantiate(&plan.exec, graph, nullptr, nullptr, 0) != hipSuccess)
+      plan.exec = nullptr;
+    if (graph) hipGraphDestroy(graph);
+  }
+  (void)hipGetLastError();
+  return &(g_bt[key] = plan);
+}
+
+}  // namespace
+
+// A: the reduced matrices (reflectors in rows, made explicit in place),
+// Z: tridiagonal eigenvectors (column-major, ldz) -> eigenvectors of A.
+// lda == ldz, a multiple of 64 (zero padding past n).  Tbuf: 2 x batch x
+// nblk x BT x BT, W1, W2: batch x n x BT, Vt: batch x lda x BT.
+KFAC_API int kfac_tridiag_backtransform(float* A, int lda, long long strideA, const float* tau,
+                                        float* Z, int ldz, long long strideZ, int n, int batch,
+                                        float* Tbuf, float* W1, float* W2, float* Vt,
+                                        int use_graph, hipStream_t stream) {
+  if (lda % 64 || ldz % 64 || lda != ldz || n < 2) return -2;
+  const BtArgs a{A, lda, strideA, tau, Z, ldz, strideZ, n, batch, Tbuf, W1, W2, Vt};
+  int err = 0;
+  BtPlan* plan = plan_for(a, &err);
+  if (!plan) return err ? err : -4;
+  if (use_graph && plan->exec) return (int)hipGraphLaunch(plan->exec, stream);
+  return run_plan(a, *plan, stream);
+}
+
+KFAC_API int kfac_backtransform_prepare(float* A, int lda, long long strideA, const float* tau,
+                                        float* Z, int ldz, long long strideZ, int n, int batch,
+                                        float* Tbuf, float* W1, float* W2, float* Vt) {
+  if (lda % 64 || ldz % 64 || lda != ldz || n < 2) return -2;
+  const BtArgs a{A, lda, strideA, tau, Z, ldz, strideZ, n, batch, Tbuf, W1, W2, Vt};
+  int err = 0;
+  return plan_for(a, &err) ? 0 : (err ? err : -4);
+}
+
+// Tridiagonal divide and conquer only, every matrix of the batch (eigenvalues
+// ascending in d, tridiagonal eigenvectors into Z, column-major).
+KFAC_API int kfac_stedc_batched(float* d, float* e, float* Z, int ldz, long long strideZ, int n,
+                                int batch, int* info, hipStream_t stream) {
+  rocblas_handle h = handle_for(stream);
+  if (!h) return -2;
+  for (int b = 0; b < batch; ++b) {
+    rocblas_status st = rocsolver_sstedc(h, rocblas_evect_tridiagonal, n, d + (long long)b * n,
+                                         e + (long long)b * n, Z + b * strideZ, ldz, info + b);
+    if (st != rocblas_status_success) return 1000 + (int)st;
+  }
+  return 0;
 }
 
 // C <- Q C with Q from kfac_sytrd_batched (single matrix).

@@ -21,6 +21,7 @@
 // kfac/layers/utils.py:4-43,164-178 (A_conv = P^T P / (B * S^3), G_conv =
 // g^T g / (B * S^3), linear: a^T a / rows).
 #include "common.h"
+#include "devtable.h"
 #include <type_traits>
 
 namespace {
@@ -452,10 +453,10 @@ struct SyrkBatch {
 static_assert(sizeof(SyrkBatch) <= 4096, "kernel arguments are limited to 4 KB");
 
 template <int DT>
-__global__ __launch_bounds__(256) void syrk_vec_grouped_kernel(SyrkBatch batch) {
+__global__ __launch_bounds__(256) void syrk_vec_grouped_kernel(const SyrkBatch* __restrict__ batch) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BT * VLDK];
-  const SyrkProblem* t = batch.prob;
-  const int count = batch.count;
+  const SyrkProblem* t = batch->prob;
+  const int count = batch->count;
   int lo = 0, hi = count - 1;
   const int b = blockIdx.x;
   while (lo < hi) {
@@ -522,9 +523,9 @@ struct EmaBatch {
 };
 static_assert(sizeof(EmaBatch) <= 4096, "kernel arguments are limited to 4 KB");
 
-__global__ __launch_bounds__(256) void factor_ema_grouped_kernel(EmaBatch batch) {
-  const EmaJob* t = batch.job;
-  const int count = batch.count;
+__global__ __launch_bounds__(256) void factor_ema_grouped_kernel(const EmaBatch* __restrict__ batch) {
+  const EmaJob* t = batch->job;
+  const int count = batch->count;
   int lo = 0, hi = count - 1;
   const int b = blockIdx.x;
   while (lo < hi) {
@@ -802,6 +803,7 @@ KFAC_API int kfac_syrk_grouped(const void* host_table, int count, int dtype, hip
   const SyrkProblem* t = (const SyrkProblem*)host_table;
   for (int base = 0; base < count; base += MAX_SYRK_PROBLEMS) {
     SyrkBatch b;
+    memset(&b, 0, sizeof(b));   // deterministic table bytes (devtable key)
     b.count = count - base < MAX_SYRK_PROBLEMS ? count - base : MAX_SYRK_PROBLEMS;
     int blocks = 0;
     for (int k = 0; k < b.count; ++k) {
@@ -810,10 +812,13 @@ KFAC_API int kfac_syrk_grouped(const void* host_table, int count, int dtype, hip
       blocks += b.prob[k].blocks;
     }
     if (blocks == 0) continue;
+    int terr = 0;
+    const SyrkBatch* d = (const SyrkBatch*)kfac_devtable::get(&b, sizeof(b), stream, &terr);
+    if (!d) return terr;
     if (dtype == KDT_BF16)
-      hipLaunchKernelGGL(syrk_vec_grouped_kernel<KDT_BF16>, dim3(blocks), dim3(256), 0, stream, b);
+      hipLaunchKernelGGL(syrk_vec_grouped_kernel<KDT_BF16>, dim3(blocks), dim3(256), 0, stream, d);
     else if (dtype == KDT_F16)
-      hipLaunchKernelGGL(syrk_vec_grouped_kernel<KDT_F16>, dim3(blocks), dim3(256), 0, stream, b);
+      hipLaunchKernelGGL(syrk_vec_grouped_kernel<KDT_F16>, dim3(blocks), dim3(256), 0, stream, d);
     else
       return -1;
     int err = (int)hipGetLastError();
@@ -826,6 +831,7 @@ KFAC_API int kfac_ema_grouped(const void* host_table, int count, hipStream_t str
   const EmaJob* t = (const EmaJob*)host_table;
   for (int base = 0; base < count; base += MAX_EMA_JOBS) {
     EmaBatch b;
+    memset(&b, 0, sizeof(b));   // deterministic table bytes (devtable key)
     b.count = count - base < MAX_EMA_JOBS ? count - base : MAX_EMA_JOBS;
     int rows = 0;
     for (int k = 0; k < b.count; ++k) {
@@ -834,7 +840,10 @@ KFAC_API int kfac_ema_grouped(const void* host_table, int count, hipStream_t str
       rows += b.job[k].n;
     }
     if (rows == 0) continue;
-    hipLaunchKernelGGL(factor_ema_grouped_kernel, dim3(rows), dim3(256), 0, stream, b);
+    int terr = 0;
+    const EmaBatch* d = (const EmaBatch*)kfac_devtable::get(&b, sizeof(b), stream, &terr);
+    if (!d) return terr;
+    hipLaunchKernelGGL(factor_ema_grouped_kernel, dim3(rows), dim3(256), 0, stream, d);
     int err = (int)hipGetLastError();
     if (err) return err;
   }

@@ -16,6 +16,7 @@
 // Descriptor tables travel by value in the kernel arguments (< 4 KB), so a
 // table can be rebuilt every step without any H2D copy.
 #include "common.h"
+#include "devtable.h"
 
 namespace {
 
@@ -72,7 +73,9 @@ __device__ __forceinline__ void store_g(const Mat2D& m, long long idx, float v) 
   else ((uint16_t*)m.g)[idx] = f32_to_f16_bits(v);
 }
 
-__global__ __launch_bounds__(256) void grouped_kl_dot_kernel(GroupTable t, double* vg) {
+__global__ __launch_bounds__(256) void grouped_kl_dot_kernel(const GroupTable* __restrict__ tp,
+                                                             double* vg) {
+  const GroupTable& t = *tp;
   const int e = find_entry(t, blockIdx.x);
   const Mat2D m = t.m[e];
   const long long n = (long long)m.rows * m.cols;
@@ -89,9 +92,11 @@ __global__ __launch_bounds__(256) void grouped_kl_dot_kernel(GroupTable t, doubl
   if (threadIdx.x == 0) atomicAdd(vg, part[0] + part[1] + part[2] + part[3]);
 }
 
-__global__ __launch_bounds__(256) void grouped_apply_kernel(GroupTable t, const double* vg,
+__global__ __launch_bounds__(256) void grouped_apply_kernel(const GroupTable* __restrict__ tp,
+                                                            const double* vg,
                                                             double lr2, double kl_clip,
                                                             int use_clip) {
+  const GroupTable& t = *tp;
   float nu = 1.f;
   if (use_clip) {
     double s = (*vg) * lr2;
@@ -147,6 +152,7 @@ static int build_tables_and_launch(const KfacMatRecord* recs, int count, bool do
                                    double lr2, double kl_clip, int use_clip, hipStream_t stream) {
   for (int base = 0; base < count; base += MAXG) {
     GroupTable t;
+    memset(&t, 0, sizeof(t));   // deterministic table bytes (devtable key)
     t.count = count - base < MAXG ? count - base : MAXG;
     int blocks = 0;
     for (int k = 0; k < t.count; ++k) {
@@ -161,10 +167,13 @@ static int build_tables_and_launch(const KfacMatRecord* recs, int count, bool do
     }
     t.block_prefix[t.count] = blocks;
     if (blocks == 0) continue;
+    int terr = 0;
+    const GroupTable* d = (const GroupTable*)kfac_devtable::get(&t, sizeof(t), stream, &terr);
+    if (!d) return terr;
     if (dot)
-      hipLaunchKernelGGL(grouped_kl_dot_kernel, dim3(blocks), dim3(256), 0, stream, t, vg);
+      hipLaunchKernelGGL(grouped_kl_dot_kernel, dim3(blocks), dim3(256), 0, stream, d, vg);
     else
-      hipLaunchKernelGGL(grouped_apply_kernel, dim3(blocks), dim3(256), 0, stream, t, vg, lr2,
+      hipLaunchKernelGGL(grouped_apply_kernel, dim3(blocks), dim3(256), 0, stream, d, vg, lr2,
                          kl_clip, use_clip);
     int err = (int)hipGetLastError();
     if (err) return err;

@@ -27,26 +27,11 @@
 // Auxiliary launches: `gather_grad` builds Gct planes from the .grad tensors
 // (any memory layout, bias as the last K-FAC column), `split_copy` builds the
 // QA/QG/QAt/QGt planes and Dt after each inverse update.
-#include "common.h"
+#include "pgemm.h"
+#include "devtable.h"
 
 namespace {
 
-enum { PREC_F32 = 0, PREC_BF16X3 = 1 };
-enum { EPI_STORE = 0, EPI_HADAMARD = 1, EPI_HADAMARD_VEC = 2, EPI_FINAL = 3 };
-
-
-struct PGemm {
-  const void* a_hi; const void* a_lo; long long lda;
-  const void* b_hi; const void* b_lo; long long ldb;
-  void* c_hi; void* c_lo; long long ldc;
-  // EPI_HADAMARD: C *= dmat[m*ldd + n]; EPI_HADAMARD_VEC: C /= (vn[n]*vm[m] + damping)
-  const float* dmat; long long ldd;
-  const float* vm; const float* vn; float damping;
-  // EPI_FINAL: KL dot partner Grad[m][n] = g_hi/g_lo planes of Gct at [n*ldg + m]
-  const void* g_hi; const void* g_lo; long long ldg;
-  int M, N, K, epi;
-  int tile_begin, tiles_n;
-};
 
 __device__ __forceinline__ int find_problem(const PGemm* __restrict__ t, int count, int blk) {
   int lo = 0, hi = count - 1;
@@ -228,6 +213,10 @@ __global__ __launch_bounds__(64 * WM * WN) void pgemm_kernel(const PGemm* __rest
                       bf16_bits_to_f32(((const uint16_t*)P.g_lo)[go]);
           else g = ((const float*)P.g_hi)[go];
           kl_part += v * g;
+        } else if (P.epi == EPI_SUB) {
+          ((float*)P.c_hi)[o] -= v;
+        } else if (P.epi == EPI_ATOMIC) {
+          atomicAdd((float*)P.c_hi + o, v);
         } else if (X3) {
           uint16_t h, l;
           split_bf16(v, h, l);
@@ -261,10 +250,11 @@ __device__ __forceinline__ float load_any(const void* p, long long i, int dt) {
   return f16_bits_to_f32(((const uint16_t*)p)[i]);
 }
 
-// The job table travels BY VALUE (kernel arguments): the .grad pointers are
-// baked into each launch, so a graph-captured launch and an eager one never
-// share a mutable table (with zero_grad(set_to_none=True) every eager step
-// allocates new gradients while the captured graph keeps its own).
+// The job table lives in an immutable, content-addressed device copy
+// (csrc/devtable.h): a graph-captured launch and an eager one never share a
+// mutable table (with zero_grad(set_to_none=True) every eager step allocates
+// new gradients while the captured graph keeps its own), and no ~4 KB table
+// travels as a by-value kernel argument (corrupted in hipGraph replays).
 constexpr int MAX_GATHER = 36;   // 36 x 104 B: the batch stays under the 4 KB kernel-argument limit
 struct GatherBatch {
   int count, pad[3];
@@ -273,9 +263,9 @@ struct GatherBatch {
 static_assert(sizeof(GatherBatch) <= 4096, "kernel arguments are limited to 4 KB");
 
 template <int PREC>
-__global__ __launch_bounds__(256) void gather_grad_kernel(GatherBatch batch) {
-  const GatherJob* jobs = batch.job;
-  const int count = batch.count;
+__global__ __launch_bounds__(256) void gather_grad_kernel(const GatherBatch* __restrict__ batch) {
+  const GatherJob* jobs = batch->job;
+  const int count = batch->count;
   __shared__ float tile[64][65];
   int lo = 0, hi = count - 1;
   while (lo < hi) {
@@ -324,12 +314,6 @@ __global__ __launch_bounds__(256) void gather_grad_kernel(GatherBatch batch) {
 // ---------------------------------------------------------------- split
 // dst[r][c] (planes or fp32, ld ldo) <- src[r][c] (fp32, ld lds), or the
 // transpose dst[c][r] <- src[r][c] when `trans`.  rows x cols of src.
-struct SplitJob {
-  const float* src; long long lds;
-  void* o_hi; void* o_lo; long long ldo;
-  int rows, cols, trans, tile_begin, tiles_c;
-};
-
 template <int PREC>
 __global__ __launch_bounds__(256) void split_copy_kernel(const SplitJob* __restrict__ jobs,
                                                          int count) {
@@ -409,6 +393,7 @@ KFAC_API int kfac_gather_grad(int prec, const void* host_jobs, int count, hipStr
   const GatherJob* t = (const GatherJob*)host_jobs;
   for (int base = 0; base < count; base += MAX_GATHER) {
     GatherBatch b;
+    memset(&b, 0, sizeof(b));   // deterministic table bytes (devtable key)
     b.count = count - base < MAX_GATHER ? count - base : MAX_GATHER;
     int tiles = 0;
     for (int k = 0; k < b.count; ++k) {
@@ -418,10 +403,13 @@ KFAC_API int kfac_gather_grad(int prec, const void* host_jobs, int count, hipStr
       tiles += ((b.job[k].nA + 63) / 64) * b.job[k].tiles_g;
     }
     if (tiles == 0) continue;
+    int terr = 0;
+    const GatherBatch* d = (const GatherBatch*)kfac_devtable::get(&b, sizeof(b), stream, &terr);
+    if (!d) return terr;
     if (prec == PREC_BF16X3)
-      hipLaunchKernelGGL(gather_grad_kernel<PREC_BF16X3>, dim3(tiles), dim3(256), 0, stream, b);
+      hipLaunchKernelGGL(gather_grad_kernel<PREC_BF16X3>, dim3(tiles), dim3(256), 0, stream, d);
     else
-      hipLaunchKernelGGL(gather_grad_kernel<PREC_F32>, dim3(tiles), dim3(256), 0, stream, b);
+      hipLaunchKernelGGL(gather_grad_kernel<PREC_F32>, dim3(tiles), dim3(256), 0, stream, d);
     int err = (int)hipGetLastError();
     if (err) return err;
   }

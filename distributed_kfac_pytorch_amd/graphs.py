@@ -32,15 +32,25 @@ replay.
 
 Contract: inputs are read from tensors whose storage does not change between
 calls (copy each batch into them); `optimizer.zero_grad(set_to_none=False)`
-(gradients that stay put); the step returns a tensor (the loss).  Known
-issue: with `set_to_none=True` the first replay after an eager inverse step
-diverges on ResNet-50 (not on ResNet-20: tests/test_gpu_graphs.py); the
-root cause is not isolated yet, so keep the gradients in place.  Eager fallback: `enabled=False`, no
-GPU, or an exception during capture (warned once).
+(gradients that stay put); the step returns a tensor (the loss).  Eager
+fallback: `enabled=False`, no GPU, or an exception during capture (warned once).
+
+Every graph is captured with keep_graph=True and its memset nodes are rewritten
+into fill kernels before instantiation (ops/_lib.finalize_graph,
+csrc/graph_fix.hip): on this ROCm runtime a captured memset node does not
+reliably clear its target on replay, and MIOpen zeroes the accumulation
+workspace of ResNet-50's channels_last weight-gradient convolutions that way --
+replayed steps picked up whatever the previous user of that memory left
+(NaN / 1e30 gradients in layer2.0.conv1, scripts/probes/debug_fb_graph.py).
+Eager steps and replays run on one side stream, joined to the caller's
+stream by events; the device is synchronised once after each eager
+(inverse-update) step, which also drains the eigensolver's worker streams.
 """
 import warnings
 
 import torch
+
+from .ops import _lib
 
 __all__ = ['GraphedTrainStep']
 
@@ -122,7 +132,13 @@ class GraphedTrainStep(object):
         kind = self._kind()
         if not self.enabled or kind == 'eager':
             self.eager_steps += 1
-            return self._eager()
+            out = self._eager()
+            if self.enabled:
+                # drain every stream the eager step used (the eigensolver's
+                # worker streams are joined by events only) before the next
+                # replay; once per inv_update_freq steps
+                torch.cuda.synchronize()
+            return out
         if not self.segmented:
             return self._run_segment('step', kind, self.step_fn, advances=True)
         loss = self._run_segment('fb', kind, self.fb, advances=False)
@@ -135,6 +151,20 @@ class GraphedTrainStep(object):
         return loss
 
     def _eager(self):
+        if not self.enabled:
+            return self._eager_body()
+        # eager steps run on the capture stream too: every AccumulateGrad node
+        # (created once per parameter and kept alive across steps, e.g. by
+        # K-FAC's saved activations) then belongs to that stream, and no
+        # capture records a cross-stream dependency on the legacy stream
+        cur = torch.cuda.current_stream()
+        self.side.wait_stream(cur)
+        with torch.cuda.stream(self.side):
+            out = self._eager_body()
+        cur.wait_stream(self.side)
+        return out
+
+    def _eager_body(self):
         if not self.segmented:
             return self.step_fn()
         loss = self.fb()
@@ -147,7 +177,7 @@ class GraphedTrainStep(object):
         key = self._key(seg, kind)
         g = self.graphs.get(key)
         if g is not None:
-            g.replay()
+            self._replay(g)
             if advances:
                 self._advance()
             self.replays += 1
@@ -162,16 +192,26 @@ class GraphedTrainStep(object):
             return out
         return self._capture(key, fn, advances)
 
+    def _replay(self, g):
+        """Replay on the capture stream, joined to the caller's stream by events."""
+        cur = torch.cuda.current_stream()
+        self.side.wait_stream(cur)
+        with torch.cuda.stream(self.side):
+            g.replay()
+        cur.wait_stream(self.side)
+
     def _capture(self, key, fn, advances):
         step0 = self.pre.param_groups[0]['step'] if self.pre is not None else None
         torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
+        g = _lib.new_graph()
         try:
             # a private memory pool per graph: segments and kinds replay in
             # any order, so one graph's outputs must never alias another's
             # temporaries
             with torch.cuda.graph(g, stream=self.side):
                 out = fn()
+            # memset nodes (MIOpen's zeroed workspaces) -> fill kernels
+            _lib.finalize_graph(g)
         except Exception as e:  # pragma: no cover - depends on the HIP runtime
             warnings.warn('hipGraph capture of the training step failed ({}); running '
                           'eagerly from now on'.format(e))
@@ -185,7 +225,7 @@ class GraphedTrainStep(object):
             self.pre.param_groups[0]['step'] = step0
         self.graphs[key] = g
         self.outputs[key] = out
-        g.replay()
+        self._replay(g)
         if advances:
             self._advance()
         self.replays += 1

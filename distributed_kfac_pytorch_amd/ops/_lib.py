@@ -66,7 +66,18 @@ _SIGS = {
     'kfac_max_small_eig_n': [],
     'kfac_syevd_batched': [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp],
     'kfac_stedc': [c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
-    'kfac_sytrd_batched': [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp],
+    'kfac_rocsolver_sytrd_batched': [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp],
+    'kfac_sytrd_batched': [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp],
+    'kfac_sytrd_forget': [c_vp],
+    'kfac_sytrd_prepare': [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp],
+    'kfac_sytrd_ws_floats': [c_int],
+    'kfac_stedc_batched': [c_vp, c_vp, c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp],
+    'kfac_tridiag_backtransform': [c_vp, c_int, c_ll, c_vp, c_vp, c_int, c_ll, c_int, c_int,
+                                   c_vp, c_vp, c_vp, c_vp, c_int, c_vp],
+    'kfac_backtransform_prepare': [c_vp, c_int, c_ll, c_vp, c_vp, c_int, c_ll, c_int, c_int,
+                                   c_vp, c_vp, c_vp, c_vp],
+    'kfac_stedc_ormtr_batched': [c_vp, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_int,
+                                 c_int, c_vp, c_vp],
     'kfac_ormtr': [c_vp, c_vp, c_vp, c_int, c_int, c_vp],
     'kfac_pgemm': [c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp],
     'kfac_gather_grad': [c_int, c_vp, c_int, c_vp],
@@ -74,7 +85,11 @@ _SIGS = {
     'kfac_pgemm_record_size': [],
     'kfac_gather_record_size': [],
     'kfac_split_record_size': [],
+    'kfac_graph_fix_memsets': [c_vp, c_int, ctypes.POINTER(c_ll)],
 }
+
+
+_RESTYPES = {'kfac_sytrd_ws_floats': c_ll, 'kfac_sytrd_forget': None}
 
 
 def _load():
@@ -90,7 +105,7 @@ def _load():
             for name, argt in _SIGS.items():
                 fn = getattr(lib, name)
                 fn.argtypes = argt
-                fn.restype = c_int
+                fn.restype = _RESTYPES.get(name, c_int)
             _lib = lib
         except OSError as e:
             _load_error = str(e)
@@ -129,6 +144,34 @@ def ptr(t):
 def check(err, name):
     if err != 0:
         raise RuntimeError('{} failed with HIP error {}'.format(name, err))
+
+
+# Replace captured memset nodes by fill kernels (csrc/graph_fix.hip); 0 = keep
+# them (A/B runs of the ROCm 7.2 memset-node issue)
+FIX_GRAPH_MEMSETS = os.environ.get('KFAC_GRAPH_FIX_MEMSETS', '1') != '0'
+graph_memset_stats = {'graphs': 0, 'memsets': 0, 'bytes': 0, 'replaced': 0}
+
+
+def new_graph():
+    """A torch.cuda.CUDAGraph that keeps its hipGraph after capture, so that
+    finalize_graph() can rewrite it before it is instantiated."""
+    return torch.cuda.CUDAGraph(keep_graph=True)
+
+
+def finalize_graph(g):
+    """Rewrite the memset nodes of a graph captured with new_graph() into
+    kernel nodes (captured memset nodes do not reliably clear their target on
+    replay with this ROCm runtime: csrc/graph_fix.hip), then instantiate it."""
+    stats = (c_ll * 3)()
+    check(lib().kfac_graph_fix_memsets(c_vp(g.raw_cuda_graph()), int(FIX_GRAPH_MEMSETS), stats),
+          'kfac_graph_fix_memsets')
+    st = graph_memset_stats
+    st['graphs'] += 1
+    st['memsets'] += stats[0]
+    st['bytes'] += stats[1]
+    st['replaced'] += stats[2]
+    g.instantiate()
+    return g
 
 
 _ws = {}

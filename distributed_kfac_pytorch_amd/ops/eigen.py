@@ -3,10 +3,16 @@
 GPU path (MI355X):
   * n <= 192: every such factor of the step is solved by ONE launch of the
     batched LDS Jacobi kernel (csrc/eig_jacobi.hip), one workgroup per matrix.
-  * larger n: grouped by size class, each class in ONE strided-batched
-    divide-and-conquer call (csrc/eig_library.hip); classes run concurrently
-    on a pool of side streams (each solve is dominated by serial panel steps
-    at these sizes: profiles/r1_rocsolver_variants.log).
+  * larger n: grouped by size class; classes run concurrently on a pool of
+    side streams.  LARGE_PATH selects the solver of a class ('auto', the
+    default: 'tridiag' for n >= TRIDIAG_MIN_N, else 'syevd'):
+      'tridiag'  the hand-written blocked Householder reduction
+                 (csrc/eig_tridiag.hip: 3 launches per column for the whole
+                 class, captured into one hipGraph) + rocSOLVER's tridiagonal
+                 divide and conquer and back-transformation per matrix
+      'syevd'    one strided-batched rocSOLVER syevd call per class, whose
+                 reduction is latency bound per column
+                 (profiles/r1_rocsolver_fill_split.log)
 CPU path: torch.linalg.eigh (the reference semantics, kfac/layers/utils.py:45-74).
 
 Results: ascending eigenvalues clipped at `clip` (reference default 0.0),
@@ -21,6 +27,13 @@ from . import _lib
 __all__ = ['symeig_many', 'inverse_many', 'SMALL_N']
 
 SMALL_N = 192
+LARGE_PATH = os.environ.get('KFAC_EIG_LARGE', 'auto')
+# 'auto': the hand-written path from this n up (it wins from 2048 on, rocSOLVER
+# syevd's latency per column wins below: profiles/r1_tridiag_vs_syevd.log)
+TRIDIAG_MIN_N = int(os.environ.get('KFAC_TRIDIAG_MIN_N', '2048'))
+TRIDIAG_GRAPH = bool(int(os.environ.get('KFAC_TRIDIAG_GRAPH', '1')))
+TRIDIAG_BACK = os.environ.get('KFAC_TRIDIAG_BACK', 'wy')   # 'wy' (batched GEMMs) | 'ormtr'
+BT = 128   # back-transformation block (csrc/eig_library.hip)
 SPLIT_N = 1 << 30   # never split: batched big classes beat concurrent singles (r1_eigh_split.log)
 _streams = {}
 
@@ -96,6 +109,99 @@ def _syevd_class(mats, clip, stream):
 
 
 _INFOS = []
+_TRI_BUFS = {}
+
+
+def _tri_buffers(dev, n, b):
+    """Persistent per-(device, n, batch) buffers of the hand-written path: the
+    captured reduction graph addresses them, so they live (and are reused)
+    for the whole run."""
+    key = (str(dev), n, b)
+    bufs = _TRI_BUFS.get(key)
+    if bufs is None:
+        L = _lib.lib()
+        lda = (n + 63) // 64 * 64   # zero-padded rows: k-steps of the MFMA GEMMs
+        wsf = int(L.kfac_sytrd_ws_floats(n))
+        f32 = dict(dtype=torch.float32, device=dev)
+        nblk = (n + BT - 1) // BT
+        bufs = dict(lda=lda, A=torch.zeros(b, n, lda, **f32), Z=torch.zeros(b, n, lda, **f32),
+                    d=torch.zeros(b, n, **f32), e=torch.zeros(b, n, **f32),
+                    tau=torch.zeros(b, n, **f32), ws=torch.zeros(b * wsf, **f32),
+                    info=torch.zeros(b, dtype=torch.int32, device=dev),
+                    T=torch.zeros(2 * b * nblk * BT * BT, **f32),
+                    W1=torch.zeros(b * BT * n, **f32), W2=torch.zeros(b * BT * n, **f32),
+                    Vt=torch.zeros(b * BT * lda, **f32))
+        _TRI_BUFS[key] = bufs
+    return bufs
+
+
+def _tridiag_class(mats, clip, stream, use_graph=None):
+    """Every matrix of one size n: hand-written blocked tridiagonalisation
+    (csrc/eig_tridiag.hip), rocSOLVER's tridiagonal divide and conquer per
+    matrix, then the batched compact-WY back-transformation (three strided-
+    batched GEMMs per 128 reflectors for the whole class), on `stream`."""
+    n = mats[0].shape[0]
+    b = len(mats)
+    dev = mats[0].device
+    L = _lib.lib()
+    if use_graph is None:
+        use_graph = TRIDIAG_GRAPH
+    with torch.cuda.stream(stream):
+        B = _tri_buffers(dev, n, b)
+        lda = B['lda']
+        for i, A in enumerate(mats):
+            B['A'][i, :, :n].copy_(A)
+        sA = n * lda
+        cs = _lib.c_vp(stream.cuda_stream)
+        _lib.check(L.kfac_sytrd_batched(_lib.ptr(B['A']), lda, sA, n, b, _lib.ptr(B['d']),
+                                        _lib.ptr(B['e']), _lib.ptr(B['tau']), _lib.ptr(B['ws']),
+                                        int(use_graph), cs), 'kfac_sytrd_batched')
+        if TRIDIAG_BACK == 'ormtr':
+            _lib.check(L.kfac_stedc_ormtr_batched(_lib.ptr(B['A']), lda, sA, _lib.ptr(B['d']),
+                                                  _lib.ptr(B['e']), _lib.ptr(B['tau']),
+                                                  _lib.ptr(B['Z']), lda, sA, n, b,
+                                                  _lib.ptr(B['info']), cs),
+                       'kfac_stedc_ormtr_batched')
+        else:
+            _lib.check(L.kfac_stedc_batched(_lib.ptr(B['d']), _lib.ptr(B['e']), _lib.ptr(B['Z']),
+                                            lda, sA, n, b, _lib.ptr(B['info']), cs),
+                       'kfac_stedc_batched')
+            _lib.check(L.kfac_tridiag_backtransform(*_bt_args(B, n, b), int(use_graph), cs),
+                       'kfac_tridiag_backtransform')
+        _INFOS.append(B['info'].clone())
+        del _INFOS[:-256]
+        # column-major eigenvector k (row k of Z) -> column k of a row-major Q
+        Q = B['Z'][:, :, :n].transpose(1, 2).contiguous()
+        D = B['d'].clone()
+        if clip is not None:
+            D.clamp_(min=clip)
+    return [(Q[i], D[i]) for i in range(b)]
+
+
+def _bt_args(B, n, b):
+    lda = B['lda']
+    return (_lib.ptr(B['A']), lda, n * lda, _lib.ptr(B['tau']), _lib.ptr(B['Z']), lda, n * lda,
+            n, b, _lib.ptr(B['T']), _lib.ptr(B['W1']), _lib.ptr(B['W2']), _lib.ptr(B['Vt']))
+
+
+def _tridiag_prepare(n, b, dev):
+    """Allocate the class buffers and build its reduction hipGraph now, from
+    the calling thread, before concurrent class solves start: a capture must
+    not overlap other threads' library calls (hipBLASLt inside rocBLAS)."""
+    B = _tri_buffers(dev, n, b)
+    lda = B['lda']
+    _lib.check(_lib.lib().kfac_sytrd_prepare(_lib.ptr(B['A']), lda, n * lda, n, b,
+                                             _lib.ptr(B['d']), _lib.ptr(B['e']),
+                                             _lib.ptr(B['tau']), _lib.ptr(B['ws'])),
+               'kfac_sytrd_prepare')
+    _lib.check(_lib.lib().kfac_backtransform_prepare(*_bt_args(B, n, b)),
+               'kfac_backtransform_prepare')
+
+
+def _class_solver(n):
+    if LARGE_PATH == 'tridiag' or (LARGE_PATH == 'auto' and n >= TRIDIAG_MIN_N):
+        return _tridiag_class
+    return _syevd_class
 
 
 def check_solver_status():
@@ -150,10 +256,15 @@ def _library_eigh(mats, clip, n_workers=None):
     if n_workers <= 1:
         cur = torch.cuda.current_stream(dev)
         for idx in jobs:
-            for i, r in zip(idx, _syevd_class([mats[i] for i in idx], clip, cur)):
+            solve = _class_solver(mats[idx[0]].shape[0])
+            for i, r in zip(idx, solve([mats[i] for i in idx], clip, cur)):
                 outs[i] = r
         return outs
     cur = torch.cuda.current_stream(dev)
+    for idx in jobs:
+        n = mats[idx[0]].shape[0]
+        if _class_solver(n) is _tridiag_class and TRIDIAG_GRAPH:
+            _tridiag_prepare(n, len(idx), dev)
     k = min(n_workers, len(jobs))
     pool = _side_streams(dev, k)
     for s in pool:
@@ -168,7 +279,8 @@ def _library_eigh(mats, clip, n_workers=None):
 
     def work(j):
         torch.cuda.set_device(dev)
-        return [(idx, _syevd_class([mats[i] for i in idx], clip, pool[j])) for idx in assign[j]]
+        return [(idx, _class_solver(mats[idx[0]].shape[0])([mats[i] for i in idx], clip, pool[j]))
+                for idx in assign[j]]
 
     for res in _thread_pool(k).map(work, range(k)):
         for idx, rs in res:

@@ -36,6 +36,7 @@ import torch.optim as optim
 
 from . import comm
 from . import layers as kfac_layers
+from .ops import _lib
 from .ops import precond as precond_ops
 from .ops import eigen as eigen_ops
 from .ops import precond_fused
@@ -46,6 +47,38 @@ from .utils import distribution
 from .utils.tracing import PhaseTimer
 
 __all__ = ['CommMethod', 'KFAC']
+
+# KFAC_DEBUG_EIG=1: host-check every eigendecomposition of an inverse step
+# (finite results, residual) -- a debugging aid, syncs the device
+_DEBUG_EIG = bool(int(__import__('os').environ.get('KFAC_DEBUG_EIG', '0')))
+
+
+def _debug_check_eig(jobs, mats, results):
+    for (layer, which), A, (Q, d) in zip(jobs, mats, results):
+        fin = bool(torch.isfinite(Q).all()) and bool(torch.isfinite(d).all())
+        A64 = A.double()
+        res = float((A64 @ Q.double() - Q.double() * d.double()).norm() / A64.norm()) \
+            if fin else float('nan')
+        if not fin or res > 1e-4:
+            print('KFAC_DEBUG_EIG: {} {} n={} finite={} input_finite={} resid={:.2e}'.format(
+                layer, which, A.shape[0], fin, bool(torch.isfinite(A).all()), res), flush=True)
+
+
+def _check_factors_finite(jobs, mats):
+    """Raise on a non-finite factor before it reaches the eigensolvers: an
+    inverse update over NaN factors ended in an illegal-address GPU fault
+    instead of an error (the data-dependent deflation / iteration logic of the
+    solvers is not NaN-safe).  One multi-tensor norm and one host read per
+    inverse update."""
+    if not mats or not mats[0].is_cuda:
+        return
+    norms = torch.stack(torch._foreach_norm(mats, 1))
+    ok = torch.isfinite(norms)
+    if bool(ok.all()):
+        return
+    bad = ['{} {}'.format(l, w) for (l, w), f in zip(jobs, ok.tolist()) if not f]
+    raise FloatingPointError('non-finite K-FAC factor(s) at an inverse update: {}'.format(
+        ', '.join(bad[:8])))
 
 
 class CommMethod(enum.Enum):
@@ -163,6 +196,7 @@ class KFAC(optim.Optimizer):
         self._graph_sig = None
         self._graph_scale = None
         self._graph_warm = False
+        self._sync_before_replay = False
 
         comm.init_comm_backend()
         size = comm.backend.size()
@@ -441,6 +475,11 @@ class KFAC(optim.Optimizer):
     def _graph_replay(self):
         sig = self._graph_signature()
         if self._graph is not None and sig == self._graph_sig:
+            if self._sync_before_replay:
+                # new eigendata came from side streams this step: drain them
+                # before the replay (see graphs.GraphedTrainStep)
+                torch.cuda.synchronize()
+                self._sync_before_replay = False
             self._graph.replay()
             return
         if not self._graph_warm or sig != self._graph_sig:
@@ -451,11 +490,12 @@ class KFAC(optim.Optimizer):
             self._precondition_and_apply()
             return
         try:
-            g = torch.cuda.CUDAGraph()
+            g = _lib.new_graph()
             # the captured ops read .grad; run them on a clean copy of the
             # current grads after capture (capture itself does not execute)
             with torch.cuda.graph(g):
                 self._graph_scale = self._precondition_and_apply()
+            _lib.finalize_graph(g)
             self._graph = g
             self._graph.replay()
         except Exception as e:  # pragma: no cover - depends on the HIP runtime
@@ -509,10 +549,13 @@ class KFAC(optim.Optimizer):
         if not jobs:
             return
         mats = [l.state[w].to(torch.float32) for l, w in jobs]
+        _check_factors_finite(jobs, mats)
         if self.use_eigen_decomp:
             results = eigen_ops.symeig_many(mats, clip=0.0, solver=self.eigen_solver)
             if self.check_solver:
                 eigen_ops.check_solver_status()
+            if _DEBUG_EIG:
+                _debug_check_eig(jobs, mats, results)
             results = [(Q.to(l.inv_dtype), d.to(l.inv_dtype))
                        for (l, _), (Q, d) in zip(jobs, results)]
         else:
@@ -544,6 +587,7 @@ class KFAC(optim.Optimizer):
 
     def _eigendata_updated(self):
         """New eigendata is in place: refresh the fused kernels' operand copies."""
+        self._sync_before_replay = True
         if self.fused is not None:
             self.fused.refresh_eigen()
 

@@ -15,7 +15,7 @@ run() {  # run <name> <seconds> <cmd...>
 }
 STEPS=${STEPS:-100}
 if [ -z "$SKIP_TESTS" ]; then
-  run pytest_gpu 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  run pytest_gpu 540 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
   run smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ -z "$SKIP_BENCH" ]; then

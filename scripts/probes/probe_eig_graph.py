@@ -17,7 +17,7 @@ for n, b in ((4608, 3), (2304, 6), (1024, 6), (512, 6)):
 
     def call():
         A.copy_(A0)
-        _lib.check(L.kfac_sytrd_batched(_lib.ptr(A), n, b, _lib.ptr(D), _lib.ptr(E), _lib.ptr(tau), 1,
+        _lib.check(L.kfac_rocsolver_sytrd_batched(_lib.ptr(A), n, b, _lib.ptr(D), _lib.ptr(E), _lib.ptr(tau), 1,
                                         _lib.stream(dev)), 'sytrd')
     call(); torch.cuda.synchronize()
     t = time.perf_counter(); call(); torch.cuda.synchronize(); te = (time.perf_counter() - t) * 1e3
