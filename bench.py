@@ -66,10 +66,11 @@ def parse():
                          'bf16x3 = split-bf16 MFMA, ~1e-5 relative error)')
     ap.add_argument('--graphs', type=int, default=1,
                     help='hipGraph capture of the training step (1/0)')
-    ap.add_argument('--set-to-none', type=int, default=0,
+    ap.add_argument('--set-to-none', type=int, default=1,
                     help='optimizer.zero_grad(set_to_none=...) (single-rank / DDP paths); '
-                         '1 is ~0.7 ms/step faster but NaNs after graph replays follow an '
-                         'eager inverse step (under investigation)')
+                         '1 skips the gradient fill + accumulate kernels (~0.8 ms/step); the '
+                         'earlier NaNs with 1 were MIOpen workspace memsets inside captured '
+                         'graphs (csrc/graph_fix.hip)')
     ap.add_argument('--ddp', action='store_true',
                     help='eager torch DDP instead of the graphed flat-arena all-reduce')
     return ap.parse_args()
