@@ -71,6 +71,9 @@ def parse():
                          '1 skips the gradient fill + accumulate kernels (~0.8 ms/step); the '
                          'earlier NaNs with 1 were MIOpen workspace memsets inside captured '
                          'graphs (csrc/graph_fix.hip)')
+    ap.add_argument('--inverse-lag', type=int, default=0,
+                    help='KFAC(inverse_lag=L): eigendecompositions of an inverse step run on a '
+                         'side stream and take effect L steps later (0 = reference schedule)')
     ap.add_argument('--ddp', action='store_true',
                     help='eager torch DDP instead of the graphed flat-arena all-reduce')
     return ap.parse_args()
@@ -109,6 +112,7 @@ def main():
                         distribute_layer_factors=False, eigen_solver=args.eigen_solver,
                         profile=args.profile_phases, precond_precision=args.precond_precision,
                         compute_factor_in_hook=grad_sync is not None,
+                        inverse_lag=args.inverse_lag,
                         use_hip_graphs=not os.environ.get('KFAC_NO_TAIL_GRAPH'))
 
     B, S = args.batch_size, args.image_size
@@ -162,6 +166,8 @@ def main():
         if args.check_finite:
             kl = float(pre.fused.kl) if (pre is not None and pre.fused is not None) else 0.0
             print('step', i, 'loss', float(loss.item()), 'kl', kl, flush=True)
+    if pre is not None:
+        pre.wait_inverses()   # a lagged solve launched in the window is timed in full
     if device.type == 'cuda':
         torch.cuda.synchronize()
     if dist.is_initialized():
@@ -198,7 +204,8 @@ def main():
                            'factor_update_freq': args.kfac_cov_update_freq,
                            'inv_update_freq': args.kfac_update_freq,
                            'damping': args.damping, 'kl_clip': args.kl_clip,
-                           'precond_precision': args.precond_precision},
+                           'precond_precision': args.precond_precision,
+                           'inverse_lag': args.inverse_lag},
                        'hip_graphs': use_graphs,
                        'grad_allreduce': 'ddp' if grad_sync is None and world > 1 else
                                          ('flat-arena' if world > 1 else None),

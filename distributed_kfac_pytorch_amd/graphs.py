@@ -31,8 +31,10 @@ key, so a scheduler that changes them triggers a re-capture, never a stale
 replay.
 
 Contract: inputs are read from tensors whose storage does not change between
-calls (copy each batch into them); `optimizer.zero_grad(set_to_none=False)`
-(gradients that stay put); the step returns a tensor (the loss).  Eager
+calls (copy each batch into them); `optimizer.zero_grad()` with either
+`set_to_none` (True lets each graph's backward produce fresh .grad tensors from
+its private pool; the K-FAC tail graph keys on the grad pointers); the step
+returns a tensor (the loss).  Eager
 fallback: `enabled=False`, no GPU, or an exception during capture (warned once).
 
 Every graph is captured with keep_graph=True and its memset nodes are rewritten
@@ -95,6 +97,8 @@ class GraphedTrainStep(object):
         p = pre.param_groups[0]
         if not pre.workers_assigned or p['step'] % p['inv_update_freq'] == 0:
             return 'eager'
+        if getattr(pre, 'inverse_apply_due', None) is not None and pre.inverse_apply_due():
+            return 'eager'    # a lagged inverse update is stored this step (host work)
         if p['step'] % p['factor_update_freq'] == 0:
             return 'factor'
         return 'plain'
@@ -136,8 +140,13 @@ class GraphedTrainStep(object):
             if self.enabled:
                 # drain every stream the eager step used (the eigensolver's
                 # worker streams are joined by events only) before the next
-                # replay; once per inv_update_freq steps
-                torch.cuda.synchronize()
+                # replay; once per inv_update_freq steps.  A lagged inverse
+                # update in flight keeps running: only this step's streams.
+                if self.pre is not None and getattr(self.pre, 'inverses_in_flight', False):
+                    self.side.synchronize()
+                    torch.cuda.current_stream().synchronize()
+                else:
+                    torch.cuda.synchronize()
             return out
         if not self.segmented:
             return self._run_segment('step', kind, self.step_fn, advances=True)
@@ -202,6 +211,8 @@ class GraphedTrainStep(object):
 
     def _capture(self, key, fn, advances):
         step0 = self.pre.param_groups[0]['step'] if self.pre is not None else None
+        if self.pre is not None and hasattr(self.pre, 'wait_inverses'):
+            self.pre.wait_inverses()   # no solver-thread library calls during a capture
         torch.cuda.synchronize()
         g = _lib.new_graph()
         try:

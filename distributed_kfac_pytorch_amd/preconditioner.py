@@ -107,6 +107,17 @@ class _DeviceKLScale(object):
         return precond_ops.kl_scale(self.vg, self.lr, self.kl_clip)
 
 
+_INV_EXECUTOR = None
+
+
+def _inverse_executor():
+    global _INV_EXECUTOR
+    if _INV_EXECUTOR is None:
+        import concurrent.futures
+        _INV_EXECUTOR = concurrent.futures.ThreadPoolExecutor(1, thread_name_prefix='kfac-inv')
+    return _INV_EXECUTOR
+
+
 class KFAC(optim.Optimizer):
     def __init__(self, model, damping=0.001, factor_decay=0.95, factor_update_freq=10,
                  inv_update_freq=100, kl_clip=0.001, lr=0.1, accumulate_data=False,
@@ -117,7 +128,7 @@ class KFAC(optim.Optimizer):
                  use_eigen_decomp=True, skip_layers=[], verbose=False,
                  bucket_cap_mb=64.0, symmetry_aware_comm=True, eigen_solver='auto',
                  profile=False, use_hip_graphs=True, precond_precision='fp32',
-                 fused_precondition=True):
+                 fused_precondition=True, inverse_lag=0):
         if not 0.0 <= lr:
             raise ValueError('Invalid learning rate: {}'.format(lr))
         if not 0.0 < factor_decay <= 1:
@@ -130,6 +141,8 @@ class KFAC(optim.Optimizer):
             raise ValueError('Invalid factor update frequency: {}'.format(factor_update_freq))
         if not 0 < inv_update_freq:
             raise ValueError('Invalid K-FAC update frequency: {}'.format(inv_update_freq))
+        if not 0 <= inverse_lag < inv_update_freq:
+            raise ValueError('inverse_lag must be in [0, inv_update_freq): {}'.format(inverse_lag))
         if inv_update_freq % factor_update_freq != 0:
             warnings.warn('It is suggested that inv_update_freq be a multiple of '
                           'factor_update_freq')
@@ -197,6 +210,13 @@ class KFAC(optim.Optimizer):
         self._graph_scale = None
         self._graph_warm = False
         self._sync_before_replay = False
+        # lagged inverses (inverse_lag > 0): the eigendecompositions of step k
+        # run on a side stream, launched by a host thread, while steps
+        # k .. k+lag-1 keep preconditioning with the previous eigendata
+        self.inverse_lag = int(inverse_lag)
+        self._pending_inv = None
+        self._inv_stream = None
+        self._have_inverses = False
 
         comm.init_comm_backend()
         size = comm.backend.size()
@@ -262,6 +282,7 @@ class KFAC(optim.Optimizer):
 
     # ------------------------------------------------------------ state dict
     def state_dict(self, include_layer_factors=True, include_layer_inverses=False):
+        self.wait_inverses()
         sd = super(KFAC, self).state_dict()
         layers = None
         if include_layer_factors:
@@ -415,13 +436,21 @@ class KFAC(optim.Optimizer):
         if not self.workers_assigned:
             self._assign_workers()
             self.workers_assigned = True
-        if p['step'] % p['inv_update_freq'] == 0:
+        inv_step = p['step'] % p['inv_update_freq'] == 0
+        if self._pending_inv is not None and (inv_step or self.inverse_apply_due()):
             with t('inverses'):
-                self.compute_inverses(damping=p['damping'])
-            if self.comm_method in (CommMethod.COMM_OPT, CommMethod.HYBRID_OPT):
-                with t('inverse_comm'):
-                    self.broadcast_inverses()
-            self._eigendata_updated()
+                self._apply_lagged_inverses()
+        if inv_step:
+            if self.inverse_lag > 0 and self._have_inverses:
+                with t('inverses'):
+                    self._launch_lagged_inverses(p['damping'])
+            else:
+                with t('inverses'):
+                    self.compute_inverses(damping=p['damping'])
+                if self.comm_method in (CommMethod.COMM_OPT, CommMethod.HYBRID_OPT):
+                    with t('inverse_comm'):
+                        self.broadcast_inverses()
+                self._eigendata_updated()
         if self._graph_eligible():
             with t('precondition'):
                 self._graph_replay()
@@ -489,6 +518,7 @@ class KFAC(optim.Optimizer):
             self._graph_warm = True
             self._precondition_and_apply()
             return
+        self.wait_inverses()   # no solver thread may run library calls during a capture
         try:
             g = _lib.new_graph()
             # the captured ops read .grad; run them on a clean copy of the
@@ -534,9 +564,7 @@ class KFAC(optim.Optimizer):
             handles.extend(layer.broadcast_gradient())
         comm.backend.sync(handles)
 
-    @torch.no_grad()
-    def compute_inverses(self, damping=0.001):
-        """Eigendecompose / invert every factor this rank owns, in one batch."""
+    def _inverse_jobs(self):
         rank = comm.backend.rank()
         jobs = []
         for layer in self.layers:
@@ -546,24 +574,124 @@ class KFAC(optim.Optimizer):
                 layer._ensure_inv_buffers(which)
                 if getattr(layer, 'compute_{}_inv_rank'.format(which)) == rank:
                     jobs.append((layer, which))
+        return jobs
+
+    def _solve_inverses(self, jobs, mats, damping):
+        if self.use_eigen_decomp:
+            results = eigen_ops.symeig_many(mats, clip=0.0, solver=self.eigen_solver)
+            if _DEBUG_EIG:
+                _debug_check_eig(jobs, mats, results)
+            return [(Q.to(l.inv_dtype), d.to(l.inv_dtype))
+                    for (l, _), (Q, d) in zip(jobs, results)]
+        return [r.to(l.inv_dtype)
+                for (l, _), r in zip(jobs, eigen_ops.inverse_many(mats, damping))]
+
+    @staticmethod
+    def _store_inverses(jobs, results, damping):
+        # A before G: the G owner forms dGdA from both eigenvalue sets
+        for (layer, which), res in sorted(zip(jobs, results), key=lambda x: x[0][1]):
+            layer.finish_inverse(which, res, damping)
+
+    @torch.no_grad()
+    def compute_inverses(self, damping=0.001):
+        """Eigendecompose / invert every factor this rank owns, in one batch."""
+        self._drop_lagged_inverses()
+        jobs = self._inverse_jobs()
+        self._have_inverses = True
         if not jobs:
             return
         mats = [l.state[w].to(torch.float32) for l, w in jobs]
         _check_factors_finite(jobs, mats)
-        if self.use_eigen_decomp:
-            results = eigen_ops.symeig_many(mats, clip=0.0, solver=self.eigen_solver)
-            if self.check_solver:
-                eigen_ops.check_solver_status()
-            if _DEBUG_EIG:
-                _debug_check_eig(jobs, mats, results)
-            results = [(Q.to(l.inv_dtype), d.to(l.inv_dtype))
-                       for (l, _), (Q, d) in zip(jobs, results)]
-        else:
-            results = [r.to(l.inv_dtype)
-                       for (l, _), r in zip(jobs, eigen_ops.inverse_many(mats, damping))]
-        # A before G: the G owner forms dGdA from both eigenvalue sets
-        for (layer, which), res in sorted(zip(jobs, results), key=lambda x: x[0][1]):
-            layer.finish_inverse(which, res, damping)
+        results = self._solve_inverses(jobs, mats, damping)
+        if self.use_eigen_decomp and self.check_solver:
+            eigen_ops.check_solver_status()
+        self._store_inverses(jobs, results, damping)
+
+    # ------------------------------------------------------ lagged inverses
+    # inverse_lag = L > 0 (opt-in; 0 is the reference's synchronous schedule,
+    # kfac/preconditioner.py:506-510): the inverse update of step k
+    # snapshots the factors, launches their eigendecompositions on a side
+    # stream from a host thread and returns; steps k .. k+L-1 precondition
+    # with the previous eigendata, step k+L waits for the solve, stores and
+    # broadcasts the result.  The eigensolver is panel-latency bound
+    # (profiles/README.md), so the model's kernels fill the CUs it leaves
+    # idle.  Asynchronous, stale curvature inverses as in Ba, Grosse and
+    # Martens, "Distributed second-order optimization using Kronecker-factored
+    # approximations" (ICLR 2017).  All ranks apply at the same step, so the
+    # eigendata broadcast stays a matched collective.
+
+    def inverse_apply_due(self):
+        """True when this step stores the lagged inverse update."""
+        pend = self._pending_inv
+        return pend is not None and self.param_groups[0]['step'] >= pend['apply_at']
+
+    @property
+    def inverses_in_flight(self):
+        return self._pending_inv is not None
+
+    def _launch_lagged_inverses(self, damping):
+        jobs = self._inverse_jobs()
+        pend = dict(jobs=jobs, damping=damping, results=None, future=None, event=None,
+                    apply_at=self.param_groups[0]['step'] + self.inverse_lag)
+        self._pending_inv = pend
+        if not jobs:
+            return
+        # private fp32 snapshot: factor updates of steps k+1.. must not race the solve
+        mats = [l.state[w].to(torch.float32, copy=True) for l, w in jobs]
+        if not mats[0].is_cuda:
+            pend['results'] = self._solve_inverses(jobs, mats, damping)
+            return
+        dev = mats[0].device
+        cur = torch.cuda.current_stream(dev)
+        if self._inv_stream is None:
+            self._inv_stream = torch.cuda.Stream(device=dev)
+        s = self._inv_stream
+        s.wait_stream(cur)
+        for m in mats:
+            m.record_stream(s)
+
+        def work():
+            torch.cuda.set_device(dev)
+            with torch.cuda.stream(s):
+                _check_factors_finite(jobs, mats)
+                res = self._solve_inverses(jobs, mats, damping)
+                ev = torch.cuda.Event()
+                ev.record(s)
+            return res, ev
+
+        pend['future'] = _inverse_executor().submit(work)
+
+    def wait_inverses(self):
+        """Host-join the solver thread of a lagged inverse update (its GPU
+        work may still run; it is applied at its step).  Called before any
+        graph capture and by state_dict()."""
+        pend = self._pending_inv
+        if pend is not None and pend['future'] is not None:
+            fut, pend['future'] = pend['future'], None
+            pend['results'], pend['event'] = fut.result()
+
+    def _apply_lagged_inverses(self):
+        self.wait_inverses()
+        pend, self._pending_inv = self._pending_inv, None
+        jobs, results = pend['jobs'], pend['results']
+        if jobs:
+            if pend['event'] is not None:
+                cur = torch.cuda.current_stream()
+                cur.wait_event(pend['event'])
+                for r in results:
+                    for t in (r if isinstance(r, tuple) else (r,)):
+                        t.record_stream(cur)
+                if self.use_eigen_decomp and self.check_solver:
+                    eigen_ops.check_solver_status()
+            self._store_inverses(jobs, results, pend['damping'])
+        if self.comm_method in (CommMethod.COMM_OPT, CommMethod.HYBRID_OPT):
+            self.broadcast_inverses()
+        self._eigendata_updated()
+
+    def _drop_lagged_inverses(self):
+        if self._pending_inv is not None:
+            self.wait_inverses()
+            self._pending_inv = None
 
     @torch.no_grad()
     def compute_factors(self, alpha=0.95):

@@ -40,7 +40,8 @@ def kfac_strategy(rank, world, port, out_dir, cfg):
                     grad_worker_fraction=cfg.get('fraction', 0.25),
                     distribute_layer_factors=cfg.get('distribute', False),
                     precompute_outer_eigen=cfg.get('prediv', True),
-                    use_eigen_decomp=cfg.get('eigen', True))
+                    use_eigen_decomp=cfg.get('eigen', True),
+                    inverse_lag=cfg.get('lag', 0))
     grads, factors = run_steps(model, pre, data, cfg['steps'])
     torch.save({'grads': grads, 'factors': factors},
                os.path.join(out_dir, 'rank{}.pt'.format(rank)))

@@ -47,7 +47,8 @@ def _single_run(cfg):
     model, data = build_case({'seed': 0, 'batch': 6, 'steps': cfg['steps']})
     pre = kfac.KFAC(model, factor_update_freq=1, inv_update_freq=cfg.get('inv_freq', 2),
                     lr=0.05, damping=0.003, precompute_outer_eigen=cfg.get('prediv', True),
-                    use_eigen_decomp=cfg.get('eigen', True))
+                    use_eigen_decomp=cfg.get('eigen', True),
+                    inverse_lag=cfg.get('lag', 0))
     return run_steps(model, pre, data, cfg['steps'])
 
 

@@ -10,12 +10,13 @@ from distributed_kfac_pytorch_amd.models import resnet_cifar
 pytestmark = pytest.mark.gpu
 
 
-def _train(use_graphs, steps=25, precision='fp32', segmented=False, set_to_none=False):
+def _train(use_graphs, steps=25, precision='fp32', segmented=False, set_to_none=False, lag=0):
     torch.manual_seed(0)
     m = resnet_cifar.resnet20().cuda().to(memory_format=torch.channels_last)
     opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9)
     pre = kfac.KFAC(m, factor_update_freq=2, inv_update_freq=10, lr=0.05,
-                    precond_precision=precision, compute_factor_in_hook=segmented)
+                    precond_precision=precision, compute_factor_in_hook=segmented,
+                    inverse_lag=lag)
     g = torch.Generator(device='cuda').manual_seed(3)
     xs = [torch.randn(16, 3, 32, 32, device='cuda', generator=g) for _ in range(steps)]
     ys = [torch.randint(0, 10, (16,), device='cuda', generator=g) for _ in range(steps)]
@@ -99,3 +100,18 @@ def test_graphed_set_to_none_matches_eager():
         assert abs(a - b) < 2e-2 * max(1.0, abs(a)), (le, lg)
     noise, diff = _pdiff(pe, pe2), _pdiff(pe, pg)
     assert diff < max(5e-3, 20 * noise), (diff, noise)
+
+
+@pytest.mark.parametrize('segmented', [False, True])
+def test_graphed_lagged_inverses_match_eager(segmented):
+    """KFAC(inverse_lag=4): the solves of steps 10 and 20 run on a side stream
+    from a host thread while graphs replay; they are stored at steps 14 and 24
+    (eager steps).  Graphed and eager runs agree."""
+    le, pe, _ = _train(False, steps=25, lag=4, segmented=segmented)
+    le2, pe2, _ = _train(False, steps=25, lag=4, segmented=segmented)
+    lg, pg, sg = _train(True, steps=25, lag=4, segmented=segmented)
+    assert sg.replays > 0 and sg.eager_steps == 5     # 0, 10, 14, 20, 24
+    for a, b in zip(le, lg):
+        assert abs(a - b) < 2e-2 * max(1.0, abs(a)), (le, lg)
+    noise, diff = _pdiff(pe, pe2), _pdiff(pe, pg)
+    assert diff < max(1e-2, 20 * noise), (diff, noise)
