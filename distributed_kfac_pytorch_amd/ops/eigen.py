@@ -34,7 +34,10 @@ TRIDIAG_MIN_N = int(os.environ.get('KFAC_TRIDIAG_MIN_N', '2048'))
 TRIDIAG_GRAPH = bool(int(os.environ.get('KFAC_TRIDIAG_GRAPH', '1')))
 TRIDIAG_BACK = os.environ.get('KFAC_TRIDIAG_BACK', 'wy')   # 'wy' (batched GEMMs) | 'ormtr'
 BT = 128   # back-transformation block (csrc/eig_library.hip)
-SPLIT_N = 1 << 30   # never split: batched big classes beat concurrent singles (r1_eigh_split.log)
+# size classes from this n up are solved as concurrent single-matrix jobs
+# (default: never; rocSOLVER syevd batches beat concurrent singles,
+# r1_eigh_split.log; KFAC_EIG_SPLIT_N re-evaluates it for the tridiag path)
+SPLIT_N = int(os.environ.get('KFAC_EIG_SPLIT_N', str(1 << 30)))
 _streams = {}
 
 
@@ -112,11 +115,12 @@ _INFOS = []
 _TRI_BUFS = {}
 
 
-def _tri_buffers(dev, n, b):
-    """Persistent per-(device, n, batch) buffers of the hand-written path: the
-    captured reduction graph addresses them, so they live (and are reused)
-    for the whole run."""
-    key = (str(dev), n, b)
+def _tri_buffers(dev, n, b, slot=0):
+    """Persistent per-(device, n, batch, slot) buffers of the hand-written
+    path: the captured reduction graph addresses them, so they live (and are
+    reused) for the whole run.  Concurrent jobs of one (n, b) use distinct
+    slots."""
+    key = (str(dev), n, b, slot)
     bufs = _TRI_BUFS.get(key)
     if bufs is None:
         L = _lib.lib()
@@ -135,7 +139,7 @@ def _tri_buffers(dev, n, b):
     return bufs
 
 
-def _tridiag_class(mats, clip, stream, use_graph=None):
+def _tridiag_class(mats, clip, stream, use_graph=None, slot=0):
     """Every matrix of one size n: hand-written blocked tridiagonalisation
     (csrc/eig_tridiag.hip), rocSOLVER's tridiagonal divide and conquer per
     matrix, then the batched compact-WY back-transformation (three strided-
@@ -147,7 +151,7 @@ def _tridiag_class(mats, clip, stream, use_graph=None):
     if use_graph is None:
         use_graph = TRIDIAG_GRAPH
     with torch.cuda.stream(stream):
-        B = _tri_buffers(dev, n, b)
+        B = _tri_buffers(dev, n, b, slot)
         lda = B['lda']
         for i, A in enumerate(mats):
             B['A'][i, :, :n].copy_(A)
@@ -184,11 +188,11 @@ def _bt_args(B, n, b):
             n, b, _lib.ptr(B['T']), _lib.ptr(B['W1']), _lib.ptr(B['W2']), _lib.ptr(B['Vt']))
 
 
-def _tridiag_prepare(n, b, dev):
+def _tridiag_prepare(n, b, dev, slot=0):
     """Allocate the class buffers and build its reduction hipGraph now, from
     the calling thread, before concurrent class solves start: a capture must
     not overlap other threads' library calls (hipBLASLt inside rocBLAS)."""
-    B = _tri_buffers(dev, n, b)
+    B = _tri_buffers(dev, n, b, slot)
     lda = B['lda']
     _lib.check(_lib.lib().kfac_sytrd_prepare(_lib.ptr(B['A']), lda, n * lda, n, b,
                                              _lib.ptr(B['d']), _lib.ptr(B['e']),
@@ -261,10 +265,16 @@ def _library_eigh(mats, clip, n_workers=None):
                 outs[i] = r
         return outs
     cur = torch.cuda.current_stream(dev)
-    for idx in jobs:
+    # jobs of one (n, b) run concurrently on distinct buffer slots
+    slot, seen = {}, {}
+    for j, idx in enumerate(jobs):
+        key = (mats[idx[0]].shape[0], len(idx))
+        slot[j] = seen.get(key, 0)
+        seen[key] = slot[j] + 1
+    for j, idx in enumerate(jobs):
         n = mats[idx[0]].shape[0]
         if _class_solver(n) is _tridiag_class and TRIDIAG_GRAPH:
-            _tridiag_prepare(n, len(idx), dev)
+            _tridiag_prepare(n, len(idx), dev, slot[j])
     k = min(n_workers, len(jobs))
     pool = _side_streams(dev, k)
     for s in pool:
@@ -272,15 +282,21 @@ def _library_eigh(mats, clip, n_workers=None):
     # greedy LPT of the jobs over the workers (cost ~ n^3, a batch nearly free)
     load = [0.0] * k
     assign = [[] for _ in range(k)]
-    for idx in jobs:
+    for jb, idx in enumerate(jobs):
         j = min(range(k), key=lambda w: load[w])
-        assign[j].append(idx)
+        assign[j].append((jb, idx))
         load[j] += float(mats[idx[0]].shape[0]) ** 3 * (1.0 + 0.3 * (len(idx) - 1))
+
+    def solve(jb, idx, stream):
+        fn = _class_solver(mats[idx[0]].shape[0])
+        sub = [mats[i] for i in idx]
+        if fn is _tridiag_class:
+            return fn(sub, clip, stream, slot=slot[jb])
+        return fn(sub, clip, stream)
 
     def work(j):
         torch.cuda.set_device(dev)
-        return [(idx, _class_solver(mats[idx[0]].shape[0])([mats[i] for i in idx], clip, pool[j]))
-                for idx in assign[j]]
+        return [(idx, solve(jb, idx, pool[j])) for jb, idx in assign[j]]
 
     for res in _thread_pool(k).map(work, range(k)):
         for idx, rs in res:
@@ -288,7 +304,7 @@ def _library_eigh(mats, clip, n_workers=None):
                 outs[i] = r
     for j, s in enumerate(pool[:k]):
         cur.wait_stream(s)
-        for idx in assign[j]:
+        for _, idx in assign[j]:
             for i in idx:
                 mats[i].record_stream(s)
                 outs[i][0].record_stream(cur)

@@ -691,6 +691,10 @@ class KFAC(optim.Optimizer):
     def _drop_lagged_inverses(self):
         if self._pending_inv is not None:
             self.wait_inverses()
+            ev = self._pending_inv['event']
+            if ev is not None:
+                # the solver's persistent buffers are reused by the next solve
+                torch.cuda.current_stream().wait_event(ev)
             self._pending_inv = None
 
     @torch.no_grad()

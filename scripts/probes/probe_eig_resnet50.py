@@ -1,0 +1,74 @@
+"""Probe: wall time of one full ResNet-50 inverse update (symeig_many over every
+A and G factor size of the 54 K-FAC layers, random SPD matrices) under eigensolver
+scheduling variants: size-class batching vs concurrent single-matrix jobs for
+the big classes (SPLIT_N), worker streams, tridiag threshold."""
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.getcwd())
+from distributed_kfac_pytorch_amd.models import resnet  # noqa: E402
+from distributed_kfac_pytorch_amd.ops import eigen  # noqa: E402
+
+
+def sizes():
+    m = resnet.resnet50()
+    out = []
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Conv2d):
+            out += [mod.in_channels * mod.kernel_size[0] * mod.kernel_size[1] +
+                    (mod.bias is not None), mod.out_channels]
+        elif isinstance(mod, torch.nn.Linear):
+            out += [mod.in_features + 1, mod.out_features]
+    return out
+
+
+def main():
+    dev = torch.device('cuda')
+    side = torch.cuda.Stream()
+    torch.cuda.set_stream(side)
+    ns = sizes()
+    g = torch.Generator(device=dev).manual_seed(0)
+    mats = []
+    for n in ns:
+        x = torch.randn(n, max(64, n // 2), device=dev, generator=g)
+        mats.append(x @ x.t() / x.shape[1] + 1e-3 * torch.eye(n, device=dev))
+    print('factors', len(ns), 'sum n^3 %.3g' % sum(float(n) ** 3 for n in ns), flush=True)
+    variants = [('default', {}), ('split4608', {'SPLIT_N': 4096}),
+                ('split2048', {'SPLIT_N': 2048}),
+                ('split4608_w6', {'SPLIT_N': 4096, 'W': 6}),
+                ('w8', {'W': 8})]
+    if len(sys.argv) > 1:
+        variants = [v for v in variants if v[0] in sys.argv[1:]]
+    res = {}
+    base = dict(SPLIT_N=eigen.SPLIT_N, TRIDIAG_MIN_N=eigen.TRIDIAG_MIN_N)
+    for name, cfg in variants:
+        eigen.SPLIT_N = cfg.get('SPLIT_N', base['SPLIT_N'])
+        eigen.TRIDIAG_MIN_N = cfg.get('TRIDIAG_MIN_N', base['TRIDIAG_MIN_N'])
+        if 'W' in cfg:
+            os.environ['KFAC_EIGH_WORKERS'] = str(cfg['W'])
+        else:
+            os.environ.pop('KFAC_EIGH_WORKERS', None)
+        eigen.symeig_many(mats)       # warm: buffers, graphs
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(3):
+            t = time.perf_counter()
+            outs = eigen.symeig_many(mats)
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t) * 1e3)
+        eigen.check_solver_status()
+        err = 0.0
+        for A, (Q, d) in zip(mats[-8:], outs[-8:]):
+            err = max(err, float((A @ Q - Q * d).norm() / A.norm()))
+        res[name] = {'ms': min(ts), 'all_ms': ts, 'resid': err}
+        print('%-14s %8.2f ms  (runs %s)  resid %.1e' % (name, min(ts),
+              ' '.join('%.1f' % t for t in ts), err), flush=True)
+    print(json.dumps(res))
+
+
+if __name__ == '__main__':
+    main()
