@@ -45,6 +45,7 @@ from .parallel.plan import ExecutionPlan
 from .parallel import collectives
 from .utils import distribution
 from .utils.tracing import PhaseTimer
+from .utils import comm_check
 
 __all__ = ['CommMethod', 'KFAC']
 
@@ -128,7 +129,7 @@ class KFAC(optim.Optimizer):
                  use_eigen_decomp=True, skip_layers=[], verbose=False,
                  bucket_cap_mb=64.0, symmetry_aware_comm=True, eigen_solver='auto',
                  profile=False, use_hip_graphs=True, precond_precision='fp32',
-                 fused_precondition=True, inverse_lag=0):
+                 fused_precondition=True, inverse_lag=0, comm_check=False):
         if not 0.0 <= lr:
             raise ValueError('Invalid learning rate: {}'.format(lr))
         if not 0.0 < factor_decay <= 1:
@@ -192,6 +193,10 @@ class KFAC(optim.Optimizer):
         self.eigen_solver = eigen_solver
         # host-checks the eigensolver status once per inverse step (one sync)
         self.check_solver = True
+        # debug mode: checksum-compare the buffers each collective phase must
+        # leave identical on every rank (utils/comm_check.py)
+        self.comm_check = bool(comm_check) or \
+            bool(int(__import__('os').environ.get('KFAC_COMM_CHECK', '0')))
         self.workers_assigned = False
         self.plan = None
         self.timer = PhaseTimer(enabled=profile)
@@ -433,6 +438,8 @@ class KFAC(optim.Optimizer):
                     self.compute_factors(alpha=p['factor_decay'])
             with t('factor_comm'):
                 self.allreduce_factors()
+            if self.comm_check:
+                self._check_comm('factor all-reduce', ('A', 'G'))
         if not self.workers_assigned:
             self._assign_workers()
             self.workers_assigned = True
@@ -450,6 +457,8 @@ class KFAC(optim.Optimizer):
                 if self.comm_method in (CommMethod.COMM_OPT, CommMethod.HYBRID_OPT):
                     with t('inverse_comm'):
                         self.broadcast_inverses()
+                    if self.comm_check and self.comm_method == CommMethod.COMM_OPT:
+                        self._check_comm('eigendata broadcast', self._broadcast_keys())
                 self._eigendata_updated()
         if self._graph_eligible():
             with t('precondition'):
@@ -460,6 +469,8 @@ class KFAC(optim.Optimizer):
             if self.comm_method in (CommMethod.MEM_OPT, CommMethod.HYBRID_OPT):
                 with t('grad_comm'):
                     self.broadcast_gradients()
+                if self.comm_check and self.comm_method == CommMethod.MEM_OPT:
+                    self._check_comm('gradient broadcast', None)
             with t('update'):
                 scale = None if p['kl_clip'] is None else self._compute_grad_scale()
                 self.update_gradients(scale)
@@ -534,6 +545,31 @@ class KFAC(optim.Optimizer):
             self.use_hip_graphs = False
             self._graph = None
             self._precondition_and_apply()
+
+    def _broadcast_keys(self):
+        # the per-layer state the eigendata broadcast delivers to every rank
+        if not self.use_eigen_decomp:
+            return ('A_inv', 'G_inv')
+        return ('QA', 'QG', 'dGdA') if self.precompute_outer_eigen else ('QA', 'QG', 'dA', 'dG')
+
+    def _check_comm(self, phase, keys):
+        """Debug mode: raise comm_check.CommConsistencyError unless the
+        `keys` of every layer's state (or, with keys=None, every layer's
+        preconditioned gradient) are identical on every rank."""
+        if comm.backend.size() == 1:
+            return
+        named = []
+        for i, layer in enumerate(self.layers):
+            tag = '{}:{}'.format(i, type(layer.module).__name__)
+            if keys is None:
+                g = layer.preconditioned_gradient
+                parts = list(g) if isinstance(g, (list, tuple)) else [g]
+                named += [('{}.grad{}'.format(tag, j), x) for j, x in enumerate(parts)
+                          if x is not None]
+            else:
+                named += [('{}.{}'.format(tag, k), layer.state[k]) for k in keys
+                          if layer.state.get(k) is not None]
+        comm_check.assert_consistent(named, phase)
 
     def allreduce_factors(self):
         if comm.backend.size() == 1:
@@ -686,6 +722,8 @@ class KFAC(optim.Optimizer):
             self._store_inverses(jobs, results, pend['damping'])
         if self.comm_method in (CommMethod.COMM_OPT, CommMethod.HYBRID_OPT):
             self.broadcast_inverses()
+            if self.comm_check and self.comm_method == CommMethod.COMM_OPT:
+                self._check_comm('eigendata broadcast', self._broadcast_keys())
         self._eigendata_updated()
 
     def _drop_lagged_inverses(self):

@@ -120,3 +120,19 @@ def test_bench_distributed_cpu(tmp_path, method):
     assert rec['n_gpus'] == 2 and rec['steps'] == 2 and rec['warmup'] == 1
     assert rec['config']['global_batch'] == 4
     assert rec['value'] > 0 and rec['config']['parallelism'] == 'dp2'
+
+
+@pytest.mark.parametrize('method,mode', [('COMM_OPT', 'clean'), ('MEM_OPT', 'clean'),
+                                         ('COMM_OPT', 'skip_allreduce'),
+                                         ('COMM_OPT', 'corrupt_eigendata')])
+def test_comm_consistency_check(tmp_path, method, mode):
+    """Debug mode: cross-rank checksums after each collective
+    phase pass on clean runs and name the buffers of a sabotaged one."""
+    _spawn(_dist_worker.comm_check, 2, tmp_path, {'method': method, 'mode': mode})
+    errs = [torch.load(os.path.join(tmp_path, 'rank{}.pt'.format(r)))['err'] for r in range(2)]
+    if mode == 'clean':
+        assert errs == [None, None], errs
+    elif mode == 'skip_allreduce':
+        assert all(e is not None and 'factor all-reduce' in e and '.A' in e for e in errs), errs
+    else:
+        assert all(e is not None and 'eigendata broadcast' in e and '0:' in e for e in errs), errs
