@@ -25,7 +25,11 @@ def is_distributed():
 
 def get_local_device(no_cuda=False):
     if torch.cuda.is_available() and not no_cuda:
-        return torch.device('cuda', int(os.environ.get('LOCAL_RANK', '0')))
+        # modulo the visible devices: a multi-rank rehearsal on a one-GPU box
+        # (KFAC_DIST_BACKEND=gloo) puts every rank on cuda:0; on a full node
+        # LOCAL_RANK < device_count and this is the identity
+        n = max(1, torch.cuda.device_count())
+        return torch.device('cuda', int(os.environ.get('LOCAL_RANK', '0')) % n)
     return torch.device('cpu')
 
 
