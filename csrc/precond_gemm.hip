@@ -58,9 +58,11 @@ __device__ __forceinline__ void split_bf16(float x, uint16_t& h, uint16_t& l) {
 //         dimension below 256 (layers with 64..192 channels)
 constexpr int TK = 32;
 
-template <int PREC, int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(64 * WM * WN) void pgemm_kernel(const PGemm* __restrict__ table,
-                                                             int count, double* __restrict__ kl) {
+// WPE: minimum waves per SIMD the register allocator must allow (1 = no
+// constraint).  WPE 6 fits three 8-wave workgroups per CU (80 VGPRs).
+template <int PREC, int BM, int BN, int WM, int WN, int WPE = 1>
+__global__ __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(WPE)))
+void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict__ kl) {
   constexpr bool X3 = (PREC == PREC_BF16X3);
   constexpr int NT = 64 * WM * WN;                // threads
   constexpr int MI = BM / WM / 32, NJ = BN / WN / 32;
@@ -375,6 +377,8 @@ KFAC_API int kfac_pgemm(int prec, int tile, const void* dev_table, int count, in
     case 5: hipLaunchKernelGGL((pgemm_kernel<P, 128, 128, 4, 4>), g, dim3(1024), 0, stream, t, count, kl); break; \
     case 6: hipLaunchKernelGGL((pgemm_kernel<P, 256, 128, 4, 2>), g, dim3(512), 0, stream, t, count, kl); break; \
     case 7: hipLaunchKernelGGL((pgemm_kernel<P, 128, 256, 2, 4>), g, dim3(512), 0, stream, t, count, kl); break; \
+    case 8: hipLaunchKernelGGL((pgemm_kernel<P, 128, 128, 4, 2, 6>), g, dim3(512), 0, stream, t, count, kl); break; \
+    case 9: hipLaunchKernelGGL((pgemm_kernel<P, 128, 128, 4, 2, 5>), g, dim3(512), 0, stream, t, count, kl); break; \
     default: hipLaunchKernelGGL((pgemm_kernel<P, 128, 128, 2, 2>), g, dim3(256), 0, stream, t, count, kl); break; \
   }
   if (prec == PREC_BF16X3) {

@@ -41,7 +41,7 @@ BIG_TILE = 256    # big tile class: half the operand traffic per FLOP
 BIG_TILES = False  # measured 2.7x slower on ResNet-50 (profiles/r1_pgemm_variants.log)
 # kernel tile configurations of csrc/precond_gemm.hip: id -> (BM, BN)
 TILE_SHAPES = {0: (128, 128), 1: (256, 256), 2: (64, 64), 3: (128, 128), 4: (128, 64),
-               5: (128, 128), 6: (256, 128), 7: (128, 256)}
+               5: (128, 128), 6: (256, 128), 7: (128, 256), 8: (128, 128), 9: (128, 128)}
 # tile configuration of every problem not in the big class, per precision
 # (profiles/r1_pgemm_variants.md: bf16x3 128x128 with 8 waves 1.64 ms vs 1.94
 # ms with 4 waves; fp32 128x128 with 16 waves 2.98 ms vs 3.55 ms)

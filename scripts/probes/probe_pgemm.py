@@ -41,7 +41,7 @@ for b in fz.bufs:
     flops[2] += 2.0 * nG * nA * nG
     flops[3] += 2.0 * nG * nA * nA
 from distributed_kfac_pytorch_amd.ops import precond_fused as pf
-for cfg in (0, 3, 5, 6, 7):
+for cfg in [int(c) for c in os.environ.get('PGEMM_CFGS', '0,3,5,6,7').split(',')]:
     pf.TILE_CFG = cfg
     fz._build_stage_tables()
     t = timeit(lambda: fz.run(damping=0.001))
