@@ -40,7 +40,9 @@ def main():
     variants = [('default', {}), ('split4608', {'SPLIT_N': 4096}),
                 ('split2048', {'SPLIT_N': 2048}),
                 ('split4608_w6', {'SPLIT_N': 4096, 'W': 6}),
-                ('w8', {'W': 8})]
+                ('w8', {'W': 8}),
+                ('tri1000', {'TRIDIAG_MIN_N': 1000}), ('tri500', {'TRIDIAG_MIN_N': 500}),
+                ('tri240', {'TRIDIAG_MIN_N': 240}), ('w2', {'W': 2}), ('w1', {'W': 1})]
     if len(sys.argv) > 1:
         variants = [v for v in variants if v[0] in sys.argv[1:]]
     res = {}
