@@ -339,10 +339,33 @@ def symeig_many(mats, clip=0.0, solver='auto'):
     return outs
 
 
-def inverse_many(mats, damping):
-    """(F + damping I)^-1 for symmetric positive definite F (Cholesky)."""
-    outs = []
-    for A in mats:
-        M = A + torch.diag(A.new_full((A.shape[0],), damping))
-        outs.append(torch.cholesky_inverse(torch.linalg.cholesky(M)))
+def inverse_many(mats, damping, check=True):
+    """(F + damping I)^-1 for symmetric positive definite F (Cholesky), the
+    reference's inverse path (kfac/layers/utils.py:76-96).
+
+    One batched potrf + potri per size class (ResNet-50: ~12 classes for 108
+    factors) instead of two library calls per matrix, and `cholesky_ex`: the
+    factorisation status of every class is checked with ONE host read at the
+    end instead of a device sync per matrix.  Results are views of the
+    per-class batch."""
+    outs = [None] * len(mats)
+    groups = {}
+    for i, A in enumerate(mats):
+        groups.setdefault((A.shape[0], A.dtype, A.device), []).append(i)
+    infos = []
+    for idx in groups.values():
+        M = torch.stack([mats[i] for i in idx])
+        M.diagonal(dim1=-2, dim2=-1).add_(damping)
+        L, info = torch.linalg.cholesky_ex(M)
+        inv = torch.cholesky_inverse(L)
+        infos.append((idx, info))
+        for k, i in enumerate(idx):
+            outs[i] = inv[k]
+    if check and infos:
+        bad = torch.cat([info.reshape(-1) for _, info in infos]).ne(0)
+        if bool(bad.any()):
+            flat = [i for idx, _ in infos for i in idx]
+            which = [flat[k] for k in bad.nonzero().reshape(-1).tolist()]
+            raise torch.linalg.LinAlgError(
+                'Cholesky of the damped factor(s) {} failed (not positive definite)'.format(which))
     return outs

@@ -1,5 +1,6 @@
 """CPU layer math: reference identities and helper round trips."""
 import torch
+import pytest
 
 from distributed_kfac_pytorch_amd.layers import utils as lutils
 from distributed_kfac_pytorch_amd.layers import Conv2dLayer, LinearLayer, LinearMultiLayer
@@ -95,3 +96,26 @@ def test_conv_dilation_factor():
     P = u.transpose(1, 2).reshape(-1, 18) / 36
     want = P.t() @ P / P.shape[0]
     assert torch.allclose(layer._get_A_factor([x]), want, atol=1e-6)
+
+
+def test_inverse_many_batched_classes_match_per_matrix():
+    """ops.eigen.inverse_many batches by size class; on CPU the batched LAPACK
+    calls reproduce the per-matrix reference path bit for bit."""
+    from distributed_kfac_pytorch_amd.ops import eigen as eigen_ops
+    g = torch.Generator().manual_seed(3)
+    mats = []
+    for n in (5, 9, 5, 12, 9, 5):
+        x = torch.randn(n, 2 * n, generator=g)
+        mats.append(x @ x.t() / (2 * n))
+    outs = eigen_ops.inverse_many(mats, 0.01)
+    for A, out in zip(mats, outs):
+        M = A + torch.diag(A.new_full((A.shape[0],), 0.01))
+        ref = torch.cholesky_inverse(torch.linalg.cholesky(M))
+        assert torch.equal(out, ref)
+
+
+def test_inverse_many_raises_on_indefinite():
+    from distributed_kfac_pytorch_amd.ops import eigen as eigen_ops
+    bad = -torch.eye(4)
+    with pytest.raises(torch.linalg.LinAlgError):
+        eigen_ops.inverse_many([torch.eye(4), bad], 0.001)
