@@ -9,6 +9,7 @@ recorded on the current stream around each K-FAC pipeline phase, resolved
 lazily so timing never forces a host sync inside `step()`.
 """
 import collections
+import os
 import time
 
 import torch
@@ -67,6 +68,15 @@ def _device_sync():
         torch.cuda.synchronize()
 
 
+def _roctx_ok():
+    try:
+        torch.cuda.nvtx.range_push('kfac/probe')
+        torch.cuda.nvtx.range_pop()
+        return True
+    except Exception:   # a torch build without roctx/nvtx bindings
+        return False
+
+
 class PhaseTimer(object):
     """Accumulates per-phase device time using events on the current stream.
 
@@ -77,8 +87,14 @@ class PhaseTimer(object):
     On CPU it falls back to perf_counter.
     """
 
-    def __init__(self, enabled=False):
+    def __init__(self, enabled=False, ranges=None):
         self.enabled = enabled
+        # roctx ranges 'kfac/<phase>' around every phase (torch.cuda.nvtx binds
+        # roctx on ROCm): visible to `rocprofv3 --marker-trace` without the
+        # timers' events.  KFAC_ROCTX=1 turns them on process-wide.
+        if ranges is None:
+            ranges = os.environ.get('KFAC_ROCTX', '0') not in ('', '0')
+        self.ranges = bool(ranges) and _roctx_ok()
         self._pending = []           # (name, start_event, end_event)
         self._totals = collections.defaultdict(float)
         self._counts = collections.defaultdict(int)
@@ -88,6 +104,8 @@ class PhaseTimer(object):
             self.timer, self.name = timer, name
 
         def __enter__(self):
+            if self.timer.ranges:
+                torch.cuda.nvtx.range_push('kfac/' + self.name)
             if not self.timer.enabled:
                 return self
             if torch.cuda.is_available() and torch.cuda.is_initialized():
@@ -98,6 +116,8 @@ class PhaseTimer(object):
             return self
 
         def __exit__(self, *exc):
+            if self.timer.ranges:
+                torch.cuda.nvtx.range_pop()
             if not self.timer.enabled:
                 return False
             if isinstance(self.start, float):

@@ -18,3 +18,23 @@ def test_checksums_detect_transpose_and_nan():
 
 def test_assert_consistent_single_process_is_noop():
     comm_check.assert_consistent([('x', torch.ones(3))], 'phase')
+
+
+def test_phase_timer_roctx_ranges_balanced(monkeypatch):
+    """PhaseTimer(ranges=True) pushes one 'kfac/<phase>' range per phase and
+    pops it on exit, also when the phase raises."""
+    from distributed_kfac_pytorch_amd.utils import tracing
+    pushed = []
+    monkeypatch.setattr(torch.cuda.nvtx, 'range_push', lambda n: pushed.append(n) or 0)
+    monkeypatch.setattr(torch.cuda.nvtx, 'range_pop', lambda: pushed.pop() and 0)
+    t = tracing.PhaseTimer(enabled=True, ranges=True)
+    with t('factors'):
+        assert pushed == ['kfac/factors']
+    assert pushed == []
+    try:
+        with t('inverses'):
+            raise ValueError('x')
+    except ValueError:
+        pass
+    assert pushed == []
+    assert 'factors' in t.summary()
