@@ -60,6 +60,10 @@ CASES = [
     (4, {'method': 'COMM_OPT', 'prediv': False}),
     (2, {'method': 'COMM_OPT', 'eigen': False}),
     (4, {'method': 'MEM_OPT', 'eigen': False}),
+    # world 8 = one MI355X node's rank count
+    (8, {'method': 'COMM_OPT'}),
+    (8, {'method': 'MEM_OPT'}),
+    (8, {'method': 'HYBRID_OPT', 'fraction': 0.25}),
 ]
 
 
@@ -70,13 +74,29 @@ def test_strategy_equivalence(tmp_path, world, cfg):
     cfg = dict(cfg, steps=4)
     ref_grads, ref_factors = _single(cfg)
     _spawn(_dist_worker.kfac_strategy, world, tmp_path, cfg)
+    # world 2 and 4: the averaged sum of identical tensors is exact (x+x,
+    # (x+x)+(x+x)), so every strategy is BIT-identical to world 1.  World 8:
+    # gloo's ring accumulates 3x, 5x, ... which round, so the factors differ
+    # from world 1 in the last bit (~1e-8); there the ranks must still agree
+    # bit for bit with each other and match world 1 to fp32 round-off.
+    exact = world in (2, 4)
+
+    def same(a, b):
+        return torch.equal(a, b) if exact else torch.allclose(a, b, rtol=1e-4, atol=1e-6)
+
+    res0 = None
     for r in range(world):
         res = torch.load(os.path.join(str(tmp_path), 'rank{}.pt'.format(r)), weights_only=True)
         for step, (gs, rs) in enumerate(zip(res['grads'], ref_grads)):
             for a, b in zip(gs, rs):
-                assert torch.equal(a, b), (r, step, (a - b).abs().max().item())
+                assert same(a, b), (r, step, (a - b).abs().max().item())
         for (a, g), (ra, rg) in zip(res['factors'], ref_factors):
-            assert torch.equal(a, ra) and torch.equal(g, rg)
+            assert same(a, ra) and same(g, rg)
+        if res0 is None:
+            res0 = res
+        else:
+            for gs, g0 in zip(res['grads'], res0['grads']):
+                assert all(torch.equal(a, b) for a, b in zip(gs, g0)), r
 
 
 def test_distribute_layer_factors_without_prediv(tmp_path):
