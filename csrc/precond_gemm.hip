@@ -60,7 +60,9 @@ constexpr int TK = 32;
 
 // WPE: minimum waves per SIMD the register allocator must allow (1 = no
 // constraint).  WPE 6 fits three 8-wave workgroups per CU (80 VGPRs).
-template <int PREC, int BM, int BN, int WM, int WN, int WPE = 1>
+// DBUF: two LDS images -- the next k-step is stored into the idle image
+// right after the MFMAs, one barrier per k-step instead of two.
+template <int PREC, int BM, int BN, int WM, int WN, int WPE = 1, bool DBUF = false>
 __global__ __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(WPE)))
 void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict__ kl) {
   constexpr bool X3 = (PREC == PREC_BF16X3);
@@ -70,7 +72,7 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   constexpr int LDF32 = TK + 4;   // 16-byte aligned chunk writes
   // one LDS array (guide: a second __shared__ object can de-pipeline loads)
   constexpr int LDS_BYTES = X3 ? (2 * (BM + BN) * LDB16 * 2) : ((BM + BN) * LDF32 * 4);
-  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES * (DBUF ? 2 : 1)];
 
   const int pi = find_problem(table, count, blockIdx.x);
   const PGemm& P = table[pi];
@@ -114,20 +116,20 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
     }
   };
   // LDS image: [A hi | A lo | B hi | B lo] rows of LDB16 bf16 (X3) or [A | B] rows of LDF32 f32
-  auto store = [&]() {
+  auto store = [&](unsigned char* img) {
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
       const int c = tid + NT * q;
       const int plane = c / (BM * CPR), row = (c % (BM * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
-      if (X3) *(uint4*)((uint16_t*)smem + (plane * BM + row) * LDB16 + kof) = ra[q];
-      else *(uint4*)((float*)smem + row * LDF32 + kof) = ra[q];
+      if (X3) *(uint4*)((uint16_t*)img + (plane * BM + row) * LDB16 + kof) = ra[q];
+      else *(uint4*)((float*)img + row * LDF32 + kof) = ra[q];
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
       const int c = tid + NT * q;
       const int plane = c / (BN * CPR), row = (c % (BN * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
-      if (X3) *(uint4*)((uint16_t*)smem + (2 * BM + plane * BN + row) * LDB16 + kof) = rb[q];
-      else *(uint4*)((float*)smem + (BM + row) * LDF32 + kof) = rb[q];
+      if (X3) *(uint4*)((uint16_t*)img + (2 * BM + plane * BN + row) * LDB16 + kof) = rb[q];
+      else *(uint4*)((float*)img + (BM + row) * LDF32 + kof) = rb[q];
     }
   };
 
@@ -141,12 +143,21 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
 
   const int arow0 = wr * (BM / WM), brow0 = wc * (BN / WN);
   load(0);
-  for (int ks = 0; ks < ksteps; ++ks) {
-    store();
+  if constexpr (DBUF) {
+    store(smem);
     __syncthreads();
+  }
+  for (int ks = 0; ks < ksteps; ++ks) {
+    unsigned char* cur = smem;
+    if constexpr (DBUF) {
+      cur = smem + (ks & 1) * LDS_BYTES;
+    } else {
+      store(smem);
+      __syncthreads();
+    }
     if (ks + 1 < ksteps) load((ks + 1) * TK);   // global loads in flight under the MFMAs
     if constexpr (X3) {
-      const uint16_t* sAh = (const uint16_t*)smem;
+      const uint16_t* sAh = (const uint16_t*)cur;
       const uint16_t* sAl = sAh + BM * LDB16;
       const uint16_t* sBh = sAh + 2 * BM * LDB16;
       const uint16_t* sBl = sBh + BN * LDB16;
@@ -173,7 +184,7 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
         }
       }
     } else {
-      const float* sA = (const float*)smem;
+      const float* sA = (const float*)cur;
       const float* sB = sA + BM * LDF32;
 #pragma unroll
       for (int kk = 0; kk < TK / 2; ++kk) {
@@ -188,6 +199,10 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b[j], acc[i][j], 0, 0, 0);
         }
       }
+    }
+    if constexpr (DBUF) {
+      // the idle image was last read in iteration ks-1, before its barrier
+      if (ks + 1 < ksteps) store(smem + ((ks + 1) & 1) * LDS_BYTES);
     }
     __syncthreads();
   }
@@ -379,6 +394,8 @@ KFAC_API int kfac_pgemm(int prec, int tile, const void* dev_table, int count, in
     case 7: hipLaunchKernelGGL((pgemm_kernel<P, 128, 256, 2, 4>), g, dim3(512), 0, stream, t, count, kl); break; \
     case 8: hipLaunchKernelGGL((pgemm_kernel<P, 128, 128, 4, 2, 6>), g, dim3(512), 0, stream, t, count, kl); break; \
     case 9: hipLaunchKernelGGL((pgemm_kernel<P, 128, 128, 4, 2, 5>), g, dim3(512), 0, stream, t, count, kl); break; \
+    case 10: hipLaunchKernelGGL((pgemm_kernel<P, 128, 128, 4, 2, 1, true>), g, dim3(512), 0, stream, t, count, kl); break; \
+    case 11: hipLaunchKernelGGL((pgemm_kernel<P, 128, 128, 4, 4, 1, true>), g, dim3(1024), 0, stream, t, count, kl); break; \
     default: hipLaunchKernelGGL((pgemm_kernel<P, 128, 128, 2, 2>), g, dim3(256), 0, stream, t, count, kl); break; \
   }
   if (prec == PREC_BF16X3) {

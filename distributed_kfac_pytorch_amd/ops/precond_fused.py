@@ -26,6 +26,8 @@ share a mutable table.
 """
 import ctypes
 
+import os
+
 import torch
 
 from . import _lib
@@ -41,12 +43,15 @@ BIG_TILE = 256    # big tile class: half the operand traffic per FLOP
 BIG_TILES = False  # measured 2.7x slower on ResNet-50 (profiles/r1_pgemm_variants.log)
 # kernel tile configurations of csrc/precond_gemm.hip: id -> (BM, BN)
 TILE_SHAPES = {0: (128, 128), 1: (256, 256), 2: (64, 64), 3: (128, 128), 4: (128, 64),
-               5: (128, 128), 6: (256, 128), 7: (128, 256), 8: (128, 128), 9: (128, 128)}
+               5: (128, 128), 6: (256, 128), 7: (128, 256), 8: (128, 128), 9: (128, 128),
+               10: (128, 128), 11: (128, 128)}
 # tile configuration of every problem not in the big class, per precision
 # (profiles/r1_pgemm_variants.md: bf16x3 128x128 with 8 waves 1.64 ms vs 1.94
 # ms with 4 waves; fp32 128x128 with 16 waves 2.98 ms vs 3.55 ms)
 TILE_CFG_DEFAULT = {'bf16x3': 3, 'fp32': 5}
-TILE_CFG = None    # None: per-precision default
+# None: per-precision default; KFAC_PGEMM_TILE_CFG=<id> forces one (experiments, tests)
+TILE_CFG = int(os.environ['KFAC_PGEMM_TILE_CFG']) if os.environ.get('KFAC_PGEMM_TILE_CFG') \
+    else None
 
 
 def _tile_class(M, N, precision):
