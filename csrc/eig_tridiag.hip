@@ -27,7 +27,7 @@
 // row j is "column j".  Output: d, e, tau and the reflectors in row j
 // (e_j at j+1, v[1:] from j+2): the layout rocSOLVER's ormtr (lower) reads.
 // Reference semantics: kfac/layers/utils.py:45-74 (symeig).  The algorithm is
-// modelled phase by phase in scripts/probes/sytrd_model.py.
+// modelled phase by phase in scripts/models/sytrd_model.py.
 #include "common.h"
 
 #include <map>

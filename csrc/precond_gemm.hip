@@ -80,6 +80,9 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   const int tm = local / P.tiles_n, tn = local - tm * P.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int M = P.M, N = P.N;
+  // device-sized problems (csrc/eig_dc.hip patches M / K at run time and
+  // launches the worst-case tile grid): tiles past the problem exit at once
+  if (m0 >= M || n0 >= N) return;
   const int ksteps = (P.K + TK - 1) / TK;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;

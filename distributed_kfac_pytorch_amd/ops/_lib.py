@@ -39,6 +39,18 @@ class EigRecord(ctypes.Structure):
     _fields_ = [('A', c_vp), ('Q', c_vp), ('d', c_vp), ('Vt', c_vp), ('n', c_ll)]
 
 
+class ReduceRecord(ctypes.Structure):
+    # csrc/eig_reduce.hip KfacReduceRecord
+    _fields_ = [('A', c_vp), ('lda', c_ll), ('d', c_vp), ('e', c_vp), ('tau', c_vp),
+                ('ws', c_vp), ('n', c_ll)]
+
+
+class DcRecord(ctypes.Structure):
+    # csrc/eig_dc.hip KfacDcRecord
+    _fields_ = [('d', c_vp), ('e', c_vp), ('dout', c_vp), ('Zout', c_vp), ('ldz', c_ll),
+                ('ws', c_vp), ('n', c_ll)]
+
+
 _SIGS = {
     'kfac_syrk_patch': [c_int, c_vp, c_ll, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_int, c_int,
                         c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_vp, c_int,
@@ -86,10 +98,19 @@ _SIGS = {
     'kfac_gather_record_size': [],
     'kfac_split_record_size': [],
     'kfac_graph_fix_memsets': [c_vp, c_int, ctypes.POINTER(c_ll)],
+    'kfac_dc_batched': [ctypes.POINTER(DcRecord), c_int, c_int, c_vp],
+    'kfac_reduce_batched': [ctypes.POINTER(ReduceRecord), c_int, c_int, c_vp],
+    'kfac_reduce_prepare': [ctypes.POINTER(ReduceRecord), c_int],
+    'kfac_reduce_ws_floats': [c_int],
+    'kfac_reduce_stamps': [c_vp],
+    'kfac_dc_prepare': [ctypes.POINTER(DcRecord), c_int],
+    'kfac_dc_ws_bytes': [c_int],
+    'kfac_dc_info_offset': [c_int],
 }
 
 
-_RESTYPES = {'kfac_sytrd_ws_floats': c_ll, 'kfac_sytrd_forget': None}
+_RESTYPES = {'kfac_sytrd_ws_floats': c_ll, 'kfac_sytrd_forget': None, 'kfac_dc_ws_bytes': c_ll,
+             'kfac_reduce_ws_floats': c_ll}
 
 
 def _load():

@@ -27,12 +27,19 @@ from . import _lib
 __all__ = ['symeig_many', 'inverse_many', 'SMALL_N']
 
 SMALL_N = 192
-LARGE_PATH = os.environ.get('KFAC_EIG_LARGE', 'auto')
+# 'fused' (default): every large factor through ONE ragged fused reduction, ONE
+# batched divide and conquer and the WY back-transformation (no library
+# solver); 'auto' / 'tridiag' / 'syevd': the per-size-class paths of round 1
+LARGE_PATH = os.environ.get('KFAC_EIG_LARGE', 'fused')
+FUSED_MAX_N = 5120   # csrc/eig_reduce.hip NTMAX * TB (larger factors: per-class path)
 # 'auto': the hand-written path from this n up (it wins from 2048 on, rocSOLVER
 # syevd's latency per column wins below: profiles/r1_tridiag_vs_syevd.log)
 TRIDIAG_MIN_N = int(os.environ.get('KFAC_TRIDIAG_MIN_N', '2048'))
 TRIDIAG_GRAPH = bool(int(os.environ.get('KFAC_TRIDIAG_GRAPH', '1')))
 TRIDIAG_BACK = os.environ.get('KFAC_TRIDIAG_BACK', 'wy')   # 'wy' (batched GEMMs) | 'ormtr'
+# tridiagonal eigensolver: 'dc' = the hand-written batched divide and conquer
+# (csrc/eig_dc.hip), 'stedc' = rocSOLVER (A/B comparisons only)
+TRIDIAG_SOLVER = os.environ.get('KFAC_TRIDIAG_SOLVER', 'dc')
 BT = 128   # back-transformation block (csrc/eig_library.hip)
 # size classes from this n up are solved as concurrent single-matrix jobs
 # (default: never; rocSOLVER syevd batches beat concurrent singles,
@@ -128,8 +135,13 @@ def _tri_buffers(dev, n, b, slot=0):
         wsf = int(L.kfac_sytrd_ws_floats(n))
         f32 = dict(dtype=torch.float32, device=dev)
         nblk = (n + BT - 1) // BT
+        wsb = int(L.kfac_dc_ws_bytes(n))
+        rwsf = int(L.kfac_reduce_ws_floats(n))
         bufs = dict(lda=lda, A=torch.zeros(b, n, lda, **f32), Z=torch.zeros(b, n, lda, **f32),
                     d=torch.zeros(b, n, **f32), e=torch.zeros(b, n, **f32),
+                    w=torch.zeros(b, n, **f32), wsb=wsb,
+                    dcws=torch.zeros(b * wsb, dtype=torch.uint8, device=dev),
+                    rwsf=rwsf, rws=torch.zeros(b * rwsf, **f32),
                     tau=torch.zeros(b, n, **f32), ws=torch.zeros(b * wsf, **f32),
                     info=torch.zeros(b, dtype=torch.int32, device=dev),
                     T=torch.zeros(2 * b * nblk * BT * BT, **f32),
@@ -166,20 +178,86 @@ def _tridiag_class(mats, clip, stream, use_graph=None, slot=0):
                                                   _lib.ptr(B['Z']), lda, sA, n, b,
                                                   _lib.ptr(B['info']), cs),
                        'kfac_stedc_ormtr_batched')
-        else:
+            D = B['d'].clone()
+            _INFOS.append(B['info'].clone())
+        elif TRIDIAG_SOLVER == 'stedc':
             _lib.check(L.kfac_stedc_batched(_lib.ptr(B['d']), _lib.ptr(B['e']), _lib.ptr(B['Z']),
                                             lda, sA, n, b, _lib.ptr(B['info']), cs),
                        'kfac_stedc_batched')
             _lib.check(L.kfac_tridiag_backtransform(*_bt_args(B, n, b), int(use_graph), cs),
                        'kfac_tridiag_backtransform')
-        _INFOS.append(B['info'].clone())
+            D = B['d'].clone()
+            _INFOS.append(B['info'].clone())
+        else:
+            _lib.check(L.kfac_dc_batched(_dc_records(B, n, b), b, int(use_graph), cs),
+                       'kfac_dc_batched')
+            _lib.check(L.kfac_tridiag_backtransform(*_bt_args(B, n, b), int(use_graph), cs),
+                       'kfac_tridiag_backtransform')
+            D = B['w'].clone()
+            _INFOS.append(_dc_info(B, n, b))
         del _INFOS[:-256]
         # column-major eigenvector k (row k of Z) -> column k of a row-major Q
         Q = B['Z'][:, :, :n].transpose(1, 2).contiguous()
-        D = B['d'].clone()
         if clip is not None:
             D.clamp_(min=clip)
     return [(Q[i], D[i]) for i in range(b)]
+
+
+def _dc_records(B, n, b):
+    recs = (_lib.DcRecord * b)()
+    lda, wsb = B['lda'], B['wsb']
+    for i in range(b):
+        r = recs[i]
+        r.d = B['d'][i].data_ptr()
+        r.e = B['e'][i].data_ptr()
+        r.dout = B['w'][i].data_ptr()
+        r.Zout = B['Z'][i].data_ptr()
+        r.ldz = lda
+        r.ws = B['dcws'].data_ptr() + i * wsb
+        r.n = n
+    return recs
+
+
+def _dc_info(B, n, b):
+    """Per matrix: secular roots of the divide and conquer that hit the
+    iteration cap (device int in the workspace), as a (b,) int32 tensor."""
+    off = int(_lib.lib().kfac_dc_info_offset(n))
+    return B['dcws'].view(b, B['wsb'])[:, off:off + 4].contiguous().view(torch.int32).reshape(b)
+
+
+def tridiag_eigh(ds, es, use_graph=False):
+    """Eigen-decompose symmetric tridiagonal matrices (fp32 CUDA vectors d of
+    length n, e of length >= n-1) with ONE batched divide-and-conquer launch
+    sequence (csrc/eig_dc.hip; sizes may differ) -> [(w ascending, Z rows =
+    eigenvectors)]."""
+    L = _lib.lib()
+    dev = ds[0].device
+    recs = (_lib.DcRecord * len(ds))()
+    keep, outs = [], []
+    for i, (d, e) in enumerate(zip(ds, es)):
+        n = d.shape[0]
+        lda = (n + 63) // 64 * 64
+        dd = d.contiguous().float()
+        ee = torch.zeros(n, dtype=torch.float32, device=dev)
+        ee[:n - 1] = e[:n - 1]
+        w = torch.empty(n, dtype=torch.float32, device=dev)
+        Z = torch.empty(n, lda, dtype=torch.float32, device=dev)
+        ws = torch.empty(int(L.kfac_dc_ws_bytes(n)), dtype=torch.uint8, device=dev)
+        r = recs[i]
+        r.d, r.e, r.dout, r.Zout = dd.data_ptr(), ee.data_ptr(), w.data_ptr(), Z.data_ptr()
+        r.ldz, r.ws, r.n = lda, ws.data_ptr(), n
+        keep += [dd, ee, ws]
+        outs.append((w, Z, ws, n))
+    _lib.check(L.kfac_dc_batched(recs, len(ds), int(use_graph), _lib.stream(dev)),
+               'kfac_dc_batched')
+    infos = [ws[int(L.kfac_dc_info_offset(n)):][:4].view(torch.int32) for _, _, ws, n in outs]
+    res = [(w, Z[:, :n]) for w, Z, _, n in outs]
+    torch.cuda.current_stream(dev).synchronize()
+    del keep
+    bad = [int(i.item()) for i in infos]
+    if any(bad):
+        raise RuntimeError('divide and conquer: secular roots not converged {}'.format(bad))
+    return res
 
 
 def _bt_args(B, n, b):
@@ -200,6 +278,64 @@ def _tridiag_prepare(n, b, dev, slot=0):
                'kfac_sytrd_prepare')
     _lib.check(_lib.lib().kfac_backtransform_prepare(*_bt_args(B, n, b)),
                'kfac_backtransform_prepare')
+    if TRIDIAG_SOLVER == 'dc':
+        _lib.check(_lib.lib().kfac_dc_prepare(_dc_records(B, n, b), b), 'kfac_dc_prepare')
+
+
+def _large_fused(mats, clip, stream, use_graph=True):
+    """Every large factor of the inverse update in ONE ragged launch sequence
+    per stage: the fused one-launch-per-column reduction over all matrices
+    (csrc/eig_reduce.hip), the batched divide and conquer over all matrices
+    (csrc/eig_dc.hip), then the compact-WY back-transformation per size class
+    (csrc/eig_library.hip).  No library solver, no host round trip; each stage
+    is a cached hipGraph."""
+    dev = mats[0].device
+    L = _lib.lib()
+    classes = {}
+    for i, A in enumerate(mats):
+        classes.setdefault(A.shape[0], []).append(i)
+    order = sorted(classes.items(), key=lambda kv: -kv[0])
+    total = len(mats)
+    outs = [None] * total
+    with torch.cuda.stream(stream):
+        cs = _lib.c_vp(stream.cuda_stream)
+        rr = (_lib.ReduceRecord * total)()
+        dr = (_lib.DcRecord * total)()
+        k = 0
+        bufs = []
+        for n, idx in order:
+            b = len(idx)
+            B = _tri_buffers(dev, n, b)
+            bufs.append((n, idx, B))
+            for i, m in enumerate(idx):
+                B['A'][i, :, :n].copy_(mats[m])
+            dcr = _dc_records(B, n, b)
+            for i in range(b):
+                r = rr[k]
+                r.A = B['A'][i].data_ptr()
+                r.lda = B['lda']
+                r.d = B['d'][i].data_ptr()
+                r.e = B['e'][i].data_ptr()
+                r.tau = B['tau'][i].data_ptr()
+                r.ws = B['rws'].data_ptr() + 4 * i * B['rwsf']
+                r.n = n
+                dr[k] = dcr[i]
+                k += 1
+        _lib.check(L.kfac_reduce_batched(rr, total, int(use_graph), cs), 'kfac_reduce_batched')
+        _lib.check(L.kfac_dc_batched(dr, total, int(use_graph), cs), 'kfac_dc_batched')
+        for n, idx, B in bufs:
+            b = len(idx)
+            _lib.check(L.kfac_tridiag_backtransform(*_bt_args(B, n, b), int(use_graph), cs),
+                       'kfac_tridiag_backtransform')
+            _INFOS.append(_dc_info(B, n, b))
+            Q = B['Z'][:, :, :n].transpose(1, 2).contiguous()
+            D = B['w'].clone()
+            if clip is not None:
+                D.clamp_(min=clip)
+            for i, m in enumerate(idx):
+                outs[m] = (Q[i], D[i])
+        del _INFOS[:-256]
+    return outs
 
 
 def _class_solver(n):
@@ -333,8 +469,16 @@ def symeig_many(mats, clip=0.0, solver='auto'):
         for i, r in zip(small, _jacobi_small([mats[i] for i in small], clip)):
             outs[i] = r
     if large:
-        workers = 1 if solver == 'serial' else None
-        for i, r in zip(large, _library_eigh([mats[i] for i in large], clip, workers)):
+        sub = [mats[i] for i in large]
+        if LARGE_PATH == 'fused' and max(A.shape[0] for A in sub) <= FUSED_MAX_N:
+            cur = torch.cuda.current_stream(sub[0].device)
+            res = _large_fused(sub, clip, cur)
+            for A in sub:
+                A.record_stream(cur)
+        else:
+            workers = 1 if solver == 'serial' else None
+            res = _library_eigh(sub, clip, workers)
+        for i, r in zip(large, res):
             outs[i] = r
     return outs
 

@@ -37,17 +37,23 @@ def main():
         x = torch.randn(n, max(64, n // 2), device=dev, generator=g)
         mats.append(x @ x.t() / x.shape[1] + 1e-3 * torch.eye(n, device=dev))
     print('factors', len(ns), 'sum n^3 %.3g' % sum(float(n) ** 3 for n in ns), flush=True)
-    variants = [('default', {}), ('split4608', {'SPLIT_N': 4096}),
+    variants = [('default', {}), ('r1_auto', {'LARGE': 'auto', 'SOLVER': 'stedc'}),
+                ('auto_dc', {'LARGE': 'auto'}), ('split4608', {'SPLIT_N': 4096}),
                 ('split2048', {'SPLIT_N': 2048}),
                 ('split4608_w6', {'SPLIT_N': 4096, 'W': 6}),
                 ('w8', {'W': 8}),
                 ('tri1000', {'TRIDIAG_MIN_N': 1000}), ('tri500', {'TRIDIAG_MIN_N': 500}),
-                ('tri240', {'TRIDIAG_MIN_N': 240}), ('w2', {'W': 2}), ('w1', {'W': 1})]
+                ('tri240', {'TRIDIAG_MIN_N': 240}), ('tri193', {'TRIDIAG_MIN_N': 193}),
+                ('stedc', {'SOLVER': 'stedc'}), ('stedc_tri193', {'SOLVER': 'stedc', 'TRIDIAG_MIN_N': 193}),
+                ('w2', {'W': 2}), ('w1', {'W': 1})]
     if len(sys.argv) > 1:
         variants = [v for v in variants if v[0] in sys.argv[1:]]
     res = {}
-    base = dict(SPLIT_N=eigen.SPLIT_N, TRIDIAG_MIN_N=eigen.TRIDIAG_MIN_N)
+    base = dict(SPLIT_N=eigen.SPLIT_N, TRIDIAG_MIN_N=eigen.TRIDIAG_MIN_N,
+                SOLVER=eigen.TRIDIAG_SOLVER, LARGE=eigen.LARGE_PATH)
     for name, cfg in variants:
+        eigen.LARGE_PATH = cfg.get('LARGE', base['LARGE'])
+        eigen.TRIDIAG_SOLVER = cfg.get('SOLVER', base['SOLVER'])
         eigen.SPLIT_N = cfg.get('SPLIT_N', base['SPLIT_N'])
         eigen.TRIDIAG_MIN_N = cfg.get('TRIDIAG_MIN_N', base['TRIDIAG_MIN_N'])
         if 'W' in cfg:

@@ -1,5 +1,5 @@
 """CPU check of the blocked tridiagonalisation algorithm that csrc/eig_tridiag.hip
-implements (NumPy model in scripts/probes/sytrd_model.py, fp64)."""
+implements (NumPy model in scripts/models/sytrd_model.py, fp64)."""
 import importlib.util
 import os
 
@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _model():
     spec = importlib.util.spec_from_file_location(
-        'sytrd_model', os.path.join(ROOT, 'scripts', 'probes', 'sytrd_model.py'))
+        'sytrd_model', os.path.join(ROOT, 'scripts', 'models', 'sytrd_model.py'))
     m = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(m)
     return m
