@@ -61,9 +61,13 @@ def parse():
     ap.add_argument('--profile-phases', action='store_true')
     ap.add_argument('--check-finite', action='store_true',
                     help='debug: sync and print the loss of every timed step')
-    ap.add_argument('--precond-precision', default='bf16x3', choices=['fp32', 'bf16x3'],
-                    help='fused preconditioning GEMM precision (library default: fp32; '
-                         'bf16x3 = split-bf16 MFMA, ~1e-5 relative error)')
+    ap.add_argument('--precond-precision', default='fp32', choices=['fp32', 'bf16x3'],
+                    help='fused preconditioning GEMM precision: fp32 (reference precision, '
+                         'exact-f32 MFMA; the default) or bf16x3 (split-bf16 MFMA, ~1e-5 '
+                         'relative error, opt-in)')
+    ap.add_argument('--sgd-delta', type=int, default=1,
+                    help='also time the same steps without K-FAC (hooks removed) and report '
+                         'the per-step K-FAC cost (kfac_step_ms)')
     ap.add_argument('--graphs', type=int, default=1,
                     help='hipGraph capture of the training step (1/0)')
     ap.add_argument('--set-to-none', type=int, default=1,
@@ -77,6 +81,62 @@ def parse():
     ap.add_argument('--ddp', action='store_true',
                     help='eager torch DDP instead of the graphed flat-arena all-reduce')
     return ap.parse_args()
+
+
+def _mark(device):
+    if device.type == 'cuda':
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+    return time.perf_counter()
+
+
+def step_kind(pre):
+    if pre is None:
+        return 'plain'
+    p = pre.param_groups[0]
+    if p['step'] % p['inv_update_freq'] == 0:
+        return 'inverse'
+    if p['step'] % p['factor_update_freq'] == 0:
+        return 'factor'
+    return 'plain'
+
+
+def time_sgd_only(args, model, opt, pre, forward_backward, grad_sync, use_graphs, device):
+    """The same training step without K-FAC (hooks removed, plain SGD update),
+    timed over the same number of steps: the baseline for kfac_step_ms."""
+    pre.remove_hooks()
+
+    def update():
+        opt.step()
+
+    if grad_sync is not None:
+        step = graphs.GraphedTrainStep(None, None, [opt], enabled=use_graphs,
+                                       forward_backward=forward_backward,
+                                       communicate=grad_sync, update=update)
+    else:
+        def train_step():
+            loss = forward_backward()
+            update()
+            return loss
+        step = graphs.GraphedTrainStep(train_step, None, [opt], enabled=use_graphs)
+    for _ in range(3):
+        step()
+    step.prepare()
+    if dist.is_initialized():
+        dist.barrier()
+    if device.type == 'cuda':
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if device.type == 'cuda':
+        torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=device)
+    if dist.is_initialized():
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item()) / args.steps * 1e3
 
 
 def main():
@@ -160,19 +220,28 @@ def main():
         if os.environ.get('KFAC_PROFILE_MARKER'):
             torch.cuda._sleep(1000)   # 'spin' kernel: start of the timed window in a trace
         torch.cuda.synchronize()
+    # per-step device time by step kind: events between steps (graphs stay on)
+    kinds, events = [], []
     t0 = time.perf_counter()
     for i in range(args.steps):
+        kinds.append(step_kind(pre))
+        events.append(_mark(device))
         loss = step()
         if args.check_finite:
             kl = float(pre.fused.kl) if (pre is not None and pre.fused is not None) else 0.0
             print('step', i, 'loss', float(loss.item()), 'kl', kl, flush=True)
     if pre is not None:
         pre.wait_inverses()   # a lagged solve launched in the window is timed in full
+    events.append(_mark(device))
     if device.type == 'cuda':
         torch.cuda.synchronize()
     if dist.is_initialized():
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    per_kind = {}
+    for k, a, b in zip(kinds, events[:-1], events[1:]):
+        per_kind.setdefault(k, []).append(a.elapsed_time(b) if device.type == 'cuda'
+                                          else (b - a) * 1e3)
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -182,6 +251,10 @@ def main():
     gbatch = B * world
     value = gbatch * args.steps / elapsed
     phases = pre.timer.summary() if (pre is not None and args.profile_phases) else None
+    sgd_ms = None
+    if pre is not None and args.sgd_delta:
+        sgd_ms = time_sgd_only(args, model, opt, pre, forward_backward, grad_sync, use_graphs,
+                               device)
     if rank == 0:
         rec = {
             'metric': METRIC if pre is not None else 'images/sec (whole node) ResNet-50 SGD-only',
@@ -211,9 +284,30 @@ def main():
                                          ('flat-arena' if world > 1 else None),
                        'final_loss': round(float(loss.item()), 4)},
         }
+        if per_kind:
+            rec['step_ms_by_kind'] = {k: round(sum(v) / len(v), 3) for k, v in per_kind.items()}
+            rec['steps_by_kind'] = {k: len(v) for k, v in per_kind.items()}
+        if pre is not None and sgd_ms is not None:
+            rec['sgd_only_ms_per_step'] = round(sgd_ms, 3)
+            kk = {k: round(sum(v) / len(v) - sgd_ms, 3) for k, v in per_kind.items()}
+            ff, inv = args.kfac_cov_update_freq, args.kfac_update_freq
+            mix = {'inverse': 1.0 / inv, 'factor': (inv // ff - 1.0) / inv}
+            mix['plain'] = 1.0 - mix['inverse'] - mix['factor']
+            steady = sum(mix[k] * (sum(v) / len(v)) for k, v in per_kind.items()) \
+                if set(per_kind) >= set(mix) else None
+            rec['kfac_step_ms'] = {
+                'window_mean': round(ms - sgd_ms, 3),
+                'by_kind': kk,
+                'steady_state_mix': None if steady is None else round(steady - sgd_ms, 3),
+                'steady_state_images_per_sec': None if steady is None else
+                round(gbatch * 1e3 / steady, 1),
+                'note': 'K-FAC cost per step over the same model/steps without K-FAC; '
+                        'steady_state_mix weights the measured kinds by the reference '
+                        'schedule (1 inverse + {} factor steps per {})'.format(
+                            inv // ff - 1, inv)}
         if phases is not None:
             rec['kfac_phase_ms_total'] = {k: round(v, 2) for k, v in phases.items()}
-            rec['kfac_step_ms'] = round(sum(phases.values()) / args.steps, 3)
+            rec['kfac_phase_ms_per_step'] = round(sum(phases.values()) / args.steps, 3)
         print(json.dumps(rec), flush=True)
     if dist.is_initialized():
         dist.barrier()

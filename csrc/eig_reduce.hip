@@ -1,35 +1,33 @@
-// Fused Householder tridiagonalisation: ONE launch per column for a ragged
-// batch of K-FAC factors (replaces the 3-launch-per-column
-// csrc/eig_tridiag.hip path and rocSOLVER's sytrd).
+// Batched Householder tridiagonalisation for a ragged batch of K-FAC factors
+// (replaces rocSOLVER's sytrd and the round-1 per-class
+// csrc/eig_tridiag.hip path).
 //
-// The reduction is a chain of n dependent columns; on MI355X each kernel
-// boundary costs ~1.5-3 us, so the launch count per column sets the floor
-// (profiles/r1_tridiag_kernel_stats_4608x3.csv: 3 launches = 20 us/column).
-// Launch K(j) does, for EVERY matrix of the batch that still has column j:
+// The reduction is a chain of n dependent columns, so what a column costs in
+// launches and per-workgroup latency sets the speed; every matrix of the
+// inverse update (all sizes) advances through ONE launch sequence:
 //
-//   step 1  the Householder scalars of column j-1 from the partial sums the
-//           previous launch left (|xh|^2, W^T xh, V^T xh, xh.a, xh^T yh:
-//           per-block / per-tile partials re-reduced in a fixed order, so the
-//           result is deterministic -- no atomics)
-//   step 2  w_{j-1} = tau (a + s yh - V s1 - W s2) + alpha2 v for the rows the
-//           workgroup needs; the diagonal-tile workgroups store W/V columns,
-//           the reflector row and the next vector
-//   panel   at a panel start (every NB columns) the tile is updated in place,
-//           A -= V W^T + W V^T, before it is used
-//   step 3  x_j = base row j - V W[j]^T - W V[j]^T, kept UNNORMALISED (xh):
-//           its Householder scale needs a global norm that only the next
-//           launch knows -- y_j = a_j + s_j A22 xh_j is linear in the scale
-//   step 4  yh = A22 xh over the upper 128 x 128 tiles (each off-diagonal
-//           tile feeds both its row and its column block: half the traffic of
-//           a full mat-vec), per-tile partials
+//   fin(j)   one workgroup per 256 rows (each row's work done once):
+//            step 1  Householder scalars of column j-1 from the previous
+//                    launches' partial sums (|xh|^2, W^T xh, V^T xh, xh.a,
+//                    xh^T yh), re-reduced in a fixed order: deterministic
+//            step 2  w_{j-1} = tau (a + s yh - V s1 - W s2) + alpha2 v -> the
+//                    panel columns W/V[:, c-1], reflector row j-1, d/e/tau
+//            step 3  x_j = A row j - V W[j]^T - W V[j]^T, kept UNNORMALISED
+//                    (xh): its Householder scale needs a global norm that
+//                    only the next fin knows; y_j = a_j + s_j A22 xh_j is
+//                    linear in the scale.  Partial sums for fin(j+1).
+//   upd(j)   every NB = 32 columns: A22 -= V W^T + W V^T on the upper 128 x
+//            128 tiles, exact-f32 MFMA (v_mfma_f32_32x32x2_f32)
+//   symv(j)  yh = A22 xh over the upper tiles (an off-diagonal tile feeds its
+//            row and its column block: half the traffic of a full mat-vec),
+//            per-tile partials; lean (tile + 256 floats in, no panel data) so
+//            the bandwidth-bound early columns run at high occupancy
 //
-// Base rows j, j+1 come from a snapshot the previous launch took, so a launch
-// that rewrites tiles (panel start) never reads rows another workgroup of the
-// same launch is writing.  The recurrence is modelled exactly (fp64, 1e-15)
-// in scripts/models/sytrd_fused_model.py.  Storage as before: row-major,
-// UPPER triangle maintained (== LAPACK lower, column-major); output d, e, tau
-// and reflector j in row j (beta at j+1, v[2:] after) -- the layout the
-// compact-WY back-transformation (csrc/eig_library.hip) reads.
+// The recurrence (unnormalised xh, scalars one launch late) is modelled
+// exactly in scripts/models/sytrd_fused_model.py (fp64, 1e-15).  Storage:
+// row-major, UPPER triangle maintained (== LAPACK lower, column-major); output
+// d, e, tau and reflector j in row j (beta at j+1, v[2:] after): the layout
+// the compact-WY back-transformation (csrc/eig_library.hip) reads.
 #include "common.h"
 
 #include <algorithm>
@@ -42,37 +40,36 @@
 namespace {
 
 constexpr int TB = 128;        // symv / update tile
+constexpr int FB = 256;        // rows per fin workgroup
 constexpr int NB = 32;         // panel width
-constexpr int RSW = 2 + 2 * NB + 2;   // row-block partials: |xh|^2, xh.a, W^T xh, V^T xh (+pad)
-constexpr int MAXM = 255;      // matrices per batch (one launch-offset row each)
-constexpr int NTMAX = 40;      // row blocks (n <= 5120): partial loads stay in registers
+constexpr int RSW = 2 + 2 * NB + 2;   // fin partials: |xh|^2, xh.a, W^T xh, V^T xh (+pad)
+constexpr int MAXM = 255;      // matrices per batch
+constexpr int NTMAX = 40;      // 128-row blocks (n <= 5120)
 constexpr int PQ4 = NTMAX / 4; // float4 loads of a row's yh partials
-constexpr int RSL = (NTMAX * RSW + 255) / 256;    // row-block partial loads per thread
-constexpr int TSL = (NTMAX * NTMAX + 255) / 256;  // tile partial loads per thread
-
-// debug: per-launch phase stamps of workgroup 0 (s_memrealtime, 100 MHz),
-// enabled by kfac_reduce_stamps(buffer); null in normal runs
-__device__ unsigned long long* g_stamps = nullptr;
-#define STAMP(k)                                                                     \
-  do {                                                                               \
-    if (stamps && tid == 0) stamps[(long long)j * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
+constexpr int NFMAX = (NTMAX * TB + FB - 1) / FB;   // fin blocks
+constexpr int TSL = (NTMAX * 64 + 255) / 256;       // tile partial loads per thread
+constexpr int TWS = FB + 1;    // LDS stride of the fin partial transpose
 
 struct RMat {
-  float* A; long long lda; int n; int nt;
+  float* A; long long lda; int n; int nt; int nf; int pad;
   float* d; float* e; float* tau;
   float* V; float* W;                     // n x NB (row r: NB floats)
-  float* P; float* TS; float* RS; float* XH; float* SN; float* SC;
-  long long sP, sTS, sRS, sXH, sSN;       // slot strides (floats); 2 slots each
+  float* P; float* TS; float* RS; float* XH; float* SC;
+  long long sP, sTS, sRS, sXH;            // slot strides (floats); 2 slots each
 };
+
+// debug: per-launch phase stamps of workgroup 0 of fin (s_memrealtime, 100 MHz)
+__device__ unsigned long long* g_stamps = nullptr;
+#define STAMP(k)                                                                            \
+  do {                                                                                      \
+    if (stamps && tid == 0) stamps[(long long)j * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 
 __device__ inline void tri_index(int t, int mb, int& I, int& K) {
   int i = 0;
   while (t >= mb - i) { t -= mb - i; ++i; }
   I = i; K = i + t;
 }
-
-__device__ inline int tri(int m) { return m * (m + 1) / 2; }
 
 __device__ inline void hh_scalars(double alpha, double sig2, double& beta, double& tau,
                                   double& s) {
@@ -85,134 +82,93 @@ __device__ inline void hh_scalars(double alpha, double sig2, double& beta, doubl
   }
 }
 
-// copy base rows 0 and 1 into snapshot slot 1 (read by K(0))
-__global__ __launch_bounds__(256) void reduce_prep_kernel(const RMat* __restrict__ mats) {
-  const RMat M = mats[blockIdx.y];
-  float* sn = M.SN + M.sSN;   // slot 1
-  for (int r = blockIdx.x * 256 + threadIdx.x; r < M.n; r += gridDim.x * 256) {
-    sn[r] = M.A[r];                                   // row 0 (upper: all columns)
-    sn[M.n + r] = (r >= 1) ? M.A[M.lda + r] : 0.f;    // row 1, columns >= 1
+// workgroup -> (matrix, local index) from the launch's host-built offsets
+__device__ inline void map_block(const int* __restrict__ offs, int nact, int* soff, int& mat,
+                                 int& local) {
+  __shared__ int sm[2];
+  if ((int)threadIdx.x <= nact) soff[threadIdx.x] = offs[threadIdx.x];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int b = blockIdx.x;
+    int mi = 0;
+    while (mi + 1 < nact && soff[mi + 1] <= b) ++mi;
+    sm[0] = mi;
+    sm[1] = b - soff[mi];
   }
+  __syncthreads();
+  mat = sm[0];
+  local = sm[1];
 }
 
-struct Shared {
-  // step 1 / scalar rows
-  double scal[8];                 // beta, tau, s, alpha2, prev d, alpha
+// ------------------------------------------------------------------- fin
+struct FinShared {
+  double scal[8];                 // beta, tau, s, alpha2, prev d
+  double red[3 * RSW + 8];
   float s12[2 * NB];              // s1, s2
   float vwj[4][NB];               // V[j], W[j], V[j+1], W[j+1] (full panel columns)
-  double red[4 * RSW];
-  // symv
-  float sv[2][TB];
-  float rowred[TB][33];
-  float colred[4][TB];
-  int mat, tile;
 };
 
-__global__ __launch_bounds__(256) void sytrd_col_kernel(const RMat* __restrict__ mats,
+__global__ __launch_bounds__(256) void sytrd_fin_kernel(const RMat* __restrict__ mats,
                                                         const int* __restrict__ offs, int nact,
                                                         int j) {
-  extern __shared__ __attribute__((aligned(16))) float upd[];   // panel start: V/W rows
-  __shared__ Shared S;
+  extern __shared__ __attribute__((aligned(16))) float tw[];    // [RSW][TWS] partial transpose
+  __shared__ FinShared S;
   __shared__ int soff[MAXM + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   unsigned long long* const stamps = blockIdx.x == 0 ? g_stamps : nullptr;
   STAMP(0);
-  // ---- workgroup -> (matrix, tile): this launch's tile offsets (host-built,
-  //      one parallel load) searched in LDS
-  if (tid <= nact) soff[tid] = offs[tid];
-  __syncthreads();
-  if (tid == 0) {
-    const int b = blockIdx.x;
-    int mi = 0;
-    while (mi + 1 < nact && soff[mi + 1] <= b) ++mi;
-    S.mat = mi;
-    S.tile = b - soff[mi];
-  }
-  __syncthreads();
-  const RMat M = mats[S.mat];
+  if (stamps && tid == 0) stamps[(long long)j * 16 + 8] = __builtin_amdgcn_s_memtime();
+  int mi, local;
+  map_block(offs, nact, soff, mi, local);
+  const RMat M = mats[mi];
   const int n = M.n, nt = M.nt;
-  STAMP(1);
   const long long lda = M.lda;
-  const bool fin = (j == n - 1);          // finisher: column n-2's tail, d[n-1]
-  const int s0 = (j + 1) / TB;
-  int I = 0, K = 0;
-  if (!fin) {
-    tri_index(S.tile, nt - s0, I, K);
-    I += s0; K += s0;
-  }
-  const bool lead = (S.tile == 0);
-  const bool diag = (I == K) && !fin;
-  const int c = j % NB;                    // column j's panel position
-  const int cp = (j >= 1) ? (c == 0 ? NB - 1 : c - 1) : 0;   // column j-1's position
+  const int bf = j / FB + local;           // this workgroup's 256-row block
+  const int r = bf * FB + tid;
+  const bool lead = (local == 0);
+  const bool fin = (j == n - 1);
+  const int c = j % NB;
+  const int cp = (j >= 1) ? (c == 0 ? NB - 1 : c - 1) : 0;
   const bool pstart = (c == 0 && j > 0);
-  const int cc = pstart ? NB : c;          // panel columns subtracted from base rows
+  const int cc = pstart ? NB : c;          // panel columns subtracted from A rows j, j+1
   const int cs = j & 1, ps = cs ^ 1;
-  const int s0p = j / TB;                  // first block of launch j-1
-  const float* Pp = M.P + ps * M.sP;
-  const float* SNp = M.SN + ps * M.sSN;
-  const float* XHp = M.XH + ps * M.sXH;
-
-  // ---- this thread's row: t < 128 -> block I, else block K
-  const int h = tid >> 7, lr = tid & (TB - 1);
-  const int r = (h ? K : I) * TB + lr;
-  const bool rok = !fin && r < n;
-
-  // ---- tile loads first (independent of everything below)
-  const int hw = lane >> 5, cl = lane & 31;
-  const int kk0 = cl * 4, k0 = K * TB + kk0;
-  float4 q[16];
-  if (!fin) {
-    const bool full_cols = (k0 + 3 < n);
-#pragma unroll
-    for (int it = 0; it < 16; ++it) {
-      const int rr = I * TB + wave * 32 + it * 2 + hw;
-      q[it] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (rr < n) {
-        const float* row = M.A + (long long)rr * lda;
-        if (full_cols) {
-          q[it] = *(const float4*)(row + k0);
-        } else {
-          if (k0 < n) q[it].x = row[k0];
-          if (k0 + 1 < n) q[it].y = row[k0 + 1];
-          if (k0 + 2 < n) q[it].z = row[k0 + 2];
-        }
-      }
-    }
-  }
-  // ---- every other load of the launch, issued before the first barrier
-  //      (the chain is latency bound: one memory round trip, not one per loop)
-  float vr[NB], wr[NB];
-#pragma unroll
-  for (int x = 0; x < NB; ++x) { vr[x] = 0.f; wr[x] = 0.f; }
-  float xhp = 0.f, arow = 0.f, brow = 0.f;
-  float4 pq[PQ4];                         // this row's yh partials (row-major in P)
-#pragma unroll
-  for (int u = 0; u < PQ4; ++u) pq[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int s0p = j / TB;                  // first tile block of symv(j-1)
   const int ntp = (nt + 3) & ~3;
-  const bool prow = rok && r >= j;
-  if (prow) {
-    // only the panel columns this launch reads (cc: x_j / a_j corrections,
-    // cp < cc: w_{j-1}, c <= cc: partial sums; all NB at a panel start)
+  const int nbp = nt - s0p;
+  const int f0p = (j - 1) / FB;            // first fin block of fin(j-1)
+  const float* Pp = M.P + ps * M.sP;
+  const float* XHp = M.XH + ps * M.sXH;
+  STAMP(1);
+
+  // ---- every load, in the order it is needed
+  // step-1 partials: fin(j-1) blocks x kinds (3 groups), symv(j-1) tile sums
+  double rsacc = 0.0, ts = 0.0;
+  const int rk = tid % RSW, rg = tid / RSW;
+  if (j >= 1) {
+    const float* RSp = M.RS + ps * M.sRS;
+    if (tid < 3 * RSW && (rk < 2 + cp || (rk >= 2 + NB && rk < 2 + NB + cp))) {
+      float v[(NFMAX + 2) / 3];
 #pragma unroll
-    for (int x = 0; x < NB / 4; ++x) {
-      if (4 * x < cc) {
-        const float4 a4 = *(const float4*)(M.V + (long long)r * NB + 4 * x);
-        const float4 b4 = *(const float4*)(M.W + (long long)r * NB + 4 * x);
-        vr[4 * x] = a4.x; vr[4 * x + 1] = a4.y; vr[4 * x + 2] = a4.z; vr[4 * x + 3] = a4.w;
-        wr[4 * x] = b4.x; wr[4 * x + 1] = b4.y; wr[4 * x + 2] = b4.z; wr[4 * x + 3] = b4.w;
+      for (int u = 0; u < (NFMAX + 2) / 3; ++u) {
+        const int bb = f0p + rg + 3 * u;
+        v[u] = (bb < M.nf) ? RSp[(long long)bb * RSW + rk] : 0.f;
       }
-    }
-    arow = SNp[r];            // base row j
-    brow = SNp[n + r];        // base row j+1
-    if (j >= 1) {
-      xhp = XHp[r];
-      const float4* pp = (const float4*)(Pp + (long long)r * ntp);
 #pragma unroll
-      for (int u = 0; u < PQ4; ++u)
-        if (4 * u + 3 >= s0p && 4 * u < nt) pq[u] = pp[u];
+      for (int u = 0; u < (NFMAX + 2) / 3; ++u) rsacc += (double)v[u];
     }
+    const float* TSp = M.TS + ps * M.sTS;
+    float tv[TSL];
+#pragma unroll
+    for (int u = 0; u < TSL; ++u) {      // (a, b) on a 64-wide virtual grid
+      const int f = tid + 256 * u;
+      const int ao = f >> 6, bo = f & 63;
+      tv[u] = 0.f;
+      if (ao < nbp && bo < nbp && ao <= bo) tv[u] = TSp[(long long)(s0p + ao) * nt + s0p + bo];
+    }
+#pragma unroll
+    for (int u = 0; u < TSL; ++u) ts += (double)tv[u];
   }
-  // waves 0 / 1: rows j / j+1 (every workgroup needs them for x_j and a_j)
+  // rows j / j+1 (waves 0 / 1)
   const int rw = j + wave;
   float vrow = 0.f, wrow = 0.f, pw = 0.f, xw = 0.f, aw = 0.f;
   if (wave < 2 && rw < n) {
@@ -224,75 +180,74 @@ __global__ __launch_bounds__(256) void sytrd_col_kernel(const RMat* __restrict__
       if (lane >= s0p && lane < nt) pw = Pp[(long long)rw * ntp + lane];
       xw = XHp[rw];
     }
-    aw = SNp[rw];
+    aw = M.A[(long long)j * lda + rw];     // row j of the panel's base matrix
   }
-  // step-1 partials: row-block sums (flat over blocks x kinds) and tile sums
-  float rsv[RSL];
-  double ts = 0.0;
-  const int nbp = nt - s0p;
-  if (j >= 1) {
-    const float* RSp = M.RS + ps * M.sRS + (long long)s0p * RSW;
-    const float* TSp = M.TS + ps * M.sTS;
+  // this thread's row
+  const bool rok = r < n && r >= j;
+  float vr[NB], wr[NB];
 #pragma unroll
-    for (int u = 0; u < RSL; ++u) {
-      const int f = tid + 256 * u;
-      rsv[u] = (f < nbp * RSW) ? RSp[f] : 0.f;
-    }
+  for (int x = 0; x < NB; ++x) { vr[x] = 0.f; wr[x] = 0.f; }
+  float xhp = 0.f, arow = 0.f, brow = 0.f;
+  float4 pq[PQ4];
 #pragma unroll
-    for (int u = 0; u < TSL; ++u) {
-      const int f = tid + 256 * u;
-      if (f < nbp * nbp) {
-        const int a = s0p + f / nbp, b = s0p + f % nbp;
-        if (a <= b) ts += (double)TSp[(long long)a * nt + b];
+  for (int u = 0; u < PQ4; ++u) pq[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (rok) {
+#pragma unroll
+    for (int x = 0; x < NB / 4; ++x) {
+      if (4 * x < cc) {
+        const float4 a4 = *(const float4*)(M.V + (long long)r * NB + 4 * x);
+        const float4 b4 = *(const float4*)(M.W + (long long)r * NB + 4 * x);
+        vr[4 * x] = a4.x; vr[4 * x + 1] = a4.y; vr[4 * x + 2] = a4.z; vr[4 * x + 3] = a4.w;
+        wr[4 * x] = b4.x; wr[4 * x + 1] = b4.y; wr[4 * x + 2] = b4.z; wr[4 * x + 3] = b4.w;
       }
     }
+    arow = M.A[(long long)j * lda + r];                       // base row j
+    if (j + 1 < n && r >= j + 1) brow = M.A[(long long)(j + 1) * lda + r];   // base row j+1
+    if (j >= 1) {
+      xhp = XHp[r];
+      const float4* pp = (const float4*)(Pp + (long long)r * ntp);
+#pragma unroll
+      for (int u = 0; u < PQ4; ++u)
+        if (4 * u + 3 >= s0p && 4 * u < nt) pq[u] = pp[u];
+    }
   }
-
   STAMP(2);
+
   // ---- step 1: scalars of column j-1 (every workgroup, same fixed order)
-  float* sRS = &S.rowred[0][0];           // staging: blocks x RSW
   if (wave < 2 && lane < NB) {
     S.vwj[2 * wave][lane] = vrow;
     S.vwj[2 * wave + 1][lane] = wrow;
   }
   if (j >= 1) {
-#pragma unroll
-    for (int u = 0; u < RSL; ++u) {
-      const int f = tid + 256 * u;
-      if (f < nbp * RSW) sRS[f] = rsv[u];
-    }
+    if (tid < 3 * RSW) S.red[tid] = rsacc;
     ts = wave_reduce_sum_d(ts);
     if (lane == 0) S.red[3 * RSW + wave] = ts;
   }
   __syncthreads();
   if (j >= 1) {
-    if (tid < RSW) {
-      double acc = 0.0;
-      if (tid < 2 + cp || (tid >= 2 + NB && tid < 2 + NB + cp))
-        for (int bb = 0; bb < nbp; ++bb) acc += (double)sRS[bb * RSW + tid];
-      S.red[tid] = acc;
-    }
-    __syncthreads();
     if (wave == 0) {
-      const double sig2 = S.red[0], xa = S.red[1];
+      auto R = [&](int k) { return S.red[k] + S.red[RSW + k] + S.red[2 * RSW + k]; };
+      const double sig2 = R(0), xa = R(1);
       const double xy = S.red[3 * RSW] + S.red[3 * RSW + 1] + S.red[3 * RSW + 2] +
                         S.red[3 * RSW + 3];
       const float* SCp = M.SC + ps * 4;
       const double alpha = SCp[0];
-      double beta, tau, s;
-      hh_scalars(alpha, sig2, beta, tau, s);
+      double beta, tau, sc;
+      hh_scalars(alpha, sig2, beta, tau, sc);
       // s1 = W^T v, s2 = V^T v over rows >= j (v[j] = 1): row j of the panel
       double s1 = 0.0, s2 = 0.0;
       if (lane < cp) {
-        s1 = (double)S.vwj[1][lane] + s * S.red[2 + lane];
-        s2 = (double)S.vwj[0][lane] + s * S.red[2 + NB + lane];
+        s1 = (double)S.vwj[1][lane] + sc * R(2 + lane);
+        s2 = (double)S.vwj[0][lane] + sc * R(2 + NB + lane);
+      }
+      const double s1s2 = wave_reduce_sum_d(s1 * s2);
+      if (lane < NB) {
         S.s12[lane] = (float)s1;
         S.s12[NB + lane] = (float)s2;
       }
-      const double s1s2 = wave_reduce_sum_d(s1 * s2);
       if (lane == 0) {
-        const double vy = (double)SNp[j] + 2.0 * s * xa + s * s * xy;
-        S.scal[0] = beta; S.scal[1] = tau; S.scal[2] = s; S.scal[4] = SCp[1];
+        const double vy = (double)M.A[(long long)j * lda + j] + 2.0 * sc * xa + sc * sc * xy;
+        S.scal[0] = beta; S.scal[1] = tau; S.scal[2] = sc; S.scal[4] = SCp[1];
         S.scal[3] = -0.5 * tau * tau * (vy - 2.0 * s1s2);
       }
     }
@@ -301,7 +256,7 @@ __global__ __launch_bounds__(256) void sytrd_col_kernel(const RMat* __restrict__
   const double beta_p = S.scal[0], tau_p = S.scal[1], s_p = S.scal[2], alpha2 = S.scal[3];
   STAMP(3);
 
-  // ---- step 2 for rows j and j+1 (waves 0 / 1)
+  // ---- step 2, rows j and j+1 (waves 0 / 1): needed by every row's x_j / a_j
   if (wave < 2 && j >= 1 && rw < n) {
     const float yv = wave_reduce_sum(pw);
     float corr = (lane < cp) ? vrow * S.s12[lane] + wrow * S.s12[NB + lane] : 0.f;
@@ -318,46 +273,42 @@ __global__ __launch_bounds__(256) void sytrd_col_kernel(const RMat* __restrict__
       M.W[(long long)rw * NB + cp] = ww;
     }
   }
-  __syncthreads();
   if (lead && tid == 0 && j >= 1) {
     M.d[j - 1] = (float)S.scal[4];
     M.e[j - 1] = (float)beta_p;
     M.tau[j - 1] = (float)tau_p;
     M.A[(long long)(j - 1) * lda + j] = (float)beta_p;
   }
-  float yh = 0.f;
-#pragma unroll
-  for (int u = 0; u < PQ4; ++u) {
-    if (4 * u >= s0p) yh += pq[u].x;
-    if (4 * u + 1 >= s0p) yh += pq[u].y;
-    if (4 * u + 2 >= s0p) yh += pq[u].z;
-    if (4 * u + 3 >= s0p) yh += pq[u].w;
-  }
-
-  STAMP(4);
-  // ---- step 2 for this thread's row (r >= j+1)
-  float vmy = 0.f, wmy = 0.f;
+  // ---- step 2, this thread's row (r >= j+1)
   if (j >= 1 && rok && r >= j + 1) {
+    float yh = 0.f;
+#pragma unroll
+    for (int u = 0; u < PQ4; ++u) {
+      if (4 * u >= s0p) yh += pq[u].x;
+      if (4 * u + 1 >= s0p) yh += pq[u].y;
+      if (4 * u + 2 >= s0p) yh += pq[u].z;
+      if (4 * u + 3 >= s0p) yh += pq[u].w;
+    }
     float corr = 0.f;
 #pragma unroll
     for (int x = 0; x < NB; ++x)
       if (x < cp) corr += vr[x] * S.s12[x] + wr[x] * S.s12[NB + x];
-    vmy = (float)(s_p * (double)xhp);
-    wmy = (float)(tau_p * ((double)arow + s_p * (double)yh - (double)corr) + alpha2 * (double)vmy);
+    const float vmy = (float)(s_p * (double)xhp);
+    const float wmy =
+        (float)(tau_p * ((double)arow + s_p * (double)yh - (double)corr) + alpha2 * (double)vmy);
 #pragma unroll
     for (int x = 0; x < NB; ++x)
       if (x == cp) { vr[x] = vmy; wr[x] = wmy; }
-    if (diag && h == 0) {
-      M.V[(long long)r * NB + cp] = vmy;
-      M.W[(long long)r * NB + cp] = wmy;
-      M.A[(long long)(j - 1) * lda + r] = vmy;     // reflector j-1: v[2:] (r >= j+1)
-    }
+    M.V[(long long)r * NB + cp] = vmy;
+    M.W[(long long)r * NB + cp] = wmy;
+    M.A[(long long)(j - 1) * lda + r] = vmy;      // reflector j-1: v[2:] (r >= j+1)
   }
+  __syncthreads();      // rows j / j+1 of the panel (S.vwj) are final
+  STAMP(4);
 
-  // ---- finisher: d[n-1] = base(n-1, n-1) - 2 V[n-1] . W[n-1] over cc columns
-  if (fin) {
-    if (tid == 0) {
-      double dd = SNp[j];
+  if (fin) {            // d[n-1] = A(n-1, n-1) - 2 V[n-1] . W[n-1]
+    if (lead && tid == 0) {
+      double dd = M.A[(long long)j * lda + j];
       for (int x = 0; x < cc; ++x) dd -= 2.0 * (double)S.vwj[0][x] * (double)S.vwj[1][x];
       M.d[j] = (float)dd;
       M.e[j] = 0.f;
@@ -366,47 +317,7 @@ __global__ __launch_bounds__(256) void sytrd_col_kernel(const RMat* __restrict__
     return;
   }
 
-  // ---- panel start: A_tile -= V W^T + W V^T (rows >= j, upper), in registers
-  if (pstart) {
-    float* sV = upd;                      // [256][NB+1]
-    float* sW = upd + 256 * (NB + 1);
-#pragma unroll
-    for (int x = 0; x < NB; ++x) {
-      sV[tid * (NB + 1) + x] = (rok && r >= j) ? vr[x] : 0.f;
-      sW[tid * (NB + 1) + x] = (rok && r >= j) ? wr[x] : 0.f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int it = 0; it < 16; ++it) {
-      const int rr = wave * 32 + it * 2 + hw;      // tile row (block I)
-      const int gr = I * TB + rr;
-      float u0 = 0.f, u1 = 0.f, u2 = 0.f, u3 = 0.f;
-      const float* vi = sV + rr * (NB + 1);
-      const float* wi = sW + rr * (NB + 1);
-      const float* vk = sV + (128 + kk0) * (NB + 1);
-      const float* wk = sW + (128 + kk0) * (NB + 1);
-#pragma unroll 8
-      for (int x = 0; x < NB; ++x) {
-        const float a = vi[x], b = wi[x];
-        u0 += a * wk[x] + b * vk[x];
-        u1 += a * wk[(NB + 1) + x] + b * vk[(NB + 1) + x];
-        u2 += a * wk[2 * (NB + 1) + x] + b * vk[2 * (NB + 1) + x];
-        u3 += a * wk[3 * (NB + 1) + x] + b * vk[3 * (NB + 1) + x];
-      }
-      if (gr >= j + 1 && gr < n) {
-        float* row = M.A + (long long)gr * lda + K * TB + kk0;
-        const int gc = K * TB + kk0;
-        if (gc >= gr && gc < n) { q[it].x -= u0; row[0] = q[it].x; }
-        if (gc + 1 >= gr && gc + 1 < n) { q[it].y -= u1; row[1] = q[it].y; }
-        if (gc + 2 >= gr && gc + 2 < n) { q[it].z -= u2; row[2] = q[it].z; }
-        if (gc + 3 >= gr && gc + 3 < n) { q[it].w -= u3; row[3] = q[it].w; }
-      }
-    }
-  }
-
-  STAMP(5);
-  // ---- step 3: x_j (rows >= j+1), a_j; d_j and alpha_j by the lead
-  float* XHc = M.XH + cs * M.sXH;
+  // ---- step 3: x_j (rows >= j+1), a_j; d_j and alpha_j
   float xmy = 0.f, amy = 0.f;
   if (rok && r >= j + 1) {
     float corr = 0.f, corr1 = 0.f;
@@ -418,97 +329,189 @@ __global__ __launch_bounds__(256) void sytrd_col_kernel(const RMat* __restrict__
       }
     }
     xmy = arow - corr;
-    amy = pstart ? brow - corr1 : brow;
+    amy = pstart ? brow - corr1 : brow;    // a_j = row j+1 of the NEW panel's base
   }
   const float xh = (rok && r >= j + 2) ? xmy : 0.f;
   if (lead && tid == 0) {
-    double dd = SNp[j];
+    double dd = M.A[(long long)j * lda + j];
     for (int x = 0; x < cc; ++x) dd -= 2.0 * (double)S.vwj[0][x] * (double)S.vwj[1][x];
-    float* SCc = M.SC + cs * 4;
-    SCc[1] = (float)dd;
+    M.SC[cs * 4 + 1] = (float)dd;
   }
-  if (rok && r == j + 1 && diag && h == 0) M.SC[cs * 4] = xmy;   // alpha_j
-  if (diag && h == 0 && rok) XHc[r] = xh;
-  S.sv[h][lr] = xh;
-
-  // ---- row-block partials (diagonal tiles): |xh|^2, xh.a_j, W^T xh, V^T xh
-  //      (new panel columns), transposed through LDS and summed per kind
-  if (diag) {
-    const int cn = pstart ? 0 : c;     // columns of the current panel
-    const int nk = 2 + 2 * NB;
-    float* T = upd;                    // [TB][RSW]
-    __syncthreads();                   // the panel-start staging in upd is consumed
-    if (h == 0) {
-      float* row = T + lr * RSW;
-      row[0] = xh * xh;
-      row[1] = xh * amy;
+  if (r == j + 1 && r < n) M.SC[cs * 4] = xmy;      // alpha_j
+  if (r < n) M.XH[cs * M.sXH + r] = xh;
+  // ---- partial sums for fin(j+1): transpose through LDS, fixed-order sums
+  {
+    const int cn = pstart ? 0 : c;                // the current panel's columns
+    tw[0 * TWS + tid] = xh * xh;
+    tw[1 * TWS + tid] = xh * amy;
 #pragma unroll
-      for (int x = 0; x < NB; ++x) {
-        row[2 + x] = (x < cn) ? wr[x] * xh : 0.f;
-        row[2 + NB + x] = (x < cn) ? vr[x] * xh : 0.f;
-      }
+    for (int x = 0; x < NB; ++x) {
+      tw[(2 + x) * TWS + tid] = (x < cn) ? wr[x] * xh : 0.f;
+      tw[(2 + NB + x) * TWS + tid] = (x < cn) ? vr[x] * xh : 0.f;
     }
-    __syncthreads();
-    if (tid < 3 * RSW) {
-      const int k = tid % RSW, g = tid / RSW;
-      double acc = 0.0;
-      if (k < nk)
-        for (int rr = g; rr < TB; rr += 3) acc += (double)T[rr * RSW + k];
-      S.red[g * RSW + k] = acc;
-    }
-    __syncthreads();
-    float* RSc = M.RS + cs * M.sRS + (long long)I * RSW;
-    if (tid < RSW)
-      RSc[tid] = (float)(S.red[tid] + S.red[RSW + tid] + S.red[2 * RSW + tid]);
   }
   __syncthreads();
-
+  STAMP(5);
+  if (tid < 3 * RSW) {
+    double acc = 0.0;
+    if (rk < 2 + 2 * NB) {
+      const float* col = tw + rk * TWS;
+#pragma unroll 8
+      for (int t = rg; t < FB; t += 3) acc += (double)col[t];
+    }
+    S.red[tid] = acc;
+  }
+  __syncthreads();
+  if (tid < RSW)
+    M.RS[cs * M.sRS + (long long)bf * RSW + tid] =
+        (float)(S.red[tid] + S.red[RSW + tid] + S.red[2 * RSW + tid]);
   STAMP(6);
-  // ---- snapshot rows j+1, j+2 of the (updated) base for K(j+1)
-  float* SNc = M.SN + cs * M.sSN;
+  if (stamps && tid == 0) stamps[(long long)j * 16 + 9] = __builtin_amdgcn_s_memtime();
+}
+
+// ------------------------------------------------------------------- upd
+// A[I][K] -= L_I R_K^T with L = [V | W], R = [W | V] (rows >= q+1, upper):
+// the panel's rank-2NB update, exact-f32 MFMA, 4 waves of 64 x 64.
+__global__ __launch_bounds__(256) void sytrd_upd_kernel(const RMat* __restrict__ mats,
+                                                        const int* __restrict__ offs, int nact,
+                                                        int q) {
+  __shared__ float sL[TB][2 * NB + 1];
+  __shared__ float sR[TB][2 * NB + 1];
+  __shared__ int soff[MAXM + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int mi, local;
+  map_block(offs, nact, soff, mi, local);
+  const RMat M = mats[mi];
+  const int n = M.n, nt = M.nt;
+  const int s0 = (q + 1) / TB;
+  int I, K;
+  tri_index(local, nt - s0, I, K);
+  I += s0; K += s0;
+  for (int e = tid; e < TB * NB; e += 256) {
+    const int rr = e / NB, x = e - rr * NB;
+    const int ri = I * TB + rr, rk = K * TB + rr;
+    const float vi = ri < n ? M.V[(long long)ri * NB + x] : 0.f;
+    const float wi = ri < n ? M.W[(long long)ri * NB + x] : 0.f;
+    const float vk = rk < n ? M.V[(long long)rk * NB + x] : 0.f;
+    const float wk = rk < n ? M.W[(long long)rk * NB + x] : 0.f;
+    sL[rr][x] = vi; sL[rr][NB + x] = wi;
+    sR[rr][x] = wk; sR[rr][NB + x] = vk;
+  }
+  __syncthreads();
+  const int wr = wave >> 1, wc = wave & 1;          // 2 x 2 waves of 64 x 64
+  const int l31 = lane & 31, lh = lane >> 5;
+  f32x16_t acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int x = 0; x < 16; ++x) acc[a][b][x] = 0.f;
+#pragma unroll 4
+  for (int kk = 0; kk < NB; ++kk) {                 // k = 2 kk + lh over 2 NB
+    const int k = 2 * kk + lh;
+    float av[2], bv[2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) av[a] = sL[wr * 64 + a * 32 + l31][k];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) bv[b] = sR[wc * 64 + b * 32 + l31][k];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[b], acc[a][b], 0, 0, 0);
+  }
+  // C/D map of 32x32: row = (x&3) + 8 (x>>2) + 4 lh, col = lane & 31
+  float* A = M.A;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int x = 0; x < 16; ++x) {
+        const int gr = I * TB + wr * 64 + a * 32 + (x & 3) + 8 * (x >> 2) + 4 * lh;
+        const int gc = K * TB + wc * 64 + b * 32 + l31;
+        if (gr >= q + 1 && gr < n && gc >= gr && gc < n) {
+          float* p = A + (long long)gr * M.lda + gc;
+          *p -= acc[a][b][x];
+        }
+      }
+}
+
+// ------------------------------------------------------------------- symv
+__global__ __launch_bounds__(256) void sytrd_symv2_kernel(const RMat* __restrict__ mats,
+                                                          const int* __restrict__ offs, int nact,
+                                                          int j) {
+  __shared__ float sv[2][TB];
+  __shared__ float rowred[TB][33];
+  __shared__ float colred[4][TB];
+  __shared__ double tred[2];
+  __shared__ int soff[MAXM + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int mi, local;
+  map_block(offs, nact, soff, mi, local);
+  const RMat M = mats[mi];
+  const int n = M.n, nt = M.nt;
+  const long long lda = M.lda;
+  const int s0 = (j + 1) / TB;
+  int I, K;
+  tri_index(local, nt - s0, I, K);
+  I += s0; K += s0;
+  const bool diag = (I == K);
+  const int cs = j & 1;
+  const int ntp = (nt + 3) & ~3;
+  // xh of the rows of blocks I and K (written by fin(j))
+  {
+    const int h = tid >> 7, lr = tid & (TB - 1);
+    const int rr = (h ? K : I) * TB + lr;
+    sv[h][lr] = rr < n ? M.XH[cs * M.sXH + rr] : 0.f;
+  }
+  const int hw = lane >> 5, cl = lane & 31;
+  const int kk0 = cl * 4, k0 = K * TB + kk0;
+  float4 q[16];
+  const bool full_cols = (k0 + 3 < n);
 #pragma unroll
   for (int it = 0; it < 16; ++it) {
-    const int gr = I * TB + wave * 32 + it * 2 + hw;
-    const int gc = K * TB + kk0;
-    if (gr == j + 1 || gr == j + 2) {
-      float* o = SNc + (gr == j + 1 ? 0 : n);
-      if (gc >= gr && gc < n) o[gc] = q[it].x;
-      if (gc + 1 >= gr && gc + 1 < n) o[gc + 1] = q[it].y;
-      if (gc + 2 >= gr && gc + 2 < n) o[gc + 2] = q[it].z;
-      if (gc + 3 >= gr && gc + 3 < n) o[gc + 3] = q[it].w;
+    const int rr = I * TB + wave * 32 + it * 2 + hw;
+    q[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (rr < n) {
+      const float* row = M.A + (long long)rr * lda;
+      if (full_cols) {
+        q[it] = *(const float4*)(row + k0);
+      } else {
+        if (k0 < n) q[it].x = row[k0];
+        if (k0 + 1 < n) q[it].y = row[k0 + 1];
+        if (k0 + 2 < n) q[it].z = row[k0 + 2];
+      }
     }
   }
-
-  STAMP(7);
-  // ---- step 4: yh partials over the tile (upper triangle of diagonal tiles)
+  __syncthreads();
   float ca[4] = {0.f, 0.f, 0.f, 0.f};
-  const float vk0 = S.sv[1][kk0], vk1 = S.sv[1][kk0 + 1], vk2 = S.sv[1][kk0 + 2],
-              vk3 = S.sv[1][kk0 + 3];
+  const float vk0 = sv[1][kk0], vk1 = sv[1][kk0 + 1], vk2 = sv[1][kk0 + 2], vk3 = sv[1][kk0 + 3];
 #pragma unroll
   for (int it = 0; it < 16; ++it) {
     const int rr = wave * 32 + it * 2 + hw;
     float x0 = q[it].x, x1 = q[it].y, x2 = q[it].z, x3 = q[it].w;
-    const float vrr = S.sv[0][rr];
-    if (diag) {
+    const float vrr = sv[0][rr];
+    if (diag) {   // upper triangle only: row sums take k >= r, column sums k > r
       x0 = (kk0 >= rr) ? x0 : 0.f;
       x1 = (kk0 + 1 >= rr) ? x1 : 0.f;
       x2 = (kk0 + 2 >= rr) ? x2 : 0.f;
       x3 = (kk0 + 3 >= rr) ? x3 : 0.f;
-      S.rowred[rr][cl] = x0 * vk0 + x1 * vk1 + x2 * vk2 + x3 * vk3;
       ca[0] += (kk0 > rr) ? x0 * vrr : 0.f;
       ca[1] += (kk0 + 1 > rr) ? x1 * vrr : 0.f;
       ca[2] += (kk0 + 2 > rr) ? x2 * vrr : 0.f;
       ca[3] += (kk0 + 3 > rr) ? x3 * vrr : 0.f;
     } else {
-      S.rowred[rr][cl] = x0 * vk0 + x1 * vk1 + x2 * vk2 + x3 * vk3;
       ca[0] += x0 * vrr; ca[1] += x1 * vrr; ca[2] += x2 * vrr; ca[3] += x3 * vrr;
     }
+    rowred[rr][cl] = x0 * vk0 + x1 * vk1 + x2 * vk2 + x3 * vk3;
   }
 #pragma unroll
   for (int x = 0; x < 4; ++x) ca[x] += __shfl_xor(ca[x], 32, 64);
   if (hw == 0) {
 #pragma unroll
-    for (int x = 0; x < 4; ++x) S.colred[wave][kk0 + x] = ca[x];
+    for (int x = 0; x < 4; ++x) colred[wave][kk0 + x] = ca[x];
   }
   __syncthreads();
   float* Pc = M.P + cs * M.sP;
@@ -516,54 +519,58 @@ __global__ __launch_bounds__(256) void sytrd_col_kernel(const RMat* __restrict__
   if (tid < TB) {
     float rs = 0.f;
 #pragma unroll 8
-    for (int l = 0; l < 32; ++l) rs += S.rowred[tid][l];
-    const float csum = S.colred[0][tid] + S.colred[1][tid] + S.colred[2][tid] + S.colred[3][tid];
+    for (int l = 0; l < 32; ++l) rs += rowred[tid][l];
+    const float csum = colred[0][tid] + colred[1][tid] + colred[2][tid] + colred[3][tid];
     if (diag) {
       Pc[((long long)I * TB + tid) * ntp + K] = rs + csum;
-      tp = (double)S.sv[0][tid] * (double)(rs + csum);
+      tp = (double)sv[0][tid] * (double)(rs + csum);
     } else {
       Pc[((long long)I * TB + tid) * ntp + K] = rs;
       Pc[((long long)K * TB + tid) * ntp + I] = csum;
-      tp = (double)S.sv[0][tid] * (double)rs + (double)S.sv[1][tid] * (double)csum;
+      tp = (double)sv[0][tid] * (double)rs + (double)sv[1][tid] * (double)csum;
     }
   }
-  STAMP(8);
   tp = wave_reduce_sum_d(tp);
-  if (lane == 0 && wave < 2) S.red[4 * RSW - 2 + wave] = tp;
+  if (lane == 0 && wave < 2) tred[wave] = tp;
   __syncthreads();
-  if (tid == 0)
-    M.TS[cs * M.sTS + (long long)I * nt + K] = (float)(S.red[4 * RSW - 2] + S.red[4 * RSW - 1]);
-  STAMP(9);
+  if (tid == 0) M.TS[cs * M.sTS + (long long)I * nt + K] = (float)(tred[0] + tred[1]);
 }
 
 // ------------------------------------------------------------------ host
 struct RPlan {
   RMat* d_mats = nullptr;
-  int* d_offs = nullptr;       // per launch j: (nm + 1) cumulative tile offsets
-  std::vector<int> n_sorted;   // descending
+  int* d_offs = nullptr;        // [3][nmax][nm + 1]: fin, upd, symv workgroup offsets
+  std::vector<int> n_sorted;    // descending
+  std::vector<int> grid[3];     // [nmax] total workgroups per launch kind
+  std::vector<int> nact[3];
   int nmax = 0;
   hipGraphExec_t exec = nullptr;
 };
 
 inline int h_tri(int m) { return m * (m + 1) / 2; }
 
+// workgroups of matrix n at column j: fin, upd (panel start only), symv
+void counts(int n, int j, int out[3]) {
+  const int nt = (n + TB - 1) / TB, nf = (n + FB - 1) / FB;
+  out[0] = (j <= n - 1) ? nf - j / FB : 0;
+  out[1] = (j % NB == 0 && j > 0 && j <= n - 2) ? h_tri(nt - (j + 1) / TB) : 0;
+  out[2] = (j <= n - 2) ? h_tri(nt - (j + 1) / TB) : 0;
+}
+
 int enqueue(const RPlan& P, hipStream_t stream) {
   const int nm = (int)P.n_sorted.size();
-  hipLaunchKernelGGL(reduce_prep_kernel, dim3(8, nm), dim3(256), 0, stream, P.d_mats);
-  const size_t upd_lds = 2 * 256 * (NB + 1) * sizeof(float);
-  const size_t part_lds = TB * RSW * sizeof(float);
+  const size_t fin_lds = (size_t)RSW * TWS * sizeof(float);
+  const size_t kstride = (size_t)P.nmax * (nm + 1);
   for (int j = 0; j < P.nmax; ++j) {
-    int nact = 0, grid = 0;
-    for (int i = 0; i < nm; ++i) {
-      const int n = P.n_sorted[i];
-      if (j > n - 1) break;
-      ++nact;
-      const int nt = (n + TB - 1) / TB;
-      grid += (j <= n - 2) ? h_tri(nt - (j + 1) / TB) : 1;
-    }
-    const bool pstart = (j % NB == 0 && j > 0);
-    hipLaunchKernelGGL(sytrd_col_kernel, dim3(grid), dim3(256), pstart ? upd_lds : part_lds, stream,
-                       P.d_mats, P.d_offs + (long long)j * (nm + 1), nact, j);
+    const int* of = P.d_offs + (size_t)j * (nm + 1);
+    hipLaunchKernelGGL(sytrd_fin_kernel, dim3(P.grid[0][j]), dim3(256), fin_lds, stream,
+                       P.d_mats, of, P.nact[0][j], j);
+    if (P.grid[1][j] > 0)
+      hipLaunchKernelGGL(sytrd_upd_kernel, dim3(P.grid[1][j]), dim3(256), 0, stream, P.d_mats,
+                         of + kstride, P.nact[1][j], j);
+    if (P.grid[2][j] > 0)
+      hipLaunchKernelGGL(sytrd_symv2_kernel, dim3(P.grid[2][j]), dim3(256), 0, stream,
+                         P.d_mats, of + 2 * kstride, P.nact[2][j], j);
   }
   return (int)hipGetLastError();
 }
@@ -575,15 +582,15 @@ std::map<std::string, RPlan> g_plans;
 
 // workspace floats per matrix (V, W and the 2-slot partial rings)
 KFAC_API long long kfac_reduce_ws_floats(int n) {
-  const long long nt = (n + TB - 1) / TB;
-  long long s = 2LL * n * NB;                 // V, W
-  s += 2 * nt * TB * ((nt + 3) / 4 * 4) + 32; // P (row-major partials)
-  s += 2 * nt * nt;                           // TS
-  s += 2 * nt * RSW;                          // RS
-  s += 2LL * n;                               // XH
-  s += 4LL * n;                               // SN
-  s += 8;                                     // SC
-  return (s + 63) / 64 * 64 + 64 * 8;
+  const long long nt = (n + TB - 1) / TB, nf = (n + FB - 1) / FB;
+  auto a16 = [](long long x) { return (x + 15) / 16 * 16; };
+  long long s = 2 * a16((long long)n * NB);               // V, W
+  s += 2 * a16(nt * TB * ((nt + 3) / 4 * 4));             // P (row-major partials)
+  s += 2 * a16(nt * nt);                                  // TS
+  s += 2 * a16(nf * RSW);                                 // RS
+  s += 2 * a16(n);                                        // XH
+  s += a16(8);                                            // SC
+  return (s + 63) / 64 * 64;
 }
 
 struct KfacReduceRecord {
@@ -605,17 +612,16 @@ RPlan* plan_for(const KfacReduceRecord* recs, int count, bool capture, int* err)
     RMat M;
     memset(&M, 0, sizeof(M));
     M.A = r.A; M.lda = r.lda; M.n = (int)r.n; M.nt = (int)((r.n + TB - 1) / TB);
+    M.nf = (int)((r.n + FB - 1) / FB);
     M.d = r.d; M.e = r.e; M.tau = r.tau;
     const long long nt = M.nt, n = r.n;
     float* p = r.ws;
-    // 16-byte aligned carving
     auto take = [&](long long fl) { float* o = p; p += (fl + 15) / 16 * 16; return o; };
     M.V = take(n * NB); M.W = take(n * NB);
     M.sP = (nt * TB * ((nt + 3) / 4 * 4) + 15) / 16 * 16; M.P = take(2 * M.sP);
     M.sTS = (nt * nt + 15) / 16 * 16; M.TS = take(2 * M.sTS);
-    M.sRS = (nt * RSW + 15) / 16 * 16; M.RS = take(2 * M.sRS);
+    M.sRS = (M.nf * RSW + 15) / 16 * 16; M.RS = take(2 * M.sRS);
     M.sXH = (n + 15) / 16 * 16; M.XH = take(2 * M.sXH);
-    M.sSN = (2 * n + 15) / 16 * 16; M.SN = take(2 * M.sSN);
     M.SC = take(8);
     mats.push_back(M);
   }
@@ -623,9 +629,9 @@ RPlan* plan_for(const KfacReduceRecord* recs, int count, bool capture, int* err)
   std::lock_guard<std::mutex> lk(g_mu);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)sytrd_col_kernel,
+    (void)hipFuncSetAttribute((const void*)sytrd_fin_kernel,
                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                              2 * 256 * (NB + 1) * (int)sizeof(float));
+                              RSW * TWS * (int)sizeof(float));
     attr = true;
   }
   auto it = g_plans.find(key);
@@ -633,20 +639,31 @@ RPlan* plan_for(const KfacReduceRecord* recs, int count, bool capture, int* err)
     RPlan P;
     for (const RMat& M : mats) P.n_sorted.push_back(M.n);
     P.nmax = P.n_sorted[0];
+    const int nm = (int)mats.size();
     if ((*err = (int)hipMalloc(&P.d_mats, sizeof(RMat) * mats.size())) != 0) return nullptr;
     if ((*err = (int)hipMemcpy(P.d_mats, mats.data(), sizeof(RMat) * mats.size(),
                                hipMemcpyHostToDevice)) != 0)
       return nullptr;
-    const int nm = (int)mats.size();
-    std::vector<int> offs((size_t)P.nmax * (nm + 1), 0);
+    std::vector<int> offs((size_t)3 * P.nmax * (nm + 1), 0);
+    for (int k = 0; k < 3; ++k) {
+      P.grid[k].assign(P.nmax, 0);
+      P.nact[k].assign(P.nmax, 0);
+    }
     for (int j = 0; j < P.nmax; ++j) {
-      int acc = 0;
+      int acc[3] = {0, 0, 0};
       for (int i = 0; i < nm; ++i) {
-        offs[(size_t)j * (nm + 1) + i] = acc;
-        const int n = P.n_sorted[i];
-        if (j <= n - 1) acc += (j <= n - 2) ? h_tri((n + TB - 1) / TB - (j + 1) / TB) : 1;
+        int cnt[3];
+        counts(P.n_sorted[i], j, cnt);
+        for (int k = 0; k < 3; ++k) {
+          offs[((size_t)k * P.nmax + j) * (nm + 1) + i] = acc[k];
+          if (cnt[k] > 0) P.nact[k][j] = i + 1;
+          acc[k] += cnt[k];
+        }
       }
-      offs[(size_t)j * (nm + 1) + nm] = acc;
+      for (int k = 0; k < 3; ++k) {
+        offs[((size_t)k * P.nmax + j) * (nm + 1) + nm] = acc[k];
+        P.grid[k][j] = acc[k];
+      }
     }
     if ((*err = (int)hipMalloc(&P.d_offs, sizeof(int) * offs.size())) != 0) return nullptr;
     if ((*err = (int)hipMemcpy(P.d_offs, offs.data(), sizeof(int) * offs.size(),
@@ -674,9 +691,9 @@ RPlan* plan_for(const KfacReduceRecord* recs, int count, bool capture, int* err)
 
 }  // namespace
 
-// Tridiagonalise `count` symmetric matrices (any sizes) with one launch per
-// column for all of them: A (n x lda, row-major, upper triangle read and
-// overwritten by the reflectors), d, e, tau (n floats each), ws
+// Tridiagonalise `count` symmetric matrices (any sizes <= 5120) with one
+// launch sequence for all of them: A (n x lda, row-major, upper triangle read
+// and overwritten by the reflectors), d, e, tau (n floats each), ws
 // (kfac_reduce_ws_floats(n) floats, 256-byte aligned).
 KFAC_API int kfac_reduce_batched(const KfacReduceRecord* recs, int count, int use_graph,
                                  hipStream_t stream) {
@@ -691,8 +708,8 @@ KFAC_API int kfac_reduce_batched(const KfacReduceRecord* recs, int count, int us
   return enqueue(*plan, stream);
 }
 
-// debug: record phase stamps of workgroup 0 of every launch into `buf`
-// (nmax x 16 uint64), or stop with nullptr
+// debug: record phase stamps of the first fin workgroup of every column into
+// `buf` (nmax x 16 uint64), or stop with nullptr
 KFAC_API int kfac_reduce_stamps(unsigned long long* buf) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &buf, sizeof(buf));
 }

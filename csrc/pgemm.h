@@ -35,5 +35,8 @@ struct SplitJob {
 // memory); operands k-contiguous and zero-padded along k to a multiple of 64.
 KFAC_API int kfac_pgemm(int prec, int tile, const void* dev_table, int count, int total_tiles,
                         double* kl, hipStream_t stream);
+// kl (pgemm): NULL, or this launch's per-workgroup f64 partial slots of the
+// EPI_FINAL KL dot (total_tiles of them); kfac_kl_finalize sums slots in order.
+KFAC_API int kfac_kl_finalize(const double* part, int n, double* out, hipStream_t stream);
 KFAC_API int kfac_split_copy(int prec, const void* dev_jobs, int count, int total_tiles,
                              hipStream_t stream);

@@ -5,9 +5,11 @@
 //   hadamard        K8 middle step, in place on v1 (nG x nA, f32):
 //                   mode 0: v1 *= dGdA ; mode 1: v1 /= (dG[i]*dA[j] + damping)
 //                   (reference kfac/layers/base.py:459-470)
-//   grouped_kl_dot  K10: vg += sum over ALL layers of <v, g> in ONE launch,
-//                   accumulated in f64 on the device (the reference does one
-//                   .item() per layer: kfac/preconditioner.py:661-682).
+//   grouped_kl_dot  K10: vg = sum over ALL layers of <v, g>: one launch writes a
+//                   f64 partial per workgroup, kl_finalize sums them in a fixed
+//                   order -- deterministic, so every data-parallel rank derives
+//                   the bit-identical clip scale (the reference does one .item()
+//                   per layer: kfac/preconditioner.py:661-682).
 //   grouped_apply   K11: g = nu * v for ALL layers in ONE launch, where nu is
 //                   computed on the device from vg (no host sync):
 //                   nu = vg==0 ? 1 : min(1, sqrt(kl_clip / |vg * lr^2|)).
@@ -61,6 +63,8 @@ __device__ __forceinline__ long long g_index(const Mat2D& m, int r, int col) {
   return (long long)r * m.gs0 + (long long)c * m.gs1 + (long long)i * m.gs2 + (long long)j * m.gs3;
 }
 
+__device__ __forceinline__ void part_out(double* part, int i, double v) { part[i] = v; }
+
 __device__ __forceinline__ float load_g(const Mat2D& m, long long idx) {
   if (m.gdtype == KDT_F32) return ((const float*)m.g)[idx];
   if (m.gdtype == KDT_BF16) return bf16_bits_to_f32(((const uint16_t*)m.g)[idx]);
@@ -74,7 +78,7 @@ __device__ __forceinline__ void store_g(const Mat2D& m, long long idx, float v) 
 }
 
 __global__ __launch_bounds__(256) void grouped_kl_dot_kernel(const GroupTable* __restrict__ tp,
-                                                             double* vg) {
+                                                             double* part) {
   const GroupTable& t = *tp;
   const int e = find_entry(t, blockIdx.x);
   const Mat2D m = t.m[e];
@@ -86,10 +90,10 @@ __global__ __launch_bounds__(256) void grouped_kl_dot_kernel(const GroupTable* _
     acc += m.v[(long long)r * m.ldv + c] * load_g(m, g_index(m, r, c));
   }
   double d = wave_reduce_sum_d((double)acc);
-  __shared__ double part[4];
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = d;
+  __shared__ double part4[4];
+  if ((threadIdx.x & 63) == 0) part4[threadIdx.x >> 6] = d;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(vg, part[0] + part[1] + part[2] + part[3]);
+  if (threadIdx.x == 0) part_out(part, blockIdx.x, part4[0] + part4[1] + part4[2] + part4[3]);
 }
 
 __global__ __launch_bounds__(256) void grouped_apply_kernel(const GroupTable* __restrict__ tp,
@@ -138,7 +142,29 @@ __global__ __launch_bounds__(256) void hadamard_kernel(float* __restrict__ v, in
   }
 }
 
+// out = sum of part[0, n) in a fixed order (one workgroup)
+__global__ __launch_bounds__(256) void kl_finalize_kernel(const double* __restrict__ part, int n,
+                                                          double* out) {
+  __shared__ double red[256];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) acc += part[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0];
+}
+
 }  // namespace
+
+KFAC_API int kfac_kl_finalize(const double* part, int n, double* out, hipStream_t stream) {
+  hipLaunchKernelGGL(kl_finalize_kernel, dim3(1), dim3(256), 0, stream, part, n, out);
+  return (int)hipGetLastError();
+}
+
+KFAC_API int kfac_kl_elems_per_block() { return ELEMS_PER_BLOCK; }
 
 // entries: flat array of `count` records (ops/_lib.py MatRecord)
 struct KfacMatRecord {
@@ -150,6 +176,7 @@ struct KfacMatRecord {
 
 static int build_tables_and_launch(const KfacMatRecord* recs, int count, bool dot, double* vg,
                                    double lr2, double kl_clip, int use_clip, hipStream_t stream) {
+  int part_off = 0;   // dot: per-workgroup partial slots at vg + 1 + part_off
   for (int base = 0; base < count; base += MAXG) {
     GroupTable t;
     memset(&t, 0, sizeof(t));   // deterministic table bytes (devtable key)
@@ -170,17 +197,22 @@ static int build_tables_and_launch(const KfacMatRecord* recs, int count, bool do
     int terr = 0;
     const GroupTable* d = (const GroupTable*)kfac_devtable::get(&t, sizeof(t), stream, &terr);
     if (!d) return terr;
-    if (dot)
-      hipLaunchKernelGGL(grouped_kl_dot_kernel, dim3(blocks), dim3(256), 0, stream, d, vg);
-    else
+    if (dot) {
+      hipLaunchKernelGGL(grouped_kl_dot_kernel, dim3(blocks), dim3(256), 0, stream, d,
+                         vg + 1 + part_off);
+      part_off += blocks;
+    } else
       hipLaunchKernelGGL(grouped_apply_kernel, dim3(blocks), dim3(256), 0, stream, d, vg, lr2,
                          kl_clip, use_clip);
     int err = (int)hipGetLastError();
     if (err) return err;
   }
+  if (dot) return kfac_kl_finalize(vg + 1, part_off, vg, stream);
   return 0;
 }
 
+// vg: 1 + sum_k ceil(rows_k cols_k / kfac_kl_elems_per_block()) doubles; the
+// result lands in vg[0], the per-workgroup partials after it.
 KFAC_API int kfac_grouped_kl_dot(const KfacMatRecord* recs, int count, double* vg,
                                  hipStream_t stream) {
   return build_tables_and_launch(recs, count, true, vg, 0.0, 0.0, 0, stream);

@@ -82,7 +82,10 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   const int M = P.M, N = P.N;
   // device-sized problems (csrc/eig_dc.hip patches M / K at run time and
   // launches the worst-case tile grid): tiles past the problem exit at once
-  if (m0 >= M || n0 >= N) return;
+  if (m0 >= M || n0 >= N) {
+    if (kl != nullptr && threadIdx.x == 0) kl[blockIdx.x] = 0.0;   // its partial slot
+    return;
+  }
   const int ksteps = (P.K + TK - 1) / TK;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -246,9 +249,19 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
           ((float*)P.c_hi)[o] = v;
         }
       }
-  if (P.epi == EPI_FINAL && kl != nullptr) {
-    double d = wave_reduce_sum_d((double)kl_part);
-    if (lane == 0) atomicAdd(kl, d);
+  if (kl != nullptr) {
+    // one f64 partial per workgroup (waves summed in order, LDS is free after
+    // the k-loop's last barrier); kfac_kl_finalize adds the slots in a fixed
+    // order: deterministic, no atomics
+    double* red = (double*)smem;
+    const double d = wave_reduce_sum_d(P.epi == EPI_FINAL ? (double)kl_part : 0.0);
+    if (lane == 0) red[wave] = d;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s = 0.0;
+      for (int w = 0; w < WM * WN; ++w) s += red[w];
+      kl[blockIdx.x] = s;
+    }
   }
 }
 

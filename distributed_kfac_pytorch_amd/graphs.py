@@ -43,7 +43,7 @@ csrc/graph_fix.hip): on this ROCm runtime a captured memset node does not
 reliably clear its target on replay, and MIOpen zeroes the accumulation
 workspace of ResNet-50's channels_last weight-gradient convolutions that way --
 replayed steps picked up whatever the previous user of that memory left
-(NaN / 1e30 gradients in layer2.0.conv1, scripts/probes/debug_fb_graph.py).
+(NaN / 1e30 gradients in layer2.0.conv1, found in round 1).
 Eager steps and replays run on one side stream, joined to the caller's
 stream by events; the device is synchronised once after each eager
 (inverse-update) step, which also drains the eigensolver's worker streams.
@@ -55,6 +55,11 @@ import torch
 from .ops import _lib
 
 __all__ = ['GraphedTrainStep']
+
+
+def _world_size():
+    import torch.distributed as dist
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
 class GraphedTrainStep(object):
@@ -80,6 +85,16 @@ class GraphedTrainStep(object):
             else [optimizers]
         self.warmup = warmup
         self.enabled = enabled and torch.cuda.is_available()
+        if self.enabled and not self.segmented and _world_size() > 1:
+            # a single-segment capture would record the step's collectives (the
+            # DDP reducer's all-reduce, K-FAC's factor / eigendata / gradient
+            # communication); a capture that failed on only some ranks would
+            # leave them running mismatched collectives.  Multi-rank steps
+            # use the segmented mode (collectives between graph replays).
+            warnings.warn('GraphedTrainStep: single-segment capture is disabled at world size '
+                          '> 1; use the segmented mode (forward_backward / communicate / '
+                          'update)')
+            self.enabled = False
         self.graphs = {}
         self.outputs = {}
         self._warm = {}
@@ -112,7 +127,9 @@ class GraphedTrainStep(object):
         if self.pre is not None:
             p = self.pre.param_groups[0]
             hp.append((p['lr'], p['damping'], p['kl_clip'], p['factor_decay'],
-                       p['factor_update_freq'], p['inv_update_freq']))
+                       p['factor_update_freq'], p['inv_update_freq'],
+                       # a rebuilt execution plan moves every buffer a graph addresses
+                       getattr(self.pre, 'plan_generation', 0)))
         return (seg, kind, tuple(hp))
 
     def _advance(self):

@@ -92,6 +92,8 @@ _SIGS = {
                                  c_int, c_vp, c_vp],
     'kfac_ormtr': [c_vp, c_vp, c_vp, c_int, c_int, c_vp],
     'kfac_pgemm': [c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp],
+    'kfac_kl_finalize': [c_vp, c_int, c_vp, c_vp],
+    'kfac_kl_elems_per_block': [],
     'kfac_gather_grad': [c_int, c_vp, c_int, c_vp],
     'kfac_split_copy': [c_int, c_vp, c_int, c_int, c_vp],
     'kfac_pgemm_record_size': [],

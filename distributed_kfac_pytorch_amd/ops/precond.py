@@ -110,10 +110,15 @@ def kl_dot(pairs):
     """
     v0 = pairs[0][0]
     if _lib.use_native(v0):
-        vg = torch.zeros((), dtype=torch.float64, device=v0.device)
-        _lib.check(_lib.lib().kfac_grouped_kl_dot(_records(pairs), len(pairs), _lib.ptr(vg),
-                                                  _lib.stream(v0.device)), 'kfac_grouped_kl_dot')
-        return vg
+        # result + one partial slot per workgroup (summed in a fixed order on
+        # the device: bit-identical on every rank)
+        L = _lib.lib()
+        per = int(L.kfac_kl_elems_per_block())
+        slots = sum((v.numel() + per - 1) // per for v, _ in pairs)
+        buf = torch.empty(1 + slots, dtype=torch.float64, device=v0.device)
+        _lib.check(L.kfac_grouped_kl_dot(_records(pairs), len(pairs), _lib.ptr(buf),
+                                         _lib.stream(v0.device)), 'kfac_grouped_kl_dot')
+        return buf[0]
     vg = torch.zeros((), dtype=torch.float64)
     for v, g in pairs:
         vg += (v.reshape(g.shape) * g).sum().double()

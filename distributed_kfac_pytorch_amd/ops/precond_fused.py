@@ -171,13 +171,18 @@ class FusedPreconditioner(object):
         self.x3 = precision == 'bf16x3'
         self.device = self.layers[0].module.weight.device if self.layers else None
         self.bufs = [_LayerBufs(l, self.x3, self.device) for l in self.layers]
-        self.kl = torch.zeros((), dtype=torch.float64, device=self.device)
         self._gather_sig = None
         self._stage_tables = None
         # superseded device tables stay alive: a captured graph may use them
         self._retired_tables = []
         self.damping = 0.0
         self._build_stage_tables()
+        # KL dot of the last stage: one f64 partial slot per workgroup of its
+        # launches, summed in a fixed order (deterministic: every rank derives
+        # the same clip scale); the result is slot 0
+        self._kl_slots = sum(tiles for _, _, _, tiles in self._stage_tables[3])
+        self.kl_buf = torch.zeros(1 + self._kl_slots, dtype=torch.float64, device=self.device)
+        self.kl = self.kl_buf[0]
 
     # ------------------------------------------------------------- tables
     def _build_stage_tables(self):
@@ -339,13 +344,17 @@ class FusedPreconditioner(object):
         stream = _lib.stream(self.device)
         recs = self._gather_table()
         _lib.check(L.kfac_gather_grad(self.prec, recs, len(recs), stream), 'kfac_gather_grad')
-        if with_kl:
-            self.kl.zero_()
         for i, launches in enumerate(self._stage_tables):
-            kl = _lib.ptr(self.kl) if (with_kl and i == 3) else None
+            slot = 1
             for tile, table, count, tiles in launches:
+                kl = _lib.c_vp(self.kl_buf.data_ptr() + 8 * slot) if (with_kl and i == 3) \
+                    else None
                 _lib.check(L.kfac_pgemm(self.prec, tile, _lib.ptr(table), count, tiles, kl,
                                         stream), 'kfac_pgemm')
+                slot += tiles
+        if with_kl:
+            _lib.check(L.kfac_kl_finalize(_lib.c_vp(self.kl_buf.data_ptr() + 8), self._kl_slots,
+                                          _lib.ptr(self.kl_buf), stream), 'kfac_kl_finalize')
         for b in self.bufs:
             b.layer.preconditioned_gradient = b.layer._split_pgrad(b.layer._pgrad_matrix())
         return self.kl if with_kl else None

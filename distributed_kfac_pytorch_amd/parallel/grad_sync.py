@@ -34,6 +34,7 @@ class GradientAllreduce(object):
         for p in params:
             by_dtype.setdefault(p.dtype, []).append(p)
         self.arenas = []
+        self.views = []      # (param, arena view)
         for dtype, ps in by_dtype.items():
             total = sum(p.numel() for p in ps)
             arena = torch.zeros(total, dtype=dtype, device=ps[0].device)
@@ -42,7 +43,9 @@ class GradientAllreduce(object):
                 n = p.numel()
                 if not _dense_strides(p):
                     raise ValueError('parameter with non-dense strides {}'.format(p.stride()))
-                p.grad = torch.as_strided(arena, p.shape, p.stride(), off)
+                view = torch.as_strided(arena, p.shape, p.stride(), off)
+                p.grad = view
+                self.views.append((p, view))
                 off += n
             self.arenas.append(arena)
         if self.world > 1:
@@ -56,11 +59,34 @@ class GradientAllreduce(object):
             arena.zero_()
 
     def check_views(self):
-        """True while every .grad is still a view of the arena (an optimizer
-        `zero_grad(set_to_none=True)` breaks this)."""
-        return all(a is not None for a in self.arenas)
+        """True while every .grad is still the arena view it was bound to (an
+        optimizer `zero_grad(set_to_none=True)` or a user assigning .grad
+        breaks this: the next backward allocates gradients outside the arena,
+        which an all-reduce of the arena would silently skip)."""
+        for p, view in self.views:
+            g = p.grad
+            if g is None or g.data_ptr() != view.data_ptr() or g.stride() != view.stride():
+                return False
+        return True
+
+    def rebind(self):
+        """Point every .grad back at its arena view, copying a gradient that
+        backward produced elsewhere into the arena (None -> zeros)."""
+        with torch.no_grad():
+            for p, view in self.views:
+                g = p.grad
+                if g is not None and g.data_ptr() == view.data_ptr() and \
+                        g.stride() == view.stride():
+                    continue
+                if g is None:
+                    view.zero_()
+                else:
+                    view.copy_(g)
+                p.grad = view
 
     def __call__(self):
+        if not self.check_views():
+            self.rebind()
         if self.world <= 1:
             return
         for arena in self.arenas:

@@ -71,7 +71,7 @@ def _check_factors_finite(jobs, mats):
     instead of an error (the data-dependent deflation / iteration logic of the
     solvers is not NaN-safe).  One multi-tensor norm and one host read per
     inverse update."""
-    if not mats or not mats[0].is_cuda:
+    if not mats:
         return
     norms = torch.stack(torch._foreach_norm(mats, 1))
     ok = torch.isfinite(norms)
@@ -199,6 +199,9 @@ class KFAC(optim.Optimizer):
             bool(int(__import__('os').environ.get('KFAC_COMM_CHECK', '0')))
         self.workers_assigned = False
         self.plan = None
+        self.plan_generation = 0
+        self._plan_shapes = None
+        self._retired_plans = []
         self.timer = PhaseTimer(enabled=profile)
         self.use_hip_graphs = use_hip_graphs
         if precond_precision not in precond_fused.PRECISIONS:
@@ -313,7 +316,11 @@ class KFAC(optim.Optimizer):
             state_dict = {k: v for k, v in state_dict.items() if k != 'layers'}
         super(KFAC, self).load_state_dict(state_dict)
         if compute_inverses:
-            self._assign_workers()
+            # keep the plan (and the arenas / fused operand buffers a captured
+            # graph addresses) when the factor shapes did not change
+            if not (self.workers_assigned and self.plan is not None and
+                    self._plan_shapes == self._factor_shapes()):
+                self._assign_workers()
             self.workers_assigned = True
             self.compute_inverses(damping=self.param_groups[0]['damping'])
             if self.comm_method in (CommMethod.COMM_OPT, CommMethod.HYBRID_OPT):
@@ -675,7 +682,12 @@ class KFAC(optim.Optimizer):
         # private fp32 snapshot: factor updates of steps k+1.. must not race the solve
         mats = [l.state[w].to(torch.float32, copy=True) for l, w in jobs]
         if not mats[0].is_cuda:
-            pend['results'] = self._solve_inverses(jobs, mats, damping)
+            try:
+                _check_factors_finite(jobs, mats)
+                pend['results'] = self._solve_inverses(jobs, mats, damping)
+            except BaseException:
+                self._pending_inv = None
+                raise
             return
         dev = mats[0].device
         cur = torch.cuda.current_stream(dev)
@@ -704,7 +716,14 @@ class KFAC(optim.Optimizer):
         pend = self._pending_inv
         if pend is not None and pend['future'] is not None:
             fut, pend['future'] = pend['future'], None
-            pend['results'], pend['event'] = fut.result()
+            try:
+                pend['results'], pend['event'] = fut.result()
+            except BaseException:
+                # the solve failed (e.g. non-finite factors): drop the update so
+                # the next step does not store a half-initialised result, and
+                # surface the original error
+                self._pending_inv = None
+                raise
 
     def _apply_lagged_inverses(self):
         self.wait_inverses()
@@ -843,10 +862,21 @@ class KFAC(optim.Optimizer):
             src_ranks = allocator.get_inv_ranks(a_locs[i])
             layer.assign_gradient_workers(src_ranks, allocator.get_grad_groups(src_ranks))
         device = self.layers[0].module.weight.device
+        if self.plan is not None:
+            # buffers of a superseded plan stay alive: a captured graph may
+            # still address them (GraphedTrainStep re-captures on the new
+            # plan_generation)
+            self._retired_plans.append((self.plan, self.fused))
         self.plan = ExecutionPlan(self.layers, world, rank, a_locs, g_locs, allocator,
                                   self.use_eigen_decomp, self.precompute_outer_eigen,
                                   self.inv_dtype, build_eig_arena=True, device=device)
+        self._plan_shapes = self._factor_shapes()
+        self.plan_generation += 1
+        self._graph = None
         self._build_fused()
+
+    def _factor_shapes(self):
+        return tuple((tuple(l.state['A'].shape), tuple(l.state['G'].shape)) for l in self.layers)
 
     def _compute_grad_scale(self):
         """sum_layers <v, g> * lr^2 -> KL-clip scale, kept on the device."""

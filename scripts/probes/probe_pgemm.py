@@ -51,10 +51,12 @@ fz._build_stage_tables()
 tot = timeit(lambda: fz.run(damping=0.001))
 print('%s: full chain %.3f ms  (%.1f GFLOP real, %.1f TFLOP/s)' % (prec, tot, sum(flops) / 1e9, sum(flops) / tot / 1e9))
 for i, launches in enumerate(fz._stage_tables):
-    kl = _lib.ptr(fz.kl) if i == 3 else None
-    def stage():
+    def stage(i=i, launches=launches):
+        slot = 1
         for tile, table, count, tiles in launches:
+            kl = _lib.c_vp(fz.kl_buf.data_ptr() + 8 * slot) if i == 3 else None
             L.kfac_pgemm(fz.prec, tile, _lib.ptr(table), count, tiles, kl, stream)
+            slot += tiles
     t = timeit(stage)
     desc = ' '.join('%s:%d' % ('big' if tl else 'small', n) for tl, _, _, n in launches)
     print('  stage %d: %.3f ms  %6.1f GFLOP  %6.1f TFLOP/s  tiles %s' % (i + 1, t, flops[i] / 1e9, flops[i] / t / 1e9, desc))

@@ -40,12 +40,16 @@ def main():
             n, b, graph, it, (time.perf_counter() - t) * 1e3,
             (time.perf_counter() - t) * 1e6 / n), flush=True)
     if os.environ.get('STAMPS'):
-        st = stamps.view(n, 16)[:, :10].cpu().double()
+        full = stamps.view(n, 16).cpu().double()
+        clk = (full[1:n - 2, 9] - full[1:n - 2, 8]) / ((full[1:n - 2, 6] - full[1:n - 2, 0]) * 10.0)
+        print('fin shader clock GHz: median %.2f  min %.2f  max %.2f' % (
+            clk.median().item(), clk.min().item(), clk.max().item()))
+        st = full[:, :7]
         d = (st[:, 1:] - st[:, :-1]) * 10.0   # 100 MHz -> ns
         for name, rows in (('first 64 cols', slice(1, 65)), ('middle', slice(n // 2, n // 2 + 64)),
                            ('last 64', slice(n - 65, n - 1))):
             print(name, 'phase ns:', ' '.join('%7.0f' % v for v in d[rows].mean(0).tolist()),
-                  ' total %.0f' % ((st[rows, 9] - st[rows, 0]) * 10).mean().item())
+                  ' total %.0f' % ((st[rows, 6] - st[rows, 0]) * 10).mean().item())
 
 
 if __name__ == '__main__':

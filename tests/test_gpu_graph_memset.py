@@ -5,7 +5,7 @@ clear its target on replay; MIOpen zeroes the accumulation workspace of the
 channels_last bf16 weight-gradient convolution it picks for ResNet-50's
 layer2.0.conv1 (cudnn.benchmark) with such a memset, so a replayed backward
 returned the previous user's bytes (1e30 after a poke, NaN in training:
-scripts/probes/debug_fb_graph.py POKE mode)."""
+the round-1 forward/backward graph investigation)."""
 import ctypes
 
 import pytest

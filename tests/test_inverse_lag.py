@@ -94,3 +94,34 @@ def test_lagged_strategy_equivalence(tmp_path, world, method):
         for step, (gs, rs) in enumerate(zip(res['grads'], ref_grads)):
             for a, b in zip(gs, rs):
                 assert torch.equal(a, b), (r, step, (a - b).abs().max().item())
+
+
+def test_lagged_solve_failure_surfaces_and_resets():
+    """A lagged solve over non-finite factors raises the solver's own error
+    (not a TypeError at the step that would store it), clears the pending
+    update, and training can continue once the factors are finite again."""
+    model, data, pre = _make(2)
+    opt = torch.optim.SGD(model.parameters(), lr=0.05, momentum=0.9)
+
+    def step(i):
+        x, y = data[i % len(data)]
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(model(x), y).backward()
+        pre.step()
+        opt.step()
+
+    for i in range(4):          # step 0: synchronous inverse; steps 1-3 plain
+        step(i)
+    layer = pre.layers[0]
+    saved = layer.state['A'].clone()
+    layer.state['A'].fill_(float('nan'))
+    pre.compute_factor_in_hook = True     # keep the poisoned factor through step 4
+    with pytest.raises(FloatingPointError):
+        step(4)                 # step 4 launches the lagged solve
+    assert pre._pending_inv is None
+    layer.state['A'].copy_(saved)
+    pre.param_groups[0]['step'] = 5
+    for i in range(5, 10):
+        step(i)
+    for p in model.parameters():
+        assert torch.isfinite(p).all()

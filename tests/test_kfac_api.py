@@ -209,3 +209,44 @@ def test_inplace_relu_after_conv_hooks():
     out.retain_grad()
     nn.functional.cross_entropy(lin(torch.relu(out).flatten(1)), y).backward()
     assert torch.allclose(pre.layers[0].g_outputs[0], out.grad)
+
+
+def test_grad_arena_rebinds_after_set_to_none():
+    """GradientAllreduce keeps averaging the right tensors when an optimizer's
+    zero_grad(set_to_none=True) made backward allocate .grad outside the arena."""
+    import torch.nn.functional as F
+    from distributed_kfac_pytorch_amd.parallel.grad_sync import GradientAllreduce
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.ReLU(), torch.nn.Linear(5, 3))
+    sync = GradientAllreduce(model)
+    assert sync.check_views()
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    opt.zero_grad(set_to_none=True)
+    x, y = torch.randn(4, 6), torch.randint(0, 3, (4,))
+    F.cross_entropy(model(x), y).backward()
+    want = [p.grad.clone() for p in model.parameters()]
+    assert not sync.check_views()
+    sync()
+    assert sync.check_views()
+    for (p, view), w in zip(sync.views, want):
+        assert p.grad.data_ptr() == view.data_ptr()
+        assert torch.equal(p.grad, w)
+
+
+def test_load_state_dict_keeps_plan_and_buffers():
+    """Reloading a checkpoint with unchanged factor shapes keeps the execution
+    plan (the arenas a captured graph addresses); the inverses are recomputed."""
+    import torch.nn.functional as F
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.ReLU(), torch.nn.Linear(5, 3))
+    pre = kfac.KFAC(model, factor_update_freq=1, inv_update_freq=2)
+    for _ in range(3):
+        x, y = torch.randn(4, 6), torch.randint(0, 3, (4,))
+        model.zero_grad()
+        F.cross_entropy(model(x), y).backward()
+        pre.step()
+    plan, gen = pre.plan, pre.plan_generation
+    qa = pre.layers[0].state['QA']
+    pre.load_state_dict(pre.state_dict())
+    assert pre.plan is plan and pre.plan_generation == gen
+    assert pre.layers[0].state['QA'].data_ptr() == qa.data_ptr()
