@@ -22,8 +22,10 @@ LIB = os.path.join(OUT_DIR, 'libkfac_hip.so')
 BUILD = os.path.join(ROOT, 'build', 'hip')
 ARCH = os.environ.get('KFAC_HIP_ARCH', 'gfx950')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+# kernarg preload: the first kernel arguments arrive in SGPRs, so a latency-
+# bound launch does not start with a scalar load round trip
 FLAGS = ['-O3', '-std=c++17', '-fPIC', '--offload-arch=' + ARCH, '-munsafe-fp-atomics',
-         '-Wno-unused-result']
+         '-Wno-unused-result', '-mllvm', '-amdgpu-kernarg-preload-count=16']
 
 
 # rocSOLVER/rocBLAS: tridiagonal divide-and-conquer stage of the large-factor

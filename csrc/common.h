@@ -56,3 +56,72 @@ __device__ __forceinline__ double wave_reduce_sum_d(double v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
 }
+
+// Global-address-space views of pointers that come from memory (record
+// tables): plain pointers loaded from a struct compile to flat_* accesses,
+// which wait on lgkmcnt as well as vmcnt.  gld_if is a branch-free predicated
+// load (clamped index + select): loads written as `if (ok) v = p[i]` become
+// one branch per load with a full wait inside, i.e. one memory round trip
+// each; these issue back to back and wait once.
+#define AS1 __attribute__((address_space(1)))
+typedef float fx4 __attribute__((ext_vector_type(4)));   // native vector: loads through AS1
+template <class T>
+__device__ __forceinline__ AS1 T* gptr(T* p) { return (AS1 T*)p; }
+template <class T>
+__device__ __forceinline__ const AS1 T* gptr(const T* p) { return (const AS1 T*)p; }
+template <class T>
+__device__ __forceinline__ T gld_if(const AS1 T* p, long long i, bool ok, T z) {
+  const T v = p[ok ? i : 0];
+  return ok ? v : z;
+}
+
+// Wave sums on the VALU (no LDS round trips): DPP quad_perm / half-mirror /
+// mirror inside each 16-lane row, then the gfx950 permlane16/32 swaps across
+// rows.  Every lane ends with the same value (each pairwise add is taken in
+// both orders, which are equal), in a fixed order: deterministic.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ float swap_sum16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float swap_sum32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ double swap_sum16_d(double v) {
+  const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
+}
+__device__ __forceinline__ double swap_sum32_d(double v) {
+  const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
+}
+__device__ __forceinline__ float wave_sum(float v) {
+  v += dpp_f<0xB1>(v);     // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);     // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);    // row_half_mirror
+  v += dpp_f<0x140>(v);    // row_mirror
+  return swap_sum32(swap_sum16(v));
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+  v += dpp_d<0xB1>(v);
+  v += dpp_d<0x4E>(v);
+  v += dpp_d<0x141>(v);
+  v += dpp_d<0x140>(v);
+  return swap_sum32_d(swap_sum16_d(v));
+}

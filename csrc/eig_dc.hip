@@ -61,21 +61,25 @@ constexpr int SRC_MASK = (1 << TYP_SHIFT) - 1;
 inline long long rup(long long a, long long b) { return (a + b - 1) / b * b; }
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
+// device pointers in the global address space: accesses through a record
+// loaded from memory compile to global_* (not flat_*, which also waits on
+// lgkmcnt)
 struct DcMat {
-  const float* d; const float* e;
-  float* dout; float* Zout; long long ldz;
-  float* Zw; float* ZpT; float* U; long long ldw;
-  double* dval; double* dl; double* wv; double* defv; double* rho;
-  double* gds; double* gzs; double* gdef;
-  int* kk; int* k1a; int* nrot; int* typepos; int* gsrc; int* dsrc; int* gsrcx; int* gdefsrc;
-  int* rp; float* rcs; int* info;
+  const AS1 float* d; const AS1 float* e;
+  AS1 float* dout; AS1 float* Zout; long long ldz;
+  AS1 float* Zw; AS1 float* ZpT; AS1 float* U; long long ldw;
+  AS1 double* dval; AS1 double* dl; AS1 double* wv; AS1 double* defv; AS1 double* rho;
+  AS1 double* gds; AS1 double* gzs; AS1 double* gdef;
+  AS1 int* kk; AS1 int* k1a; AS1 int* nrot; AS1 int* typepos; AS1 int* gsrc; AS1 int* dsrc;
+  AS1 int* gsrcx; AS1 int* gdefsrc;
+  AS1 int* rp; AS1 float* rcs; AS1 int* info;
   int n; int pad;
 };
 
 struct DcNode { int mat, lo, mid, hi; };
 
 __device__ inline double block_sum(double v, double* red) {
-  v = wave_reduce_sum_d(v);
+  v = wave_sum_d(v);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   __syncthreads();
   if (lane == 0) red[wave] = v;
@@ -219,7 +223,7 @@ __global__ __launch_bounds__(256) void dc_leaf_kernel(const DcMat* __restrict__ 
       rank += (dj < di) || (dj == di && j < i);
     }
     M.dval[lo + rank] = di;
-    float* row = M.Zw + (long long)(lo + rank) * M.ldw + lo;
+    AS1 float* row = M.Zw + (long long)(lo + rank) * M.ldw + lo;
     for (int c = 0; c < nl; ++c) row[c] = (float)V[i][c];
   }
   if (tid == 0) M.kk[lo] = nl;
@@ -227,7 +231,8 @@ __global__ __launch_bounds__(256) void dc_leaf_kernel(const DcMat* __restrict__ 
 
 // ------------------------------------------------------------------- prep
 // count of elements of the ascending run a[s, e) below v (or <= v)
-__device__ inline int run_count(const double* a, int s, int e, double v, bool le) {
+template <class P>
+__device__ inline int run_count(P a, int s, int e, double v, bool le) {
   int lo = s, hi = e;
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
@@ -249,21 +254,12 @@ __global__ __launch_bounds__(256) void dc_prep_kernel(const DcMat* __restrict__ 
   const int n1 = mid - lo, n2 = hi - mid, m = hi - lo;
   const long long ldw = M.ldw;
   const int tid = threadIdx.x;
-  double *sd, *sz, *sdef;
-  int *ssrc, *sdefsrc;
-  if (use_lds) {
-    sd = (double*)dyn;
-    sz = sd + m;
-    sdef = sz + m;
-    ssrc = (int*)(sdef + m);
-    sdefsrc = ssrc + m;
-  } else {
-    sd = M.dl + lo;      // unsorted staging; the sorted arrays live in gds / gzs
-    sz = M.wv + lo;
-    sdef = M.gdef + lo;
-    ssrc = M.gsrcx + lo;
-    sdefsrc = M.gdefsrc + lo;
-  }
+  // staging arrays in LDS (use_lds) or global scratch: the body is templated
+  // on their address space (a pointer that may be either compiles to flat_*
+  // accesses, slow in the serial deflation scan).  sd / sz / ssrc: unsorted
+  // staging of steps 1-2; sd2 / sz2 / ssrc2: the sorted arrays from step 3 on
+  auto body = [&](auto sd, auto sz, auto sdef, auto ssrc, auto sdefsrc, auto sd2, auto sz2,
+                  auto ssrc2, bool copy_sorted) {
   const double beta = (double)M.e[mid - 1];
   const int kL = M.kk[lo], kR = M.kk[mid];
   // -- 1. z from the children's boundary columns, eigenvalues (unsorted staging)
@@ -296,39 +292,35 @@ __global__ __launch_bounds__(256) void dc_prep_kernel(const DcMat* __restrict__ 
   }
   __threadfence_block();
   __syncthreads();
-  if (use_lds) {
+  if (copy_sorted) {
     for (int p = tid; p < m; p += 256) {
-      sd[p] = M.gds[lo + p];
-      sz[p] = M.gzs[lo + p];
-      ssrc[p] = M.gsrcx[lo + p];
+      sd2[p] = M.gds[lo + p];
+      sz2[p] = M.gzs[lo + p];
+      ssrc2[p] = M.gsrcx[lo + p];
     }
-  } else {
-    sd = M.gds + lo;
-    sz = M.gzs + lo;
-    ssrc = M.gsrcx + lo;
   }
   __syncthreads();
   // -- 3. deflation tolerance
   double dmx = 0.0, zmx = 0.0;
   for (int p = tid; p < m; p += 256) {
-    dmx = fmax(dmx, fabs(sd[p]));
-    zmx = fmax(zmx, fabs(sz[p]));
+    dmx = fmax(dmx, fabs(sd2[p]));
+    zmx = fmax(zmx, fabs(sz2[p]));
   }
   dmx = block_max(dmx, red);
   zmx = block_max(zmx, red);
   const double tol = 8.0 * EPS32 * fmax(dmx, rho * zmx);
   // -- 4. sequential deflation scan (LAPACK dlaed2 order); survivors compacted
-  // in place at the front of sd / sz / ssrc, deflated run ascending
+  // in place at the front of sd2 / sz2 / ssrc2, deflated run ascending
   if (tid == 0) {
     int q = 0, t = 0, r = 0;
     bool have = false;
     double pd = 0.0, pz = 0.0;
     int ps = 0;
-    int* rp = M.rp + 2LL * lo;
-    float* rcs = M.rcs + 2LL * lo;
+    AS1 int* rp = M.rp + 2LL * lo;
+    AS1 float* rcs = M.rcs + 2LL * lo;
     for (int p = 0; p < m; ++p) {
-      const double dp = sd[p], zp = sz[p];
-      const int sp = ssrc[p];
+      const double dp = sd2[p], zp = sz2[p];
+      const int sp = ssrc2[p];
       double dv = 0.0;
       int dsrc_v = -1;
       if (rho * fabs(zp) <= tol) {
@@ -354,7 +346,7 @@ __global__ __launch_bounds__(256) void dc_prep_kernel(const DcMat* __restrict__ 
           pz = tau;
           ps = (sp & SRC_MASK) | (typ << TYP_SHIFT);
         } else {
-          sd[q] = pd; sz[q] = pz; ssrc[q] = ps; ++q;
+          sd2[q] = pd; sz2[q] = pz; ssrc2[q] = ps; ++q;
           pd = dp; pz = zp; ps = sp;
           continue;
         }
@@ -370,7 +362,7 @@ __global__ __launch_bounds__(256) void dc_prep_kernel(const DcMat* __restrict__ 
       sdefsrc[j] = dsrc_v;
       ++t;
     }
-    if (have) { sd[q] = pd; sz[q] = pz; ssrc[q] = ps; ++q; }
+    if (have) { sd2[q] = pd; sz2[q] = pz; ssrc2[q] = ps; ++q; }
     sh_k = q;
     sh_nrot = r;
     M.kk[lo] = q;
@@ -384,7 +376,7 @@ __global__ __launch_bounds__(256) void dc_prep_kernel(const DcMat* __restrict__ 
   const int q0 = tid * chunk, q1 = (q0 + chunk < k) ? q0 + chunk : k;
   int c1 = 0, c2 = 0, c3 = 0;
   for (int q = q0; q < q1; ++q) {
-    const int ty = ssrc[q] >> TYP_SHIFT;
+    const int ty = ssrc2[q] >> TYP_SHIFT;
     c1 += ty == 1; c2 += ty == 2; c3 += ty == 3;
   }
   sh_cnt[0][tid] = c1; sh_cnt[1][tid] = c2; sh_cnt[2][tid] = c3;
@@ -404,30 +396,44 @@ __global__ __launch_bounds__(256) void dc_prep_kernel(const DcMat* __restrict__ 
     const int K1 = s1, K2 = s2, k1al = K1 & ~3;
     PGemm* L = table + 2 * blockIdx.x;
     PGemm* R = L + 1;
-    L->a_hi = L->a_lo = M.U + (long long)lo * ldw;
-    L->b_hi = L->b_lo = M.ZpT + (long long)lo * ldw;
-    L->c_hi = L->c_lo = M.Zw + (long long)lo * ldw + lo;
+    L->a_hi = L->a_lo = (const void*)(M.U + (long long)lo * ldw);
+    L->b_hi = L->b_lo = (const void*)(M.ZpT + (long long)lo * ldw);
+    L->c_hi = L->c_lo = (void*)(M.Zw + (long long)lo * ldw + lo);
     L->M = k; L->N = n1; L->K = K1 + K2;
-    R->a_hi = R->a_lo = M.U + (long long)lo * ldw + k1al;
-    R->b_hi = R->b_lo = M.ZpT + (long long)(lo + n1) * ldw + k1al;
-    R->c_hi = R->c_lo = M.Zw + (long long)lo * ldw + lo + n1;
+    R->a_hi = R->a_lo = (const void*)(M.U + (long long)lo * ldw + k1al);
+    R->b_hi = R->b_lo = (const void*)(M.ZpT + (long long)(lo + n1) * ldw + k1al);
+    R->c_hi = R->c_lo = (void*)(M.Zw + (long long)lo * ldw + lo + n1);
     R->M = k; R->N = n2; R->K = k - k1al;
   }
   __syncthreads();
   const int off2 = (int)red[0], off3 = (int)red[0] + (int)red[1];
   int p1 = sh_cnt[0][tid], p2 = off2 + sh_cnt[1][tid], p3 = off3 + sh_cnt[2][tid];
   for (int q = q0; q < q1; ++q) {
-    const int s = ssrc[q];
+    const int s = ssrc2[q];
     const int ty = s >> TYP_SHIFT;
     const int pos = (ty == 1) ? p1++ : (ty == 2) ? p2++ : p3++;
     M.typepos[lo + q] = pos;
     M.gsrc[lo + pos] = s & SRC_MASK;
-    M.dl[lo + q] = sd[q];
-    M.wv[lo + q] = sz[q];
+    M.dl[lo + q] = sd2[q];
+    M.wv[lo + q] = sz2[q];
   }
   for (int t = tid; t < m - k; t += 256) {
     M.defv[lo + t] = sdef[t];
     M.dsrc[lo + t] = sdefsrc[t];
+  }
+  };
+  if (use_lds) {
+    typedef __attribute__((address_space(3))) double lds_d;
+    typedef __attribute__((address_space(3))) int lds_i;
+    lds_d* sd = (lds_d*)dyn;
+    lds_d* sz = sd + m;
+    lds_d* sdef = sz + m;
+    lds_i* ssrc = (lds_i*)(sdef + m);
+    lds_i* sdefsrc = ssrc + m;
+    body(sd, sz, sdef, ssrc, sdefsrc, sd, sz, ssrc, true);
+  } else {
+    body(M.dl + lo, M.wv + lo, M.gdef + lo, M.gsrcx + lo, M.gdefsrc + lo, M.gds + lo, M.gzs + lo,
+         M.gsrcx + lo, false);
   }
 }
 
@@ -440,14 +446,14 @@ __global__ __launch_bounds__(256) void dc_rotate_kernel(const DcMat* __restrict_
   const int c = blockIdx.x * 256 + threadIdx.x;
   const int nr = M.nrot[lo];
   if (c >= m || nr == 0) return;
-  const int* rp = M.rp + 2LL * lo;
-  const float* rcs = M.rcs + 2LL * lo;
-  float* base = M.Zw + (long long)lo * M.ldw + lo + c;
+  const AS1 int* rp = M.rp + 2LL * lo;
+  const AS1 float* rcs = M.rcs + 2LL * lo;
+  AS1 float* base = M.Zw + (long long)lo * M.ldw + lo + c;
   for (int r = 0; r < nr; ++r) {
     const int p = rp[2 * r], q = rp[2 * r + 1];
     const float cs = rcs[2 * r], sn = rcs[2 * r + 1];
-    float* xp = base + (long long)p * M.ldw;
-    float* yp = base + (long long)q * M.ldw;
+    AS1 float* xp = base + (long long)p * M.ldw;
+    AS1 float* yp = base + (long long)q * M.ldw;
     const float x = *xp, y = *yp;
     *xp = cs * x + sn * y;
     *yp = cs * y - sn * x;
@@ -473,8 +479,8 @@ __global__ __launch_bounds__(256) void dc_gather_kernel(const DcMat* __restrict_
     const int t = b - tiles;
     if (t >= m - k) return;
     const int src = M.dsrc[lo + t];
-    const float* s = M.Zw + (long long)(lo + (src < 0 ? 0 : src)) * ldw + lo;
-    float* o = M.U + (long long)(lo + k + t) * ldw;
+    const AS1 float* s = M.Zw + (long long)(lo + (src < 0 ? 0 : src)) * ldw + lo;
+    AS1 float* o = M.U + (long long)(lo + k + t) * ldw;
     for (int c = tid; c < m; c += 256) o[c] = s[c];
     return;
   }
@@ -523,23 +529,15 @@ __global__ __launch_bounds__(64 * RPB) void dc_secular_kernel(const DcMat* __res
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int i = blockIdx.x * RPB + wave;
   if (blockIdx.x * RPB >= m) return;   // uniform per block
-  const double* D = M.dl + lo;
-  const double* W = M.wv + lo;
-  if (use_lds) {
-    double* sD = (double*)dyn;
-    double* sW = sD + k;
-    for (int q = threadIdx.x; q < k; q += 64 * RPB) {
-      sD[q] = D[q];
-      sW[q] = W[q];
-    }
-    __syncthreads();
-    D = sD;
-    W = sW;
-  }
+  const AS1 double* Dg = M.dl + lo;
+  const AS1 double* Wg = M.wv + lo;
+  // the solve, templated on where D / W live (LDS or global): a pointer that
+  // may be either compiles to flat_* loads in the innermost loop
+  auto solve = [&](auto D, auto W) {
   if (i >= m) return;
   if (i >= k) {   // deflated row: U row (staged by the gather) -> Z row, its eigenvalue
-    const float* s = M.U + (long long)(lo + i) * ldw;
-    float* o = M.Zw + (long long)(lo + i) * ldw + lo;
+    const AS1 float* s = M.U + (long long)(lo + i) * ldw;
+    AS1 float* o = M.Zw + (long long)(lo + i) * ldw + lo;
     for (int c = lane; c < m; c += 64) o[c] = s[c];
     if (lane == 0) M.dval[lo + i] = M.defv[lo + i - k];
     return;
@@ -552,13 +550,13 @@ __global__ __launch_bounds__(64 * RPB) void dc_secular_kernel(const DcMat* __res
     const double Di = D[i];
     double f = 0.0;
     for (int q = lane; q < k; q += 64) f += rho * W[q] * W[q] / ((D[q] - Di) - mid);
-    f = 1.0 + wave_reduce_sum_d(f);
+    f = 1.0 + wave_sum_d(f);
     if (f >= 0.0) { o = i; tlo = 0.0; thi = mid; }
     else { o = i + 1; tlo = -mid; thi = 0.0; }
   } else {
     double s = 0.0;
     for (int q = lane; q < k; q += 64) s += rho * W[q] * W[q];
-    o = k - 1; tlo = 0.0; thi = wave_reduce_sum_d(s);
+    o = k - 1; tlo = 0.0; thi = wave_sum_d(s);
   }
   const double Do = D[o];
   const int left = (o == i) ? o : o - 1;
@@ -570,20 +568,20 @@ __global__ __launch_bounds__(64 * RPB) void dc_secular_kernel(const DcMat* __res
   for (; it < MAX_IT; ++it) {
     double f = 0.0, fa = 0.0, psi = 0.0, dpsi = 0.0, phi = 0.0, dphi = 0.0;
     for (int q = lane; q < k; q += 64) {
-      const double den = (D[q] - Do) - x;
-      const double term = rho * W[q] * W[q] / den;
-      const double dterm = term / den;
+      const double rden = 1.0 / ((D[q] - Do) - x);
+      const double term = rho * W[q] * W[q] * rden;
+      const double dterm = term * rden;
       f += term;
       fa += fabs(term);
       if (q <= left) { psi += term; dpsi += dterm; }
       else { phi += term; dphi += dterm; }
     }
-    f = 1.0 + wave_reduce_sum_d(f);
-    fa = wave_reduce_sum_d(fa);
-    psi = wave_reduce_sum_d(psi);
-    dpsi = wave_reduce_sum_d(dpsi);
-    phi = wave_reduce_sum_d(phi);
-    dphi = wave_reduce_sum_d(dphi);
+    f = 1.0 + wave_sum_d(f);
+    fa = wave_sum_d(fa);
+    psi = wave_sum_d(psi);
+    dpsi = wave_sum_d(dpsi);
+    phi = wave_sum_d(phi);
+    dphi = wave_sum_d(dphi);
     if (fabs(f) <= 16.0 * EPS64 * (1.0 + fa)) break;
     if (f < 0.0) tlo = x; else thi = x;
     if (thi - tlo <= 4.0 * EPS64 * fmax(fabs(tlo), fabs(thi))) break;
@@ -612,23 +610,37 @@ __global__ __launch_bounds__(64 * RPB) void dc_secular_kernel(const DcMat* __res
     }
     x = y;
   }
-  if (it == MAX_IT && lane == 0) atomicAdd(M.info, 1);
+  if (it == MAX_IT && lane == 0) atomicAdd((int*)M.info, 1);
   // eigenvector row i: u_q = w_q / (d_q - lambda), normalised, in type order
   double nrm = 0.0;
   for (int q = lane; q < k; q += 64) {
     const double u = W[q] / ((D[q] - Do) - x);
     nrm += u * u;
   }
-  nrm = wave_reduce_sum_d(nrm);
+  nrm = wave_sum_d(nrm);
   const double inv = nrm > 0.0 ? 1.0 / sqrt(nrm) : 0.0;
-  float* urow = M.U + (long long)(lo + i) * ldw;
-  const int* tp = M.typepos + lo;
+  AS1 float* urow = M.U + (long long)(lo + i) * ldw;
+  const AS1 int* tp = M.typepos + lo;
   for (int q = lane; q < k; q += 64) {
     const double u = W[q] / ((D[q] - Do) - x);
     urow[tp[q]] = (float)(u * inv);
   }
   for (int q = k + lane; q < k + PADK; q += 64) urow[q] = 0.f;
   if (lane == 0) M.dval[lo + i] = Do + x;
+  };
+  if (use_lds) {
+    typedef __attribute__((address_space(3))) double lds_double;
+    lds_double* sD = (lds_double*)dyn;
+    lds_double* sW = sD + k;
+    for (int q = threadIdx.x; q < k; q += 64 * RPB) {
+      sD[q] = Dg[q];
+      sW[q] = Wg[q];
+    }
+    __syncthreads();
+    solve((const lds_double*)sD, (const lds_double*)sW);
+  } else {
+    solve(Dg, Wg);
+  }
 }
 
 // ------------------------------------------------------------------- final
@@ -648,8 +660,8 @@ __global__ __launch_bounds__(256) void dc_final_kernel(const DcMat* __restrict__
     sh_rank = rank;
   }
   __syncthreads();
-  const float* s = M.Zw + (long long)i * M.ldw;
-  float* o = M.Zout + (long long)sh_rank * M.ldz;
+  const AS1 float* s = M.Zw + (long long)i * M.ldw;
+  AS1 float* o = M.Zout + (long long)sh_rank * M.ldz;
   for (int c = threadIdx.x; c < n; c += 256) o[c] = s[c];
 }
 
@@ -708,20 +720,23 @@ DcMat carve(const float* d, const float* e, float* dout, float* Zout, long long 
             unsigned char* ws, int n) {
   DcMat M;
   memset(&M, 0, sizeof(M));
-  M.d = d; M.e = e; M.dout = dout; M.Zout = Zout; M.ldz = ldz; M.n = n;
+  M.d = (const AS1 float*)d; M.e = (const AS1 float*)e;
+  M.dout = (AS1 float*)dout; M.Zout = (AS1 float*)Zout; M.ldz = ldz; M.n = n;
   M.ldw = rup(n + PADK, 64);
   size_t off = 0;
   auto take = [&](size_t bytes) { unsigned char* p = ws + off; off += al256(bytes); return p; };
   const size_t mat = (size_t)n * M.ldw * 4;
-  M.Zw = (float*)take(mat); M.ZpT = (float*)take(mat); M.U = (float*)take(mat);
-  M.dval = (double*)take(n * 8); M.dl = (double*)take(n * 8); M.wv = (double*)take(n * 8);
-  M.defv = (double*)take(n * 8); M.rho = (double*)take(n * 8); M.gds = (double*)take(n * 8);
-  M.gzs = (double*)take(n * 8); M.gdef = (double*)take(n * 8);
-  M.kk = (int*)take(n * 4); M.k1a = (int*)take(n * 4); M.nrot = (int*)take(n * 4);
-  M.typepos = (int*)take(n * 4); M.gsrc = (int*)take(n * 4); M.dsrc = (int*)take(n * 4);
-  M.gsrcx = (int*)take(n * 4); M.gdefsrc = (int*)take(n * 4);
-  M.rp = (int*)take(2 * n * 4); M.rcs = (float*)take(2 * n * 4);
-  M.info = (int*)take(4);
+  M.Zw = (AS1 float*)take(mat); M.ZpT = (AS1 float*)take(mat); M.U = (AS1 float*)take(mat);
+  M.dval = (AS1 double*)take(n * 8); M.dl = (AS1 double*)take(n * 8);
+  M.wv = (AS1 double*)take(n * 8); M.defv = (AS1 double*)take(n * 8);
+  M.rho = (AS1 double*)take(n * 8); M.gds = (AS1 double*)take(n * 8);
+  M.gzs = (AS1 double*)take(n * 8); M.gdef = (AS1 double*)take(n * 8);
+  M.kk = (AS1 int*)take(n * 4); M.k1a = (AS1 int*)take(n * 4); M.nrot = (AS1 int*)take(n * 4);
+  M.typepos = (AS1 int*)take(n * 4); M.gsrc = (AS1 int*)take(n * 4);
+  M.dsrc = (AS1 int*)take(n * 4); M.gsrcx = (AS1 int*)take(n * 4);
+  M.gdefsrc = (AS1 int*)take(n * 4);
+  M.rp = (AS1 int*)take(2 * n * 4); M.rcs = (AS1 float*)take(2 * n * 4);
+  M.info = (AS1 int*)take(4);
   return M;
 }
 
@@ -766,7 +781,8 @@ int build_plan(const std::vector<DcMat>& mats, DcPlan& P) {
         r.lda = M.ldw; r.ldb = M.ldw; r.ldc = M.ldw;
         r.M = 0; r.N = side ? n2 : n1; r.K = 0; r.epi = EPI_STORE;
         // placeholders until the prep kernel patches them (never read with M = 0)
-        r.a_hi = r.a_lo = M.U; r.b_hi = r.b_lo = M.ZpT; r.c_hi = r.c_lo = M.Zw;
+        r.a_hi = r.a_lo = (const void*)M.U; r.b_hi = r.b_lo = (const void*)M.ZpT;
+        r.c_hi = r.c_lo = (void*)M.Zw;
         r.tiles_n = cdiv(r.N, 128);
         r.tile_begin = tiles;
         tiles += cdiv(m, 128) * r.tiles_n;

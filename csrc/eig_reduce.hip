@@ -42,13 +42,11 @@ namespace {
 constexpr int TB = 128;        // symv / update tile
 constexpr int FB = 256;        // rows per fin workgroup
 constexpr int NB = 32;         // panel width
-constexpr int RSW = 2 + 2 * NB + 2;   // fin partials: |xh|^2, xh.a, W^T xh, V^T xh (+pad)
+constexpr int RSW = 64;       // fin partial kinds per block (see K_W / K_V)
 constexpr int MAXM = 255;      // matrices per batch
 constexpr int NTMAX = 40;      // 128-row blocks (n <= 5120)
 constexpr int PQ4 = NTMAX / 4; // float4 loads of a row's yh partials
 constexpr int NFMAX = (NTMAX * TB + FB - 1) / FB;   // fin blocks
-constexpr int TSL = (NTMAX * 64 + 255) / 256;       // tile partial loads per thread
-constexpr int TWS = FB + 1;    // LDS stride of the fin partial transpose
 
 struct RMat {
   float* A; long long lda; int n; int nt; int nf; int pad;
@@ -82,37 +80,65 @@ __device__ inline void hh_scalars(double alpha, double sig2, double& beta, doubl
   }
 }
 
-// workgroup -> (matrix, local index) from the launch's host-built offsets
+// workgroup -> (matrix, local index) from the launch's host-built offsets:
+// one compare per thread (offsets ascending), not a serial scan
 __device__ inline void map_block(const int* __restrict__ offs, int nact, int* soff, int& mat,
                                  int& local) {
-  __shared__ int sm[2];
-  if ((int)threadIdx.x <= nact) soff[threadIdx.x] = offs[threadIdx.x];
+  __shared__ int sm;
+  const int t = threadIdx.x, b = blockIdx.x;
+  if (t <= nact) soff[t] = offs[t];
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const int b = blockIdx.x;
-    int mi = 0;
-    while (mi + 1 < nact && soff[mi + 1] <= b) ++mi;
-    sm[0] = mi;
-    sm[1] = b - soff[mi];
+  if (t < nact && soff[t] <= b && b < soff[t + 1]) sm = t;
+  __syncthreads();
+  mat = sm;
+  local = b - soff[mat];
+}
+
+// in-register transpose-reduce of 64 values per lane over the wave: lane L
+// ends with the wave sum of value L (63 shuffles; pairwise, fixed order)
+template <int M>
+__device__ __forceinline__ void butterfly_stage(float (&v)[64], int lane) {
+  const bool up = (lane & M) != 0;
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const float send = up ? v[i] : v[i + M];
+    const float keep = up ? v[i + M] : v[i];
+    v[i] = keep + __shfl_xor(send, M, 64);
   }
-  __syncthreads();
-  mat = sm[0];
-  local = sm[1];
+}
+__device__ __forceinline__ float butterfly64(float (&v)[64]) {
+  const int lane = threadIdx.x & 63;
+  butterfly_stage<32>(v, lane);
+  butterfly_stage<16>(v, lane);
+  butterfly_stage<8>(v, lane);
+  butterfly_stage<4>(v, lane);
+  butterfly_stage<2>(v, lane);
+  butterfly_stage<1>(v, lane);
+  return v[0];
 }
 
 // ------------------------------------------------------------------- fin
-struct FinShared {
-  double scal[8];                 // beta, tau, s, alpha2, prev d
-  double red[3 * RSW + 8];
+// partial-sum kinds of a fin block (RSW = 64: one per lane of the butterfly):
+// |xh|^2, xh.a, W^T xh and V^T xh over the panel columns before the current
+// one (at most NB - 1 of them)
+constexpr int K_W = 2, K_V = 2 + (NB - 1);
+static_assert(K_V + NB - 1 == RSW, "fin partial kinds must fill one wave");
+constexpr int TSQ = (NTMAX * (NTMAX + 1) / 2 + 63) / 64;   // tile-sum loads per lane
+
+struct FinWave {                  // one wave's private slice (no barrier needed)
   float s12[2 * NB];              // s1, s2
-  float vwj[4][NB];               // V[j], W[j], V[j+1], W[j+1] (full panel columns)
+  float vw[4][NB];                // V[j], W[j], V[j+1], W[j+1] (current panel columns)
 };
 
+// Every wave of every fin workgroup derives column j-1's scalars and rows
+// j / j+1 itself (redundantly, from the same partials, in the same order), so
+// the waves never wait for each other until the block's partial sums at the
+// end; the cross-lane sums are DPP / permlane (common.h wave_sum*).
 __global__ __launch_bounds__(256) void sytrd_fin_kernel(const RMat* __restrict__ mats,
                                                         const int* __restrict__ offs, int nact,
                                                         int j) {
-  extern __shared__ __attribute__((aligned(16))) float tw[];    // [RSW][TWS] partial transpose
-  __shared__ FinShared S;
+  __shared__ FinWave SW[4];
+  __shared__ float wred[4][RSW];
   __shared__ int soff[MAXM + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   unsigned long long* const stamps = blockIdx.x == 0 ? g_stamps : nullptr;
@@ -125,8 +151,9 @@ __global__ __launch_bounds__(256) void sytrd_fin_kernel(const RMat* __restrict__
   const long long lda = M.lda;
   const int bf = j / FB + local;           // this workgroup's 256-row block
   const int r = bf * FB + tid;
-  const bool lead = (local == 0);
+  const bool lead = (local == 0 && wave == 0);
   const bool fin = (j == n - 1);
+  const bool has1 = (j + 1 < n);
   const int c = j % NB;
   const int cp = (j >= 1) ? (c == 0 ? NB - 1 : c - 1) : 0;
   const bool pstart = (c == 0 && j > 0);
@@ -134,151 +161,146 @@ __global__ __launch_bounds__(256) void sytrd_fin_kernel(const RMat* __restrict__
   const int cs = j & 1, ps = cs ^ 1;
   const int s0p = j / TB;                  // first tile block of symv(j-1)
   const int ntp = (nt + 3) & ~3;
-  const int nbp = nt - s0p;
+  const int ntri = (nt - s0p) * (nt - s0p + 1) / 2;   // tiles of symv(j-1)
   const int f0p = (j - 1) / FB;            // first fin block of fin(j-1)
-  const float* Pp = M.P + ps * M.sP;
-  const float* XHp = M.XH + ps * M.sXH;
+  const AS1 float* Pp = gptr(M.P) + ps * M.sP;
+  const AS1 float* XHp = gptr(M.XH) + ps * M.sXH;
+  const AS1 float* RSp = gptr(M.RS) + ps * M.sRS;
+  const AS1 float* TSp = gptr(M.TS) + ps * M.sTS;
+  AS1 float* const gA = gptr(M.A);
+  AS1 float* const gV = gptr(M.V);
+  AS1 float* const gW = gptr(M.W);
+  AS1 float* const gSC = gptr(M.SC);
   STAMP(1);
 
-  // ---- every load, in the order it is needed
-  // step-1 partials: fin(j-1) blocks x kinds (3 groups), symv(j-1) tile sums
-  double rsacc = 0.0, ts = 0.0;
-  const int rk = tid % RSW, rg = tid / RSW;
-  if (j >= 1) {
-    const float* RSp = M.RS + ps * M.sRS;
-    if (tid < 3 * RSW && (rk < 2 + cp || (rk >= 2 + NB && rk < 2 + NB + cp))) {
-      float v[(NFMAX + 2) / 3];
+  // ---- every load up front, branch-free (one memory round trip)
+  const bool j1 = (j >= 1);
+  // fin(j-1) block partials: lane x < cp sums kinds W_x / V_x over the
+  // blocks, lane u < #blocks takes |xh|^2 and xh.a of block f0p + u
+  float rw_[NFMAX], rv_[NFMAX];
 #pragma unroll
-      for (int u = 0; u < (NFMAX + 2) / 3; ++u) {
-        const int bb = f0p + rg + 3 * u;
-        v[u] = (bb < M.nf) ? RSp[(long long)bb * RSW + rk] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < (NFMAX + 2) / 3; ++u) rsacc += (double)v[u];
-    }
-    const float* TSp = M.TS + ps * M.sTS;
-    float tv[TSL];
-#pragma unroll
-    for (int u = 0; u < TSL; ++u) {      // (a, b) on a 64-wide virtual grid
-      const int f = tid + 256 * u;
-      const int ao = f >> 6, bo = f & 63;
-      tv[u] = 0.f;
-      if (ao < nbp && bo < nbp && ao <= bo) tv[u] = TSp[(long long)(s0p + ao) * nt + s0p + bo];
-    }
-#pragma unroll
-    for (int u = 0; u < TSL; ++u) ts += (double)tv[u];
+  for (int u = 0; u < NFMAX; ++u) {
+    const int bb = f0p + u;
+    const bool ok = j1 && lane < cp && bb < M.nf;
+    rw_[u] = gld_if(RSp, bb * RSW + K_W + lane, ok, 0.f);
+    rv_[u] = gld_if(RSp, bb * RSW + K_V + lane, ok, 0.f);
   }
-  // rows j / j+1 (waves 0 / 1)
-  const int rw = j + wave;
-  float vrow = 0.f, wrow = 0.f, pw = 0.f, xw = 0.f, aw = 0.f;
-  if (wave < 2 && rw < n) {
-    if (lane < NB) {
-      vrow = M.V[(long long)rw * NB + lane];
-      wrow = M.W[(long long)rw * NB + lane];
-    }
-    if (j >= 1) {
-      if (lane >= s0p && lane < nt) pw = Pp[(long long)rw * ntp + lane];
-      xw = XHp[rw];
-    }
-    aw = M.A[(long long)j * lda + rw];     // row j of the panel's base matrix
-  }
-  // this thread's row
+  const bool okb = j1 && f0p + lane < M.nf;
+  const float rs0 = gld_if(RSp, (f0p + lane) * RSW, okb, 0.f);
+  const float rs1 = gld_if(RSp, (f0p + lane) * RSW + 1, okb, 0.f);
+  float tq[TSQ];                           // symv(j-1) tile sums, triangle order
+#pragma unroll
+  for (int u = 0; u < TSQ; ++u) tq[u] = gld_if(TSp, lane + 64 * u, j1 && lane + 64 * u < ntri, 0.f);
+  const bool okp = j1 && lane >= s0p && lane < nt;
+  const float pj = gld_if(Pp, j * ntp + lane, okp, 0.f);
+  const float pj1 = gld_if(Pp, (j + 1) * ntp + lane, okp && has1, 0.f);
+  const float xhj1 = gld_if(XHp, j + 1, j1 && has1, 0.f);
+  const float alpha = gSC[ps * 4];
+  const float dprev = gSC[ps * 4 + 1];
+  float vj = gld_if(gV, j * NB + lane, lane < NB, 0.f);
+  float wj = gld_if(gW, j * NB + lane, lane < NB, 0.f);
+  float vj1 = gld_if(gV, (j + 1) * NB + lane, lane < NB && has1, 0.f);
+  float wj1 = gld_if(gW, (j + 1) * NB + lane, lane < NB && has1, 0.f);
+  const float ajj = gA[(long long)j * lda + j];
+  const float ajj1 = gld_if(gA, (long long)j * lda + j + 1, has1, 0.f);
+  // this thread's row (loads from a clamped row; unused lanes masked later)
   const bool rok = r < n && r >= j;
+  const int rc = min(r, n - 1);
   float vr[NB], wr[NB];
-#pragma unroll
-  for (int x = 0; x < NB; ++x) { vr[x] = 0.f; wr[x] = 0.f; }
-  float xhp = 0.f, arow = 0.f, brow = 0.f;
-  float4 pq[PQ4];
-#pragma unroll
-  for (int u = 0; u < PQ4; ++u) pq[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (rok) {
+  {
+    const AS1 fx4* v4 = (const AS1 fx4*)(gV + rc * NB);
+    const AS1 fx4* w4 = (const AS1 fx4*)(gW + rc * NB);
 #pragma unroll
     for (int x = 0; x < NB / 4; ++x) {
-      if (4 * x < cc) {
-        const float4 a4 = *(const float4*)(M.V + (long long)r * NB + 4 * x);
-        const float4 b4 = *(const float4*)(M.W + (long long)r * NB + 4 * x);
-        vr[4 * x] = a4.x; vr[4 * x + 1] = a4.y; vr[4 * x + 2] = a4.z; vr[4 * x + 3] = a4.w;
-        wr[4 * x] = b4.x; wr[4 * x + 1] = b4.y; wr[4 * x + 2] = b4.z; wr[4 * x + 3] = b4.w;
-      }
-    }
-    arow = M.A[(long long)j * lda + r];                       // base row j
-    if (j + 1 < n && r >= j + 1) brow = M.A[(long long)(j + 1) * lda + r];   // base row j+1
-    if (j >= 1) {
-      xhp = XHp[r];
-      const float4* pp = (const float4*)(Pp + (long long)r * ntp);
-#pragma unroll
-      for (int u = 0; u < PQ4; ++u)
-        if (4 * u + 3 >= s0p && 4 * u < nt) pq[u] = pp[u];
+      const fx4 a4 = v4[x], b4 = w4[x];
+      vr[4 * x] = a4.x; vr[4 * x + 1] = a4.y; vr[4 * x + 2] = a4.z; vr[4 * x + 3] = a4.w;
+      wr[4 * x] = b4.x; wr[4 * x + 1] = b4.y; wr[4 * x + 2] = b4.z; wr[4 * x + 3] = b4.w;
     }
   }
+  const float arow = gA[(long long)j * lda + rc];                              // base row j
+  const float brow = gld_if(gA, (long long)(j + 1) * lda + rc, has1 && r >= j + 1, 0.f);
+  const float xhp = XHp[rc];
+  fx4 pq[PQ4];
+  {
+    const AS1 fx4* pp = (const AS1 fx4*)(Pp + rc * ntp);
+    const fx4 z4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < PQ4; ++u) pq[u] = gld_if(pp, u, j1 && 4 * u + 3 >= s0p && 4 * u < nt, z4);
+  }
+  double pW = 0.0, pV = 0.0, pT = 0.0;
+#pragma unroll
+  for (int u = 0; u < NFMAX; ++u) { pW += (double)rw_[u]; pV += (double)rv_[u]; }
+#pragma unroll
+  for (int u = 0; u < TSQ; ++u) pT += (double)tq[u];
+  const double pS = rs0, pA = rs1;
   STAMP(2);
 
-  // ---- step 1: scalars of column j-1 (every workgroup, same fixed order)
-  if (wave < 2 && lane < NB) {
-    S.vwj[2 * wave][lane] = vrow;
-    S.vwj[2 * wave + 1][lane] = wrow;
-  }
+  // ---- step 1 (per wave): scalars of column j-1; step 2 for rows j, j+1
+  double beta_p = 0.0, tau_p = 0.0, s_p = 0.0, alpha2 = 0.0;
+  float s1f = 0.f, s2f = 0.f;
   if (j >= 1) {
-    if (tid < 3 * RSW) S.red[tid] = rsacc;
-    ts = wave_reduce_sum_d(ts);
-    if (lane == 0) S.red[3 * RSW + wave] = ts;
-  }
-  __syncthreads();
-  if (j >= 1) {
-    if (wave == 0) {
-      auto R = [&](int k) { return S.red[k] + S.red[RSW + k] + S.red[2 * RSW + k]; };
-      const double sig2 = R(0), xa = R(1);
-      const double xy = S.red[3 * RSW] + S.red[3 * RSW + 1] + S.red[3 * RSW + 2] +
-                        S.red[3 * RSW + 3];
-      const float* SCp = M.SC + ps * 4;
-      const double alpha = SCp[0];
-      double beta, tau, sc;
-      hh_scalars(alpha, sig2, beta, tau, sc);
-      // s1 = W^T v, s2 = V^T v over rows >= j (v[j] = 1): row j of the panel
-      double s1 = 0.0, s2 = 0.0;
-      if (lane < cp) {
-        s1 = (double)S.vwj[1][lane] + sc * R(2 + lane);
-        s2 = (double)S.vwj[0][lane] + sc * R(2 + NB + lane);
-      }
-      const double s1s2 = wave_reduce_sum_d(s1 * s2);
-      if (lane < NB) {
-        S.s12[lane] = (float)s1;
-        S.s12[NB + lane] = (float)s2;
+    const double sig2 = wave_sum_d(pS), xa = wave_sum_d(pA), xy = wave_sum_d(pT);
+    hh_scalars((double)alpha, sig2, beta_p, tau_p, s_p);
+    // s1 = W^T v, s2 = V^T v over rows >= j (v[j] = 1): row j of the panel
+    double s1 = 0.0, s2 = 0.0;
+    if (lane < cp) {
+      s1 = (double)wj + s_p * pW;
+      s2 = (double)vj + s_p * pV;
+    }
+    const double s1s2 = wave_sum_d(s1 * s2);
+    const double vy = (double)ajj + 2.0 * s_p * xa + s_p * s_p * xy;
+    alpha2 = -0.5 * tau_p * tau_p * (vy - 2.0 * s1s2);
+    s1f = (float)s1;
+    s2f = (float)s2;
+    const float yv = wave_sum(pj), yv1 = wave_sum(pj1);
+    const float cj = wave_sum(lane < cp ? vj * s1f + wj * s2f : 0.f);
+    const float cj1 = wave_sum(lane < cp ? vj1 * s1f + wj1 * s2f : 0.f);
+    const float ww = (float)(tau_p * ((double)ajj + s_p * (double)yv - (double)cj) + alpha2);
+    const float vv1 = (float)(s_p * (double)xhj1);
+    const float ww1 = (float)(tau_p * ((double)ajj1 + s_p * (double)yv1 - (double)cj1) +
+                              alpha2 * (double)vv1);
+    if (lane == cp) {
+      vj = 1.f; wj = ww;
+      vj1 = vv1; wj1 = ww1;
+    }
+    if (lead) {
+      if (lane == cp) {
+        gV[j * NB + cp] = 1.f;
+        gW[j * NB + cp] = ww;
       }
       if (lane == 0) {
-        const double vy = (double)M.A[(long long)j * lda + j] + 2.0 * sc * xa + sc * sc * xy;
-        S.scal[0] = beta; S.scal[1] = tau; S.scal[2] = sc; S.scal[4] = SCp[1];
-        S.scal[3] = -0.5 * tau * tau * (vy - 2.0 * s1s2);
+        M.d[j - 1] = dprev;
+        M.e[j - 1] = (float)beta_p;
+        M.tau[j - 1] = (float)tau_p;
+        gA[(long long)(j - 1) * lda + j] = (float)beta_p;
       }
     }
-    __syncthreads();
   }
-  const double beta_p = S.scal[0], tau_p = S.scal[1], s_p = S.scal[2], alpha2 = S.scal[3];
+  {   // d_j = A(j, j) - 2 V[j] . W[j] over the panel columns
+    const double dd = wave_sum_d(lane < cc ? (double)vj * (double)wj : 0.0);
+    if (lead && lane == 0) {
+      const float dj = (float)((double)ajj - 2.0 * dd);
+      if (fin) {
+        M.d[j] = dj;
+        M.e[j] = 0.f;
+        M.tau[j] = 0.f;
+      } else {
+        gSC[cs * 4 + 1] = dj;
+      }
+    }
+  }
+  FinWave& F = SW[wave];
+  if (lane < NB) {
+    F.s12[lane] = s1f;
+    F.s12[NB + lane] = s2f;
+    F.vw[0][lane] = vj; F.vw[1][lane] = wj;
+    F.vw[2][lane] = vj1; F.vw[3][lane] = wj1;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   STAMP(3);
 
-  // ---- step 2, rows j and j+1 (waves 0 / 1): needed by every row's x_j / a_j
-  if (wave < 2 && j >= 1 && rw < n) {
-    const float yv = wave_reduce_sum(pw);
-    float corr = (lane < cp) ? vrow * S.s12[lane] + wrow * S.s12[NB + lane] : 0.f;
-    corr = wave_reduce_sum(corr);
-    const float vv = (rw == j) ? 1.f : (float)(s_p * (double)xw);
-    const float ww = (float)(tau_p * ((double)aw + s_p * (double)yv - (double)corr) +
-                             alpha2 * (double)vv);
-    if (lane == cp) {
-      S.vwj[2 * wave][lane] = vv;
-      S.vwj[2 * wave + 1][lane] = ww;
-    }
-    if (lead && rw == j && lane == 0) {
-      M.V[(long long)rw * NB + cp] = vv;
-      M.W[(long long)rw * NB + cp] = ww;
-    }
-  }
-  if (lead && tid == 0 && j >= 1) {
-    M.d[j - 1] = (float)S.scal[4];
-    M.e[j - 1] = (float)beta_p;
-    M.tau[j - 1] = (float)tau_p;
-    M.A[(long long)(j - 1) * lda + j] = (float)beta_p;
-  }
   // ---- step 2, this thread's row (r >= j+1)
   if (j >= 1 && rok && r >= j + 1) {
     float yh = 0.f;
@@ -292,79 +314,56 @@ __global__ __launch_bounds__(256) void sytrd_fin_kernel(const RMat* __restrict__
     float corr = 0.f;
 #pragma unroll
     for (int x = 0; x < NB; ++x)
-      if (x < cp) corr += vr[x] * S.s12[x] + wr[x] * S.s12[NB + x];
+      if (x < cp) corr += vr[x] * F.s12[x] + wr[x] * F.s12[NB + x];
     const float vmy = (float)(s_p * (double)xhp);
     const float wmy =
         (float)(tau_p * ((double)arow + s_p * (double)yh - (double)corr) + alpha2 * (double)vmy);
 #pragma unroll
     for (int x = 0; x < NB; ++x)
       if (x == cp) { vr[x] = vmy; wr[x] = wmy; }
-    M.V[(long long)r * NB + cp] = vmy;
-    M.W[(long long)r * NB + cp] = wmy;
-    M.A[(long long)(j - 1) * lda + r] = vmy;      // reflector j-1: v[2:] (r >= j+1)
+    gV[r * NB + cp] = vmy;
+    gW[r * NB + cp] = wmy;
+    gA[(long long)(j - 1) * lda + r] = vmy;      // reflector j-1: v[2:] (r >= j+1)
   }
-  __syncthreads();      // rows j / j+1 of the panel (S.vwj) are final
+  if (fin) return;      // uniform: d/e/tau of the last two columns are written
   STAMP(4);
 
-  if (fin) {            // d[n-1] = A(n-1, n-1) - 2 V[n-1] . W[n-1]
-    if (lead && tid == 0) {
-      double dd = M.A[(long long)j * lda + j];
-      for (int x = 0; x < cc; ++x) dd -= 2.0 * (double)S.vwj[0][x] * (double)S.vwj[1][x];
-      M.d[j] = (float)dd;
-      M.e[j] = 0.f;
-      M.tau[j] = 0.f;
-    }
-    return;
-  }
-
-  // ---- step 3: x_j (rows >= j+1), a_j; d_j and alpha_j
+  // ---- step 3: x_j (rows >= j+1), a_j; alpha_j
   float xmy = 0.f, amy = 0.f;
   if (rok && r >= j + 1) {
     float corr = 0.f, corr1 = 0.f;
 #pragma unroll
     for (int x = 0; x < NB; ++x) {
       if (x < cc) {
-        corr += vr[x] * S.vwj[1][x] + wr[x] * S.vwj[0][x];
-        corr1 += vr[x] * S.vwj[3][x] + wr[x] * S.vwj[2][x];
+        corr += vr[x] * F.vw[1][x] + wr[x] * F.vw[0][x];
+        corr1 += vr[x] * F.vw[3][x] + wr[x] * F.vw[2][x];
       }
     }
     xmy = arow - corr;
     amy = pstart ? brow - corr1 : brow;    // a_j = row j+1 of the NEW panel's base
   }
   const float xh = (rok && r >= j + 2) ? xmy : 0.f;
-  if (lead && tid == 0) {
-    double dd = M.A[(long long)j * lda + j];
-    for (int x = 0; x < cc; ++x) dd -= 2.0 * (double)S.vwj[0][x] * (double)S.vwj[1][x];
-    M.SC[cs * 4 + 1] = (float)dd;
-  }
-  if (r == j + 1 && r < n) M.SC[cs * 4] = xmy;      // alpha_j
-  if (r < n) M.XH[cs * M.sXH + r] = xh;
-  // ---- partial sums for fin(j+1): transpose through LDS, fixed-order sums
+  if (r == j + 1 && r < n) gSC[cs * 4] = xmy;      // alpha_j
+  if (r < n) gptr(M.XH)[cs * M.sXH + r] = xh;
+  // ---- partial sums for fin(j+1): wave butterfly, then 4 waves in order
   {
-    const int cn = pstart ? 0 : c;                // the current panel's columns
-    tw[0 * TWS + tid] = xh * xh;
-    tw[1 * TWS + tid] = xh * amy;
+    const int cn = pstart ? 0 : c;                // the current panel's columns (< NB)
+    float pv[64];
+    pv[0] = xh * xh;
+    pv[1] = xh * amy;
 #pragma unroll
-    for (int x = 0; x < NB; ++x) {
-      tw[(2 + x) * TWS + tid] = (x < cn) ? wr[x] * xh : 0.f;
-      tw[(2 + NB + x) * TWS + tid] = (x < cn) ? vr[x] * xh : 0.f;
+    for (int x = 0; x < NB - 1; ++x) {
+      pv[K_W + x] = (x < cn) ? wr[x] * xh : 0.f;
+      pv[K_V + x] = (x < cn) ? vr[x] * xh : 0.f;
     }
+    wred[wave][lane] = butterfly64(pv);
   }
   __syncthreads();
   STAMP(5);
-  if (tid < 3 * RSW) {
-    double acc = 0.0;
-    if (rk < 2 + 2 * NB) {
-      const float* col = tw + rk * TWS;
-#pragma unroll 8
-      for (int t = rg; t < FB; t += 3) acc += (double)col[t];
-    }
-    S.red[tid] = acc;
-  }
-  __syncthreads();
   if (tid < RSW)
-    M.RS[cs * M.sRS + (long long)bf * RSW + tid] =
-        (float)(S.red[tid] + S.red[RSW + tid] + S.red[2 * RSW + tid]);
+    gptr(M.RS)[cs * M.sRS + bf * RSW + tid] =
+        (float)(((double)wred[0][tid] + (double)wred[1][tid]) +
+                ((double)wred[2][tid] + (double)wred[3][tid]));
   STAMP(6);
   if (stamps && tid == 0) stamps[(long long)j * 16 + 9] = __builtin_amdgcn_s_memtime();
 }
@@ -387,13 +386,17 @@ __global__ __launch_bounds__(256) void sytrd_upd_kernel(const RMat* __restrict__
   int I, K;
   tri_index(local, nt - s0, I, K);
   I += s0; K += s0;
-  for (int e = tid; e < TB * NB; e += 256) {
+  const AS1 float* gV = gptr(M.V);
+  const AS1 float* gW = gptr(M.W);
+#pragma unroll
+  for (int e0 = 0; e0 < TB * NB; e0 += 256) {
+    const int e = e0 + tid;
     const int rr = e / NB, x = e - rr * NB;
     const int ri = I * TB + rr, rk = K * TB + rr;
-    const float vi = ri < n ? M.V[(long long)ri * NB + x] : 0.f;
-    const float wi = ri < n ? M.W[(long long)ri * NB + x] : 0.f;
-    const float vk = rk < n ? M.V[(long long)rk * NB + x] : 0.f;
-    const float wk = rk < n ? M.W[(long long)rk * NB + x] : 0.f;
+    const float vi = gld_if(gV, ri * NB + x, ri < n, 0.f);
+    const float wi = gld_if(gW, ri * NB + x, ri < n, 0.f);
+    const float vk = gld_if(gV, rk * NB + x, rk < n, 0.f);
+    const float wk = gld_if(gW, rk * NB + x, rk < n, 0.f);
     sL[rr][x] = vi; sL[rr][NB + x] = wi;
     sR[rr][x] = wk; sR[rr][NB + x] = vk;
   }
@@ -421,21 +424,29 @@ __global__ __launch_bounds__(256) void sytrd_upd_kernel(const RMat* __restrict__
       for (int b = 0; b < 2; ++b)
         acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[b], acc[a][b], 0, 0, 0);
   }
-  // C/D map of 32x32: row = (x&3) + 8 (x>>2) + 4 lh, col = lane & 31
-  float* A = M.A;
+  // C/D map of 32x32: row = (x&3) + 8 (x>>2) + 4 lh, col = lane & 31.  Per
+  // 32 x 32 block: its 16 old values loaded (clamped, branch-free), then stored
+  AS1 float* const A = gptr(M.A);
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < 2; ++b) {
+      float old[16];
 #pragma unroll
       for (int x = 0; x < 16; ++x) {
         const int gr = I * TB + wr * 64 + a * 32 + (x & 3) + 8 * (x >> 2) + 4 * lh;
         const int gc = K * TB + wc * 64 + b * 32 + l31;
-        if (gr >= q + 1 && gr < n && gc >= gr && gc < n) {
-          float* p = A + (long long)gr * M.lda + gc;
-          *p -= acc[a][b][x];
-        }
+        const bool ok = gr >= q + 1 && gr < n && gc >= gr && gc < n;
+        old[x] = gld_if(A, (long long)gr * M.lda + gc, ok, 0.f);
       }
+#pragma unroll
+      for (int x = 0; x < 16; ++x) {
+        const int gr = I * TB + wr * 64 + a * 32 + (x & 3) + 8 * (x >> 2) + 4 * lh;
+        const int gc = K * TB + wc * 64 + b * 32 + l31;
+        if (gr >= q + 1 && gr < n && gc >= gr && gc < n)
+          A[(long long)gr * M.lda + gc] = old[x] - acc[a][b][x];
+      }
+    }
 }
 
 // ------------------------------------------------------------------- symv
@@ -464,26 +475,22 @@ __global__ __launch_bounds__(256) void sytrd_symv2_kernel(const RMat* __restrict
   {
     const int h = tid >> 7, lr = tid & (TB - 1);
     const int rr = (h ? K : I) * TB + lr;
-    sv[h][lr] = rr < n ? M.XH[cs * M.sXH + rr] : 0.f;
+    sv[h][lr] = gld_if(gptr(M.XH) + cs * M.sXH, rr, rr < n, 0.f);
   }
   const int hw = lane >> 5, cl = lane & 31;
   const int kk0 = cl * 4, k0 = K * TB + kk0;
+  // branch-free tile loads: row clamped to n-1, column start clamped inside
+  // the row (lda % 4 == 0, lda >= n); out-of-range entries zeroed after
+  const int kc = min(k0, (int)lda - 4);
+  const AS1 float* gA = gptr(M.A);
   float4 q[16];
-  const bool full_cols = (k0 + 3 < n);
 #pragma unroll
   for (int it = 0; it < 16; ++it) {
     const int rr = I * TB + wave * 32 + it * 2 + hw;
-    q[it] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (rr < n) {
-      const float* row = M.A + (long long)rr * lda;
-      if (full_cols) {
-        q[it] = *(const float4*)(row + k0);
-      } else {
-        if (k0 < n) q[it].x = row[k0];
-        if (k0 + 1 < n) q[it].y = row[k0 + 1];
-        if (k0 + 2 < n) q[it].z = row[k0 + 2];
-      }
-    }
+    const fx4 t = *(const AS1 fx4*)(gA + (long long)min(rr, n - 1) * lda + kc);
+    const bool ok = rr < n;
+    q[it] = make_float4((ok && k0 < n) ? t.x : 0.f, (ok && k0 + 1 < n) ? t.y : 0.f,
+                        (ok && k0 + 2 < n) ? t.z : 0.f, (ok && k0 + 3 < n) ? t.w : 0.f);
   }
   __syncthreads();
   float ca[4] = {0.f, 0.f, 0.f, 0.f};
@@ -514,7 +521,7 @@ __global__ __launch_bounds__(256) void sytrd_symv2_kernel(const RMat* __restrict
     for (int x = 0; x < 4; ++x) colred[wave][kk0 + x] = ca[x];
   }
   __syncthreads();
-  float* Pc = M.P + cs * M.sP;
+  AS1 float* const Pc = gptr(M.P) + cs * M.sP;
   double tp = 0.0;
   if (tid < TB) {
     float rs = 0.f;
@@ -530,10 +537,10 @@ __global__ __launch_bounds__(256) void sytrd_symv2_kernel(const RMat* __restrict
       tp = (double)sv[0][tid] * (double)rs + (double)sv[1][tid] * (double)csum;
     }
   }
-  tp = wave_reduce_sum_d(tp);
+  tp = wave_sum_d(tp);
   if (lane == 0 && wave < 2) tred[wave] = tp;
   __syncthreads();
-  if (tid == 0) M.TS[cs * M.sTS + (long long)I * nt + K] = (float)(tred[0] + tred[1]);
+  if (tid == 0) gptr(M.TS)[cs * M.sTS + local] = (float)(tred[0] + tred[1]);   // triangle order
 }
 
 // ------------------------------------------------------------------ host
@@ -559,11 +566,10 @@ void counts(int n, int j, int out[3]) {
 
 int enqueue(const RPlan& P, hipStream_t stream) {
   const int nm = (int)P.n_sorted.size();
-  const size_t fin_lds = (size_t)RSW * TWS * sizeof(float);
   const size_t kstride = (size_t)P.nmax * (nm + 1);
   for (int j = 0; j < P.nmax; ++j) {
     const int* of = P.d_offs + (size_t)j * (nm + 1);
-    hipLaunchKernelGGL(sytrd_fin_kernel, dim3(P.grid[0][j]), dim3(256), fin_lds, stream,
+    hipLaunchKernelGGL(sytrd_fin_kernel, dim3(P.grid[0][j]), dim3(256), 0, stream,
                        P.d_mats, of, P.nact[0][j], j);
     if (P.grid[1][j] > 0)
       hipLaunchKernelGGL(sytrd_upd_kernel, dim3(P.grid[1][j]), dim3(256), 0, stream, P.d_mats,
@@ -627,13 +633,6 @@ RPlan* plan_for(const KfacReduceRecord* recs, int count, bool capture, int* err)
   }
   const std::string key((const char*)mats.data(), sizeof(RMat) * mats.size());
   std::lock_guard<std::mutex> lk(g_mu);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)sytrd_fin_kernel,
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                              RSW * TWS * (int)sizeof(float));
-    attr = true;
-  }
   auto it = g_plans.find(key);
   if (it == g_plans.end()) {
     RPlan P;

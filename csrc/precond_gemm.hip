@@ -28,19 +28,30 @@
 // (any memory layout, bias as the last K-FAC column), `split_copy` builds the
 // QA/QG/QAt/QGt planes and Dt after each inverse update.
 #include "pgemm.h"
+
+#include <type_traits>
 #include "devtable.h"
 
 namespace {
 
 
+// record of workgroup `blk`: lane i tests record i's tile_begin (records are
+// sorted, record 0 starts at 0), one round trip instead of a dependent
+// binary search
 __device__ __forceinline__ int find_problem(const PGemm* __restrict__ t, int count, int blk) {
-  int lo = 0, hi = count - 1;
-  while (lo < hi) {
-    int mid = (lo + hi + 1) >> 1;
-    if (t[mid].tile_begin <= blk) lo = mid; else hi = mid - 1;
+  const int lane = threadIdx.x & 63;
+  const AS1 int* tb = (const AS1 int*)(gptr((const char*)t) + offsetof(PGemm, tile_begin));
+  constexpr int STRIDE = sizeof(PGemm) / sizeof(int);
+  int cnt = 0;
+  for (int base = 0; base < count; base += 64) {
+    const int i = base + lane;
+    const int b = gld_if(tb, (long long)i * STRIDE, i < count, 0x7fffffff);
+    cnt += __popcll(__ballot(b <= blk));
   }
-  return lo;
+  return cnt - 1;
 }
+
+typedef unsigned u32x4n __attribute__((ext_vector_type(4)));   // AS1 loads
 
 __device__ __forceinline__ void split_bf16(float x, uint16_t& h, uint16_t& l) {
   h = f32_to_bf16_bits(x);
@@ -75,7 +86,12 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES * (DBUF ? 2 : 1)];
 
   const int pi = find_problem(table, count, blockIdx.x);
-  const PGemm& P = table[pi];
+  const PGemm P = table[pi];                      // uniform: scalar registers
+  const AS1 unsigned char* const Ah = (const AS1 unsigned char*)P.a_hi;
+  const AS1 unsigned char* const Al = (const AS1 unsigned char*)P.a_lo;
+  const AS1 unsigned char* const Bh = (const AS1 unsigned char*)P.b_hi;
+  const AS1 unsigned char* const Bl = (const AS1 unsigned char*)P.b_lo;
+  const long long lda = P.lda, ldb = P.ldb;
   const int local = blockIdx.x - P.tile_begin;
   const int tm = local / P.tiles_n, tn = local - tm * P.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
@@ -100,25 +116,30 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   constexpr int QA = CA / NT, QB = CB / NT;
   static_assert(CA % NT == 0 && CB % NT == 0, "loader split");
   constexpr int ESZ = X3 ? 2 : 4;
-  uint4 ra[QA], rb[QB];
+  // branch-free: rows past the problem read row m0 / n0 (in range) and are
+  // zeroed by a select, so every load of a k-step issues back to back
+  u32x4n ra[QA], rb[QB];
+  const u32x4n z4 = {0u, 0u, 0u, 0u};
   auto load = [&](int k0) {
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
       const int c = tid + NT * q;
       const int plane = c / (BM * CPR), row = (c % (BM * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
       const int gm = m0 + row;
-      const unsigned char* base = (const unsigned char*)(plane ? P.a_lo : P.a_hi);
-      ra[q] = (gm < M) ? *(const uint4*)(base + ((long long)gm * P.lda + k0 + kof) * ESZ)
-                       : make_uint4(0, 0, 0, 0);
+      const bool ok = gm < M;
+      const AS1 unsigned char* base = plane ? Al : Ah;
+      const u32x4n v = *(const AS1 u32x4n*)(base + ((long long)(ok ? gm : m0) * lda + k0 + kof) * ESZ);
+      ra[q] = ok ? v : z4;
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
       const int c = tid + NT * q;
       const int plane = c / (BN * CPR), row = (c % (BN * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
       const int gn = n0 + row;
-      const unsigned char* base = (const unsigned char*)(plane ? P.b_lo : P.b_hi);
-      rb[q] = (gn < N) ? *(const uint4*)(base + ((long long)gn * P.ldb + k0 + kof) * ESZ)
-                       : make_uint4(0, 0, 0, 0);
+      const bool ok = gn < N;
+      const AS1 unsigned char* base = plane ? Bl : Bh;
+      const u32x4n v = *(const AS1 u32x4n*)(base + ((long long)(ok ? gn : n0) * ldb + k0 + kof) * ESZ);
+      rb[q] = ok ? v : z4;
     }
   };
   // LDS image: [A hi | A lo | B hi | B lo] rows of LDB16 bf16 (X3) or [A | B] rows of LDF32 f32
@@ -127,15 +148,15 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
     for (int q = 0; q < QA; ++q) {
       const int c = tid + NT * q;
       const int plane = c / (BM * CPR), row = (c % (BM * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
-      if (X3) *(uint4*)((uint16_t*)img + (plane * BM + row) * LDB16 + kof) = ra[q];
-      else *(uint4*)((float*)img + row * LDF32 + kof) = ra[q];
+      if (X3) *(u32x4n*)((uint16_t*)img + (plane * BM + row) * LDB16 + kof) = ra[q];
+      else *(u32x4n*)((float*)img + row * LDF32 + kof) = ra[q];
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
       const int c = tid + NT * q;
       const int plane = c / (BN * CPR), row = (c % (BN * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
-      if (X3) *(uint4*)((uint16_t*)img + (2 * BM + plane * BN + row) * LDB16 + kof) = rb[q];
-      else *(uint4*)((float*)img + (BM + row) * LDF32 + kof) = rb[q];
+      if (X3) *(u32x4n*)((uint16_t*)img + (2 * BM + plane * BN + row) * LDB16 + kof) = rb[q];
+      else *(u32x4n*)((float*)img + (BM + row) * LDF32 + kof) = rb[q];
     }
   };
 
@@ -213,42 +234,89 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
     __syncthreads();
   }
 
-  // ---- epilogue (C/D map of 32x32 MFMA: row = (r&3) + 8*(r>>2) + 4*lh, col = lr)
+  // ---- epilogue (C/D map of 32x32 MFMA: row = (r&3) + 8*(r>>2) + 4*lh, col = lr).
+  // Per 32x32 block: the 16 auxiliary operands (D, damping vectors, Grad for
+  // the KL dot, old C) are loaded branch-free first, then stored predicated.
+  const int epi = P.epi;
+  AS1 float* const Cf = (AS1 float*)P.c_hi;
+  AS1 uint16_t* const Ch = (AS1 uint16_t*)P.c_hi;
+  AS1 uint16_t* const Cl = (AS1 uint16_t*)P.c_lo;
+  const AS1 float* const Dm = gptr(P.dmat);
+  const AS1 float* const Vm = gptr(P.vm);
+  const AS1 float* const Vn = gptr(P.vn);
+  const AS1 float* const Gf = (const AS1 float*)P.g_hi;
+  const AS1 uint16_t* const Gh = (const AS1 uint16_t*)P.g_hi;
+  const AS1 uint16_t* const Gl = (const AS1 uint16_t*)P.g_lo;
+  const long long ldc = P.ldc, ldd = P.ldd, ldg = P.ldg;
+  const float damping = P.damping;
   float kl_part = 0.f;
+  // one straight-line loop nest per epilogue kind (a run-time kind test per
+  // element would split the loads into basic blocks with a wait each)
+  auto run = [&](auto kind) {
+    constexpr int E = decltype(kind)::value;
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + arow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      for (int j = 0; j < NJ; ++j) {
         const int n = n0 + brow0 + j * 32 + lr;
-        if (m >= M || n >= N) continue;
-        float v = acc[i][j][r];
-        if (P.epi == EPI_HADAMARD) v *= P.dmat[(long long)m * P.ldd + n];
-        else if (P.epi == EPI_HADAMARD_VEC) v /= (P.vn[n] * P.vm[m] + P.damping);
-        const long long o = (long long)m * P.ldc + n;
-        if (P.epi == EPI_FINAL) {
-          ((float*)P.c_hi)[o] = v;
-          const long long go = (long long)n * P.ldg + m;
-          float g;
-          if (X3) g = bf16_bits_to_f32(((const uint16_t*)P.g_hi)[go]) +
-                      bf16_bits_to_f32(((const uint16_t*)P.g_lo)[go]);
-          else g = ((const float*)P.g_hi)[go];
-          kl_part += v * g;
-        } else if (P.epi == EPI_SUB) {
-          ((float*)P.c_hi)[o] -= v;
-        } else if (P.epi == EPI_ATOMIC) {
-          atomicAdd((float*)P.c_hi + o, v);
-        } else if (X3) {
-          uint16_t h, l;
-          split_bf16(v, h, l);
-          ((uint16_t*)P.c_hi)[o] = h;
-          ((uint16_t*)P.c_lo)[o] = l;
-        } else {
-          ((float*)P.c_hi)[o] = v;
+        float aux[16], aux2[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + arow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          const bool ok = m < M && n < N;
+          aux[r] = 0.f;
+          aux2[r] = 0.f;
+          if constexpr (E == EPI_HADAMARD) {
+            aux[r] = gld_if(Dm, (long long)m * ldd + n, ok, 0.f);
+          } else if constexpr (E == EPI_HADAMARD_VEC) {
+            aux[r] = gld_if(Vm, m, ok, 0.f);
+            aux2[r] = gld_if(Vn, n, ok, 0.f);
+          } else if constexpr (E == EPI_FINAL) {
+            const long long go = (long long)n * ldg + m;
+            if constexpr (X3) {
+              aux[r] = bf16_bits_to_f32(gld_if(Gh, go, ok, (uint16_t)0));
+              aux2[r] = bf16_bits_to_f32(gld_if(Gl, go, ok, (uint16_t)0));
+            } else {
+              aux[r] = gld_if(Gf, go, ok, 0.f);
+            }
+          } else if constexpr (E == EPI_SUB) {
+            aux[r] = gld_if((const AS1 float*)Cf, (long long)m * ldc + n, ok, 0.f);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + arow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (m >= M || n >= N) continue;
+          float v = acc[i][j][r];
+          const long long o = (long long)m * ldc + n;
+          if constexpr (E == EPI_HADAMARD) v *= aux[r];
+          if constexpr (E == EPI_HADAMARD_VEC) v /= (aux2[r] * aux[r] + damping);
+          if constexpr (E == EPI_FINAL) {
+            Cf[o] = v;
+            kl_part += v * (aux[r] + aux2[r]);
+          } else if constexpr (E == EPI_SUB) {
+            Cf[o] = aux[r] - v;
+          } else if constexpr (E == EPI_ATOMIC) {
+            atomicAdd((float*)P.c_hi + o, v);
+          } else if constexpr (X3) {
+            uint16_t h, l;
+            split_bf16(v, h, l);
+            Ch[o] = h;
+            Cl[o] = l;
+          } else {
+            Cf[o] = v;
+          }
         }
       }
+  };
+  switch (epi) {
+    case EPI_HADAMARD: run(std::integral_constant<int, EPI_HADAMARD>()); break;
+    case EPI_HADAMARD_VEC: run(std::integral_constant<int, EPI_HADAMARD_VEC>()); break;
+    case EPI_FINAL: run(std::integral_constant<int, EPI_FINAL>()); break;
+    case EPI_SUB: run(std::integral_constant<int, EPI_SUB>()); break;
+    case EPI_ATOMIC: run(std::integral_constant<int, EPI_ATOMIC>()); break;
+    default: run(std::integral_constant<int, EPI_STORE>()); break;
+  }
   if (kl != nullptr) {
     // one f64 partial per workgroup (waves summed in order, LDS is free after
     // the k-loop's last barrier); kfac_kl_finalize adds the slots in a fixed

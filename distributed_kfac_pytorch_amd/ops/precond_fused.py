@@ -45,10 +45,12 @@ BIG_TILES = False  # measured 2.7x slower on ResNet-50 (profiles/r1_pgemm_varian
 TILE_SHAPES = {0: (128, 128), 1: (256, 256), 2: (64, 64), 3: (128, 128), 4: (128, 64),
                5: (128, 128), 6: (256, 128), 7: (128, 256), 8: (128, 128), 9: (128, 128),
                10: (128, 128), 11: (128, 128)}
-# tile configuration of every problem not in the big class, per precision
-# (profiles/r1_pgemm_variants.md: bf16x3 128x128 with 8 waves 1.64 ms vs 1.94
-# ms with 4 waves; fp32 128x128 with 16 waves 2.98 ms vs 3.55 ms)
-TILE_CFG_DEFAULT = {'bf16x3': 3, 'fp32': 5}
+# tile configuration of every problem not in the big class, per precision.
+# Round 2 (branch-free operand loads, record in scalar registers; the k-step
+# loads now really stay in flight under the MFMAs): 128 x 128 with 4 waves is
+# best in both modes, ResNet-50 chain bf16x3 1.55 ms (8 waves 1.99, round 1
+# best 1.61), fp32 2.98 ms (16 waves 3.35); profiles/r2_pgemm_sweep.log
+TILE_CFG_DEFAULT = {'bf16x3': 0, 'fp32': 0}
 # None: per-precision default; KFAC_PGEMM_TILE_CFG=<id> forces one (experiments, tests)
 TILE_CFG = int(os.environ['KFAC_PGEMM_TILE_CFG']) if os.environ.get('KFAC_PGEMM_TILE_CFG') \
     else None
@@ -176,13 +178,8 @@ class FusedPreconditioner(object):
         # superseded device tables stay alive: a captured graph may use them
         self._retired_tables = []
         self.damping = 0.0
+        self.kl_buf = None
         self._build_stage_tables()
-        # KL dot of the last stage: one f64 partial slot per workgroup of its
-        # launches, summed in a fixed order (deterministic: every rank derives
-        # the same clip scale); the result is slot 0
-        self._kl_slots = sum(tiles for _, _, _, tiles in self._stage_tables[3])
-        self.kl_buf = torch.zeros(1 + self._kl_slots, dtype=torch.float64, device=self.device)
-        self.kl = self.kl_buf[0]
 
     # ------------------------------------------------------------- tables
     def _build_stage_tables(self):
@@ -239,6 +236,16 @@ class FusedPreconditioner(object):
                 launches.append((tile, _upload(arr, self.device), len(sel), tiles))
             stages.append(launches)
         self._stage_tables = stages
+        # KL dot of the last stage: one f64 partial slot per workgroup of its
+        # launches (the count depends on the tile shapes), summed in a fixed
+        # order (deterministic: every rank derives the same clip scale); the
+        # result is slot 0.  A grown buffer retires the old one (graphs).
+        self._kl_slots = sum(tiles for _, _, _, tiles in stages[3])
+        if self.kl_buf is None or self.kl_buf.numel() < 1 + self._kl_slots:
+            if self.kl_buf is not None:
+                self._retired_tables.append(self.kl_buf)
+            self.kl_buf = torch.zeros(1 + self._kl_slots, dtype=torch.float64, device=self.device)
+            self.kl = self.kl_buf[0]
 
     def refresh_eigen(self):
         """Re-split QA/QG (+ transposes) and transpose dGdA after an inverse

@@ -31,7 +31,7 @@ def main():
     stamps = torch.zeros(n * 16, dtype=torch.int64, device=dev)
     if os.environ.get('STAMPS'):
         _lib.check(L.kfac_reduce_stamps(_lib.ptr(stamps)), 'stamps')
-    for it in range(3):
+    for it in range(int(os.environ.get('REPS', '3'))):
         torch.cuda.synchronize()
         t = time.perf_counter()
         _lib.check(L.kfac_reduce_batched(rr, b, int(graph), cs), 'reduce')

@@ -1,5 +1,7 @@
 """Hand-written blocked tridiagonalisation (csrc/eig_tridiag.hip) and the large-n
 eigensolver path built on it, against fp64 torch references."""
+import os
+
 import pytest
 import torch
 
@@ -84,10 +86,15 @@ def test_tridiag_degenerate_columns():
         assert torch.allclose(d64, torch.linalg.eigvalsh(A64), atol=1e-5)
 
 
-def test_symeig_many_routes_big_classes_to_tridiag():
-    assert eigen.LARGE_PATH == 'auto'
-    assert eigen._class_solver(eigen.TRIDIAG_MIN_N) is eigen._tridiag_class
-    assert eigen._class_solver(eigen.TRIDIAG_MIN_N - 1) is eigen._syevd_class
+@pytest.mark.parametrize('path', ['fused', 'auto'])
+def test_symeig_many_routes_big_classes_to_tridiag(path, monkeypatch):
+    # default: every large factor through the fused ragged path; 'auto' (opt-in)
+    # routes per size class (hand-written reduction >= TRIDIAG_MIN_N)
+    assert os.environ.get('KFAC_EIG_LARGE') or eigen.LARGE_PATH == 'fused'
+    monkeypatch.setattr(eigen, 'LARGE_PATH', path)
+    if path == 'auto':
+        assert eigen._class_solver(eigen.TRIDIAG_MIN_N) is eigen._tridiag_class
+        assert eigen._class_solver(eigen.TRIDIAG_MIN_N - 1) is eigen._syevd_class
     mats = [_spd(n, 50, n).float() for n in (300, 2048, 300, 2100)]
     outs = eigen.symeig_many(mats, clip=0.0)
     torch.cuda.synchronize()
