@@ -123,7 +123,10 @@ __device__ __forceinline__ float butterfly64(float (&v)[64]) {
 // one (at most NB - 1 of them)
 constexpr int K_W = 2, K_V = 2 + (NB - 1);
 static_assert(K_V + NB - 1 == RSW, "fin partial kinds must fill one wave");
-constexpr int TSQ = (NTMAX * (NTMAX + 1) / 2 + 63) / 64;   // tile-sum loads per lane
+constexpr int TSQ = (NTMAX * (NTMAX + 1) / 2 + 255) / 256;   // float4 tile-sum loads per lane
+constexpr int NFP = (NFMAX + 3) / 4 * 4;                      // RS: blocks per kind (float4 rows)
+// Every wave keeps its loads under the 63 a wave can have in flight
+// (vmcnt is 6 bits): past that, each extra batch costs a full round trip.
 
 struct FinWave {                  // one wave's private slice (no barrier needed)
   float s12[2 * NB];              // s1, s2
@@ -175,22 +178,14 @@ __global__ __launch_bounds__(256) void sytrd_fin_kernel(const RMat* __restrict__
 
   // ---- every load up front, branch-free (one memory round trip)
   const bool j1 = (j >= 1);
-  // fin(j-1) block partials: lane x < cp sums kinds W_x / V_x over the
-  // blocks, lane u < #blocks takes |xh|^2 and xh.a of block f0p + u
-  float rw_[NFMAX], rv_[NFMAX];
+  // fin(j-1) block partials, kind-major [RSW][NFP]: lane = kind, float4s of
+  // 4 blocks (blocks f0p .. nf-1 are valid)
+  fx4 rq[NFP / 4];
 #pragma unroll
-  for (int u = 0; u < NFMAX; ++u) {
-    const int bb = f0p + u;
-    const bool ok = j1 && lane < cp && bb < M.nf;
-    rw_[u] = gld_if(RSp, bb * RSW + K_W + lane, ok, 0.f);
-    rv_[u] = gld_if(RSp, bb * RSW + K_V + lane, ok, 0.f);
-  }
-  const bool okb = j1 && f0p + lane < M.nf;
-  const float rs0 = gld_if(RSp, (f0p + lane) * RSW, okb, 0.f);
-  const float rs1 = gld_if(RSp, (f0p + lane) * RSW + 1, okb, 0.f);
-  float tq[TSQ];                           // symv(j-1) tile sums, triangle order
+  for (int u = 0; u < NFP / 4; ++u) rq[u] = *(const AS1 fx4*)(RSp + lane * NFP + 4 * u);
+  fx4 tq[TSQ];                             // symv(j-1) tile sums, triangle order
 #pragma unroll
-  for (int u = 0; u < TSQ; ++u) tq[u] = gld_if(TSp, lane + 64 * u, j1 && lane + 64 * u < ntri, 0.f);
+  for (int u = 0; u < TSQ; ++u) tq[u] = *(const AS1 fx4*)(TSp + 4 * lane + 256 * u);
   const bool okp = j1 && lane >= s0p && lane < nt;
   const float pj = gld_if(Pp, j * ntp + lane, okp, 0.f);
   const float pj1 = gld_if(Pp, (j + 1) * ntp + lane, okp && has1, 0.f);
@@ -227,19 +222,34 @@ __global__ __launch_bounds__(256) void sytrd_fin_kernel(const RMat* __restrict__
 #pragma unroll
     for (int u = 0; u < PQ4; ++u) pq[u] = gld_if(pp, u, j1 && 4 * u + 3 >= s0p && 4 * u < nt, z4);
   }
-  double pW = 0.0, pV = 0.0, pT = 0.0;
+  double pK = 0.0, pT = 0.0;               // this lane's kind over the blocks; tile sums
 #pragma unroll
-  for (int u = 0; u < NFMAX; ++u) { pW += (double)rw_[u]; pV += (double)rv_[u]; }
+  for (int u = 0; u < NFP / 4; ++u) {
 #pragma unroll
-  for (int u = 0; u < TSQ; ++u) pT += (double)tq[u];
-  const double pS = rs0, pA = rs1;
+    for (int e = 0; e < 4; ++e) {
+      const int bb = 4 * u + e;
+      pK += (j1 && bb >= f0p && bb < M.nf) ? (double)rq[u][e] : 0.0;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < TSQ; ++u) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int f = 4 * lane + 256 * u + e;
+      pT += (j1 && f < ntri) ? (double)tq[u][e] : 0.0;
+    }
+  }
+  // kinds to their consumers: |xh|^2 and xh.a broadcast, W_x / V_x to lane x
+  const double pW = __shfl(pK, (K_W + lane) & 63, 64);
+  const double pV = __shfl(pK, (K_V + lane) & 63, 64);
+  const double sig2_b = __shfl(pK, 0, 64), xa_b = __shfl(pK, 1, 64);
   STAMP(2);
 
   // ---- step 1 (per wave): scalars of column j-1; step 2 for rows j, j+1
   double beta_p = 0.0, tau_p = 0.0, s_p = 0.0, alpha2 = 0.0;
   float s1f = 0.f, s2f = 0.f;
   if (j >= 1) {
-    const double sig2 = wave_sum_d(pS), xa = wave_sum_d(pA), xy = wave_sum_d(pT);
+    const double sig2 = sig2_b, xa = xa_b, xy = wave_sum_d(pT);
     hh_scalars((double)alpha, sig2, beta_p, tau_p, s_p);
     // s1 = W^T v, s2 = V^T v over rows >= j (v[j] = 1): row j of the panel
     double s1 = 0.0, s2 = 0.0;
@@ -361,7 +371,7 @@ __global__ __launch_bounds__(256) void sytrd_fin_kernel(const RMat* __restrict__
   __syncthreads();
   STAMP(5);
   if (tid < RSW)
-    gptr(M.RS)[cs * M.sRS + bf * RSW + tid] =
+    gptr(M.RS)[cs * M.sRS + tid * NFP + bf] =
         (float)(((double)wred[0][tid] + (double)wred[1][tid]) +
                 ((double)wred[2][tid] + (double)wred[3][tid]));
   STAMP(6);
@@ -592,8 +602,8 @@ KFAC_API long long kfac_reduce_ws_floats(int n) {
   auto a16 = [](long long x) { return (x + 15) / 16 * 16; };
   long long s = 2 * a16((long long)n * NB);               // V, W
   s += 2 * a16(nt * TB * ((nt + 3) / 4 * 4));             // P (row-major partials)
-  s += 2 * a16(nt * nt);                                  // TS
-  s += 2 * a16(nf * RSW);                                 // RS
+  s += 2 * std::max<long long>(a16(nt * nt), 256LL * TSQ);   // TS
+  s += 2 * a16((long long)RSW * NFP);                     // RS (kind-major)
   s += 2 * a16(n);                                        // XH
   s += a16(8);                                            // SC
   return (s + 63) / 64 * 64;
@@ -625,8 +635,9 @@ RPlan* plan_for(const KfacReduceRecord* recs, int count, bool capture, int* err)
     auto take = [&](long long fl) { float* o = p; p += (fl + 15) / 16 * 16; return o; };
     M.V = take(n * NB); M.W = take(n * NB);
     M.sP = (nt * TB * ((nt + 3) / 4 * 4) + 15) / 16 * 16; M.P = take(2 * M.sP);
-    M.sTS = (nt * nt + 15) / 16 * 16; M.TS = take(2 * M.sTS);
-    M.sRS = (M.nf * RSW + 15) / 16 * 16; M.RS = take(2 * M.sRS);
+    M.sTS = std::max<long long>((nt * nt + 15) / 16 * 16, 256LL * TSQ);   // float4 reads
+    M.TS = take(2 * M.sTS);
+    M.sRS = RSW * NFP; M.RS = take(2 * M.sRS);
     M.sXH = (n + 15) / 16 * 16; M.XH = take(2 * M.sXH);
     M.SC = take(8);
     mats.push_back(M);
