@@ -1,11 +1,15 @@
 """Symmetric eigendecomposition / damped inverse of Kronecker factors (K6, K9).
 
-GPU path (MI355X):
+GPU path (MI355X), LARGE_PATH = 'fused' (default): every factor of the step
+(any size up to FUSED_MAX_N) in ONE ragged launch sequence per stage: the
+fused tridiagonal reduction (csrc/eig_reduce.hip), the batched divide and
+conquer (csrc/eig_dc.hip), the compact-WY back-transformation.
+Per-class paths (opt-in, round 1):
   * n <= 192: every such factor of the step is solved by ONE launch of the
     batched LDS Jacobi kernel (csrc/eig_jacobi.hip), one workgroup per matrix.
   * larger n: grouped by size class; classes run concurrently on a pool of
-    side streams.  LARGE_PATH selects the solver of a class ('auto', the
-    default: 'tridiag' for n >= TRIDIAG_MIN_N, else 'syevd'):
+    side streams.  LARGE_PATH selects the solver of a class ('auto':
+    'tridiag' for n >= TRIDIAG_MIN_N, else 'syevd'):
       'tridiag'  the hand-written blocked Householder reduction
                  (csrc/eig_tridiag.hip: 3 launches per column for the whole
                  class, captured into one hipGraph) + rocSOLVER's tridiagonal
@@ -461,8 +465,16 @@ def symeig_many(mats, clip=0.0, solver='auto'):
                 d = torch.clamp(d, min=clip)
             outs.append((Q, d))
         return outs
+    # fused default: EVERY factor rides the ragged launch sequence (a small
+    # factor's reduction columns run alongside the big ones', its divide and
+    # conquer is one or two levels); the batched LDS Jacobi is the small-n
+    # solver of the per-class paths (its latency is the slowest matrix's:
+    # ~40 ms for ResNet-50's 64..192 factors, profiles/r2_eig_kernel_stats.txt)
+    fused_all = (LARGE_PATH == 'fused' and solver == 'auto'
+                 and max(A.shape[0] for A in mats) <= FUSED_MAX_N)
     small = [i for i, A in enumerate(mats)
-             if A.shape[0] <= SMALL_N and solver in ('auto', 'jacobi', 'serial')]
+             if (A.shape[0] < 2 if fused_all else A.shape[0] <= SMALL_N)
+             and solver in ('auto', 'jacobi', 'serial')]
     large = [i for i in range(len(mats)) if i not in set(small)]
     outs = [None] * len(mats)
     if small:

@@ -1,8 +1,6 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
-export REPS=1
-P="python3 scripts/probes/probe_reduce_one.py 2304 1"
-bash scripts/pmc_run.sh lat_a 90 "SQ_INSTS_VMEM SQ_INST_LEVEL_VMEM SQ_INSTS_SMEM SQ_INST_LEVEL_SMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAVES SQ_INSTS_LDS" -- $P && \
-bash scripts/pmc_run.sh lat_b 90 "SQ_INST_LEVEL_LDS SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" -- $P
+timeout -k 10 300 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_eig_dc.py > gpurun_out/t_dc.log 2>&1 && \
+timeout -k 10 200 python3 -u scripts/probes/probe_eig_resnet50.py default > gpurun_out/eig.log 2>&1
 echo rc=$?

@@ -67,7 +67,7 @@ def _kfac_factor(n, seed):
     g = torch.Generator(device=DEV).manual_seed(seed)
     A = (0.95 ** 20) * torch.eye(n, device=DEV, dtype=torch.float64)
     for _ in range(3):
-        X = torch.randn(n, n // 3, device=DEV, dtype=torch.float64, generator=g)
+        X = torch.randn(n, max(1, n // 3), device=DEV, dtype=torch.float64, generator=g)
         X *= torch.exp(torch.randn(n, 1, device=DEV, dtype=torch.float64, generator=g))
         A += 0.05 * X @ X.t() / X.shape[1]
     return A
@@ -106,6 +106,28 @@ def test_fused_ragged_large_path():
         torch.cuda.synchronize()
         eigen.check_solver_status()
     for n, A64, (Q, d) in zip(sizes, mats64, outs):
+        Q64, d64 = Q.double(), d.double()
+        ref = torch.linalg.eigvalsh(A64)
+        an = ref.abs().max().item()
+        res = ((A64 @ Q64 - Q64 * d64).norm() / (an * n ** 0.5)).item()
+        orth = (Q64.t() @ Q64 - torch.eye(n, device=DEV, dtype=torch.float64)).abs().max().item()
+        lam = ((d64 - ref.clamp(min=0)).abs().max() / an).item()
+        assert res <= 2e-5 and orth <= 1e-4 and lam <= 1e-5, (n, res, orth, lam)
+
+
+def test_fused_path_small_and_odd_sizes():
+    """The fused default takes every factor size (no Jacobi split): tiny,
+    single-leaf, one-tile and odd sizes next to a large one, in one call."""
+    assert eigen.LARGE_PATH == 'fused'
+    sizes = [2, 3, 17, 64, 65, 127, 128, 147, 192, 300, 1025]
+    mats64 = [_kfac_factor(n, 70 + i) for i, n in enumerate(sizes)]
+    mats = [m.float() for m in mats64]
+    for _ in range(2):     # plan build + graph replay
+        outs = eigen.symeig_many(mats)
+        torch.cuda.synchronize()
+        eigen.check_solver_status()
+    for n, A64, (Q, d) in zip(sizes, mats64, outs):
+        assert Q.shape == (n, n) and d.shape == (n,)
         Q64, d64 = Q.double(), d.double()
         ref = torch.linalg.eigvalsh(A64)
         an = ref.abs().max().item()
