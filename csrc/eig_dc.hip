@@ -54,7 +54,7 @@ constexpr double EPS32 = 5.9604644775390625e-08;   // 2^-24 (LAPACK slamch 'E')
 constexpr double EPS64 = 1.1102230246251565e-16;   // 2^-53
 constexpr int MAX_IT = 64;
 constexpr int RPB = 4;            // secular: roots (waves) per block
-constexpr int TILE_F32 = 5;       // pgemm 128 x 128, 16 waves
+constexpr int TILE_F32 = 0;       // pgemm 128 x 128, 4 waves (profiles/r2_pgemm_sweep.log)
 constexpr int TYP_SHIFT = 28;
 constexpr int SRC_MASK = (1 << TYP_SHIFT) - 1;
 

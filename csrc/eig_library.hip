@@ -122,7 +122,7 @@ namespace {
 
 constexpr int BT = 128;       // reflectors per block
 constexpr int KCH = 512;      // split-K chunk of S1
-constexpr int TILE_F32 = 5;   // pgemm 128 x 128 fp32 tile configuration
+constexpr int TILE_F32 = 0;   // pgemm 128 x 128 fp32, 4 waves (best since round 2: profiles/r2_pgemm_sweep.log)
 
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
