@@ -10,7 +10,10 @@
 //                (32x32x16 bf16/f16, or 32x32x2 f32 for fp32 data).  Only
 //                upper-triangular 128x128 output tiles are computed (SYRK);
 //                the row dimension (up to 4e5 rows) is split over
-//                blockIdx.y and combined with f32 atomics into a workspace.
+//                blockIdx.y; every (split, tile) stores its partial tile and
+//                tile_reduce adds the partials in a fixed order (source,
+//                split) into the workspace: bitwise-reproducible factors
+//                (the f32-atomic form remains for part == nullptr).
 //   factor_ema   K5: state = alpha*state + (1-alpha)*sym(ws), mirrored from
 //                the upper triangle, in the factor's storage dtype.
 //   triu pack/unpack K12: symmetric factors <-> packed upper triangles for
@@ -40,6 +43,7 @@ struct PatchArgs {
   float scale;
   float* ws;              // f32 workspace, row-major, leading dim ldw
   int ldw;
+  float* part;            // nullptr: f32 atomics into ws; else [split][tile][BT*BT] partials
 };
 
 constexpr int BT = 128;   // output tile
@@ -97,6 +101,83 @@ __device__ __forceinline__ void decompose_row(const PatchArgs& p, long long row,
   hb = oh * p.sth - p.ph;
   wb = ow * p.stw - p.pw;
   base = b * p.sb + (long long)hb * p.sh + (long long)wb * p.sw;
+}
+
+// Epilogue of a (tile, split) work item: the scaled 128x128 partial tile
+// stored whole into its slot of p.part (plain stores: tile_reduce adds the
+// splits in a fixed order), or, with no partial buffer, f32 atomics into the
+// upper triangle of ws.
+__device__ __forceinline__ void store_tile(const PatchArgs& p, const f32x16_t (&acc)[2][2],
+                                           int tile, int split, int ti, int tj, bool diag, int wr,
+                                           int wc, int lr, int lh) {
+  if (p.part != nullptr) {
+    const int tp = p.ntiles * (p.ntiles + 1) / 2;
+    float* dst = p.part + ((long long)split * tp + tile) * (BT * BT);
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int lrow = wr * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          const int lcol = wc * 64 + n * 32 + lr;
+          dst[lrow * BT + lcol] = p.scale * acc[m][n][r];
+        }
+    return;
+  }
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int row = ti * BT + wr * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        int col = tj * BT + wc * 64 + n * 32 + lr;
+        if (row < p.ncols && col < p.ncols && (!diag || row <= col))
+          atomicAdd(p.ws + (long long)row * p.ldw + col, p.scale * acc[m][n][r]);
+      }
+}
+
+// ws[row][col] (upper triangle, row <= col < ncols) = sum over the job's
+// contributions c (in order) and their splits s (in order) of
+// part_c[s][tile][local]: one workgroup per (job, tile pair).
+constexpr int MAX_CONTRIB = 8;
+struct RedJob {
+  float* ws; int ldw, ncols, ntiles, ncontrib;
+  const float* part[MAX_CONTRIB];
+  int splits[MAX_CONTRIB];
+  int block_begin, pad;
+};
+constexpr int MAX_RED_JOBS = 24;
+struct RedBatch {
+  int count, pad[3];
+  RedJob job[MAX_RED_JOBS];
+};
+static_assert(sizeof(RedBatch) <= 4096, "kernel arguments are limited to 4 KB");
+
+__global__ __launch_bounds__(256) void tile_reduce_kernel(const RedBatch* __restrict__ batch) {
+  const RedJob* t = batch->job;
+  int lo = 0, hi = batch->count - 1;
+  const int b = blockIdx.x;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (t[mid].block_begin <= b) lo = mid; else hi = mid - 1;
+  }
+  const RedJob& J = t[lo];
+  const int tile = b - J.block_begin;
+  int tt = tile, ti = 0, rem = J.ntiles;
+  while (tt >= rem) { tt -= rem; ++ti; --rem; }
+  const int tj = ti + tt;
+  const int tp = J.ntiles * (J.ntiles + 1) / 2;
+  for (int e = threadIdx.x; e < BT * BT; e += 256) {
+    const int row = ti * BT + e / BT, col = tj * BT + (e & (BT - 1));
+    float acc = 0.f;
+    for (int c = 0; c < J.ncontrib; ++c) {
+      const float* pc = J.part[c] + (long long)tile * (BT * BT) + e;
+      for (int sp = 0; sp < J.splits[c]; ++sp) acc += pc[(long long)sp * tp * (BT * BT)];
+    }
+    if (row <= col && col < J.ncols) J.ws[(long long)row * J.ldw + col] = acc;
+  }
 }
 
 // LANE_COLS = true when channels are the unit-stride dim (NHWC / Linear):
@@ -253,18 +334,7 @@ __global__ __launch_bounds__(256) void syrk_patch_kernel(PatchArgs p) {
     __syncthreads();
   }
 
-  // ---- epilogue: scaled f32 atomics into the upper triangle of ws
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        int row = ti * BT + wr * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        int col = tj * BT + wc * 64 + n * 32 + lr;
-        if (row < p.ncols && col < p.ncols && (!diag || row <= col))
-          atomicAdd(p.ws + (long long)row * p.ldw + col, p.scale * acc[m][n][r]);
-      }
+  store_tile(p, acc, blockIdx.x, blockIdx.y, ti, tj, diag, wr, wc, lr, lh);
 }
 
 // ---------------------------------------------------------------------------
@@ -415,17 +485,7 @@ __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int 
     __syncthreads();
   }
 
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        int row = ti * BT + wr * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        int col = tj * BT + wc * 64 + n * 32 + lr;
-        if (row < p.ncols && col < p.ncols && (!diag || row <= col))
-          atomicAdd(p.ws + (long long)row * p.ldw + col, p.scale * acc[m][n][r]);
-      }
+  store_tile(p, acc, tile, split, ti, tj, diag, wr, wc, lr, lh);
 }
 
 template <int DT>
@@ -613,8 +673,9 @@ __global__ __launch_bounds__(256) void triu_unpack_kernel(
 KFAC_API int kfac_syrk_patch(int dtype, const void* x, long long sb, long long sc, long long sh,
                              long long sw, int B, int C, int H, int W, int kh, int kw, int sth,
                              int stw, int ph, int pw, int dh, int dw, int has_bias, float scale,
-                             float* ws, int ldw, int max_blocks, hipStream_t stream) {
+                             float* ws, int ldw, int max_blocks, float* part, hipStream_t stream) {
   PatchArgs p;
+  p.part = part;
   p.x = x; p.sb = sb; p.sc = sc; p.sh = sh; p.sw = sw;
   p.B = B; p.C = C; p.H = H; p.W = W;
   p.kh = kh; p.kw = kw; p.sth = sth; p.stw = stw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
@@ -658,12 +719,13 @@ KFAC_API int kfac_syrk_patch(int dtype, const void* x, long long sb, long long s
 KFAC_API int kfac_syrk_vec(int dtype, const void* x, long long sb, long long sc, long long sh,
                            long long sw, int B, int C, int H, int W, int kh, int kw, int sth,
                            int stw, int ph, int pw, int dh, int dw, int has_bias, float scale,
-                           float* ws, int ldw, int max_blocks, hipStream_t stream) {
+                           float* ws, int ldw, int max_blocks, float* part, hipStream_t stream) {
   if (!(dtype == KDT_BF16 || dtype == KDT_F16)) return 0;
   if (sc != 1 || (C % 8) || (sb % 8) || (H > 1 && (sh % 8)) || (W > 1 && (sw % 8)) ||
       (((uintptr_t)x) & 15))
     return 0;
   PatchArgs p;
+  p.part = part;
   p.x = x; p.sb = sb; p.sc = sc; p.sh = sh; p.sw = sw;
   p.B = B; p.C = C; p.H = H; p.W = W;
   p.kh = kh; p.kw = kw; p.sth = sth; p.stw = stw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
@@ -773,6 +835,7 @@ KFAC_API int kfac_syrk_problem_init(SyrkProblem* P, int block_begin, int dtype, 
       (((uintptr_t)x) & 15))
     return 0;
   PatchArgs& p = P->p;
+  p.part = nullptr;      // kfac_syrk_problem_set_part
   p.x = x; p.sb = sb; p.sc = sc; p.sh = sh; p.sw = sw;
   p.B = B; p.C = C; p.H = H; p.W = W;
   p.kh = kh; p.kw = kw; p.sth = sth; p.stw = stw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
@@ -845,6 +908,53 @@ KFAC_API int kfac_ema_grouped(const void* host_table, int count, hipStream_t str
     if (!d) return terr;
     hipLaunchKernelGGL(factor_ema_grouped_kernel, dim3(rows), dim3(256), 0, stream, d);
     int err = (int)hipGetLastError();
+    if (err) return err;
+  }
+  return 0;
+}
+
+// Row splits kfac_syrk_patch (vec = 0) / kfac_syrk_vec (vec = 1) use for M
+// patch rows and ncols columns: a partial buffer holds splits x tile pairs x
+// 128 x 128 floats.
+KFAC_API long long kfac_syrk_splits(int vec, long long M, int ncols, int max_blocks) {
+  const long long bk = vec ? VBK : BK;
+  const int nt = (ncols + BT - 1) / BT, tiles = nt * (nt + 1) / 2;
+  if (M <= 0) return 0;
+  if (max_blocks <= 0) max_blocks = 2048;
+  long long ksteps = (M + bk - 1) / bk;
+  long long splits = (max_blocks + tiles - 1) / tiles;
+  if (splits < 1) splits = 1;
+  if (splits > ksteps) splits = ksteps;
+  const long long rps = (ksteps + splits - 1) / splits * bk;
+  return (M + rps - 1) / rps;
+}
+
+KFAC_API void kfac_syrk_problem_set_part(SyrkProblem* P, float* part) { P->p.part = part; }
+
+KFAC_API int kfac_red_job_size() { return (int)sizeof(RedJob); }
+KFAC_API int kfac_red_max_contrib() { return MAX_CONTRIB; }
+
+// host_jobs: `count` RedJob records (block_begin filled in here): one launch
+// per MAX_RED_JOBS jobs.
+KFAC_API int kfac_tile_reduce(const void* host_jobs, int count, hipStream_t stream) {
+  const RedJob* t = (const RedJob*)host_jobs;
+  for (int base = 0; base < count; base += MAX_RED_JOBS) {
+    RedBatch b;
+    memset(&b, 0, sizeof(b));   // deterministic table bytes (devtable key)
+    b.count = count - base < MAX_RED_JOBS ? count - base : MAX_RED_JOBS;
+    int blocks = 0;
+    for (int k = 0; k < b.count; ++k) {
+      b.job[k] = t[base + k];
+      if (b.job[k].ncontrib > MAX_CONTRIB) return -2;
+      b.job[k].block_begin = blocks;
+      blocks += b.job[k].ntiles * (b.job[k].ntiles + 1) / 2;
+    }
+    if (blocks == 0) continue;
+    int terr = 0;
+    const RedBatch* d = (const RedBatch*)kfac_devtable::get(&b, sizeof(b), stream, &terr);
+    if (!d) return terr;
+    hipLaunchKernelGGL(tile_reduce_kernel, dim3(blocks), dim3(256), 0, stream, d);
+    const int err = (int)hipGetLastError();
     if (err) return err;
   }
   return 0;

@@ -54,11 +54,16 @@ class DcRecord(ctypes.Structure):
 _SIGS = {
     'kfac_syrk_patch': [c_int, c_vp, c_ll, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_int, c_int,
                         c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_vp, c_int,
-                        c_int, c_vp],
+                        c_int, c_vp, c_vp],
     'kfac_factor_ema': [c_int, c_vp, c_vp, c_int, c_int, c_f, c_int, c_vp],
     'kfac_syrk_vec': [c_int, c_vp, c_ll, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_int, c_int,
                       c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_vp, c_int,
-                      c_int, c_vp],
+                      c_int, c_vp, c_vp],
+    'kfac_syrk_splits': [c_int, c_ll, c_int, c_int],
+    'kfac_syrk_problem_set_part': [c_vp, c_vp],
+    'kfac_red_job_size': [],
+    'kfac_red_max_contrib': [],
+    'kfac_tile_reduce': [c_vp, c_int, c_vp],
     'kfac_syrk_problem_size': [],
     'kfac_ema_job_size': [],
     'kfac_syrk_problem_init': [c_vp, c_int, c_int, c_vp, c_ll, c_ll, c_ll, c_ll, c_int, c_int,
@@ -112,7 +117,8 @@ _SIGS = {
 
 
 _RESTYPES = {'kfac_sytrd_ws_floats': c_ll, 'kfac_sytrd_forget': None, 'kfac_dc_ws_bytes': c_ll,
-             'kfac_reduce_ws_floats': c_ll}
+             'kfac_reduce_ws_floats': c_ll, 'kfac_syrk_splits': c_ll,
+             'kfac_syrk_problem_set_part': None}
 
 
 def _load():

@@ -72,18 +72,77 @@ def _vec_eligible(s):
             (W == 1 or sw % 8 == 0) and x.data_ptr() % 16 == 0)
 
 
-def accumulate_sources(sources, ws, allow_vec=True):
-    """ws (n x n f32, zeroed) += sum_s scale_s * P_s^T P_s  (upper triangle only).
+TILE = 128    # csrc/factors.hip output tile
 
+
+def _tile_pairs(n):
+    t = (n + TILE - 1) // TILE
+    return t * (t + 1) // 2
+
+
+class RedJob(ctypes.Structure):
+    """Mirror of csrc/factors.hip RedJob (size checked on first use)."""
+    _fields_ = [('ws', ctypes.c_void_p), ('ldw', ctypes.c_int), ('ncols', ctypes.c_int),
+                ('ntiles', ctypes.c_int), ('ncontrib', ctypes.c_int),
+                ('part', ctypes.c_void_p * 8), ('splits', ctypes.c_int * 8),
+                ('block_begin', ctypes.c_int), ('pad', ctypes.c_int)]
+
+
+def _red_job(ws_ptr, ldw, n, contribs):
+    """contribs: [(part pointer, splits)] in the fixed summation order."""
+    J = RedJob()
+    J.ws, J.ldw, J.ncols, J.ntiles = ws_ptr, ldw, n, (n + TILE - 1) // TILE
+    J.ncontrib = len(contribs)
+    for c, (ptr, sp) in enumerate(contribs):
+        J.part[c] = ptr
+        J.splits[c] = sp
+    return J
+
+
+def _check_red_layout():
+    L = _lib.lib()
+    if L.kfac_red_job_size() != ctypes.sizeof(RedJob) or L.kfac_red_max_contrib() != 8:
+        raise RuntimeError('RedJob layout mismatch with the native library')
+
+
+def accumulate_sources(sources, ws, allow_vec=True):
+    """ws (n x n f32) = sum_s scale_s * P_s^T P_s  (upper triangle only).
+
+    Deterministic: every (source, row split, tile pair) of the SYRK stores its
+    partial tile and ONE tile_reduce launch adds them in a fixed order
+    (source, split) -- bitwise-reproducible factors, no f32 atomics (the
+    atomic form, into a zeroed ws, is the fallback past MAX_CONTRIB sources).
     Returns None when ws is in the reference column order (c, kh, kw), or
     (kcols, C, kh*kw) when the channels-contiguous fast path filled it in the
     internal order (kh, kw, c) -- `kfac_factor_ema_perm` maps it back."""
     L = _lib.lib()
     stream = _lib.stream(ws.device)
     n = ws.shape[0]
-    if allow_vec and all(_vec_eligible(s) for s in sources):
-        order = None
+    det = len(sources) <= MAX_CONTRIB
+    if det:
+        _check_red_layout()
+    else:
+        ws.zero_()
+    vec = allow_vec and all(_vec_eligible(s) for s in sources)
+    parts, contribs = [], []
+    if det:
+        sizes = []
         for s in sources:
+            sp = int(L.kfac_syrk_splits(int(vec), s.rows[0], n, 0))
+            sizes.append(sp)
+        total = sum(sp * _tile_pairs(n) for sp in sizes) * TILE * TILE
+        arena = _lib.workspace(ws.device, max(total, 1), tag='syrk_parts')
+        off = 0
+        for sp in sizes:
+            ptr = arena.data_ptr() + 4 * off
+            parts.append(_lib.c_vp(ptr))
+            contribs.append((ptr, sp))
+            off += sp * _tile_pairs(n) * TILE * TILE
+    else:
+        parts = [None] * len(sources)
+    if vec:
+        order = None
+        for s, part in zip(sources, parts):
             x = s.x
             B, C, H, W = x.shape
             sb, sc, sh, sw = x.stride()
@@ -92,7 +151,7 @@ def accumulate_sources(sources, ws, allow_vec=True):
                 raise ValueError('factor source has {} columns, workspace {}'.format(s.ncols, n))
             r = L.kfac_syrk_vec(_lib.DTYPE_CODE[x.dtype], _lib.ptr(x), sb, sc, sh, sw, B, C, H, W,
                                 g.kh, g.kw, g.sh, g.sw, g.ph, g.pw, g.dh, g.dw, int(s.has_bias),
-                                s.scale, _lib.ptr(ws), ws.stride(0), 0, stream)
+                                s.scale, _lib.ptr(ws), ws.stride(0), 0, part, stream)
             if r != 1:
                 raise RuntimeError('kfac_syrk_vec failed ({})'.format(r))
             kk = g.kh * g.kw
@@ -100,8 +159,10 @@ def accumulate_sources(sources, ws, allow_vec=True):
             if order is not None and order != o:
                 raise ValueError('factor sources disagree on the patch geometry')
             order = o
+        if det:
+            _tile_reduce([_red_job(ws.data_ptr(), ws.stride(0), n, contribs)], stream)
         return None if order[2] == 1 else order
-    for s in sources:
+    for s, part in zip(sources, parts):
         x = s.x
         if x.dtype not in (torch.float32, torch.bfloat16, torch.float16):
             x = x.float()
@@ -115,8 +176,18 @@ def accumulate_sources(sources, ws, allow_vec=True):
         _lib.check(L.kfac_syrk_patch(
             _lib.DTYPE_CODE[x.dtype], _lib.ptr(x), sb, sc, sh, sw, B, C, H, W,
             g.kh, g.kw, g.sh, g.sw, g.ph, g.pw, g.dh, g.dw, int(s.has_bias), s.scale,
-            _lib.ptr(ws), ws.stride(0), 0, stream), 'kfac_syrk_patch')
+            _lib.ptr(ws), ws.stride(0), 0, part, stream), 'kfac_syrk_patch')
+    if det:
+        _tile_reduce([_red_job(ws.data_ptr(), ws.stride(0), n, contribs)], stream)
     return None
+
+
+MAX_CONTRIB = 8    # csrc/factors.hip: sources per deterministic tile reduction
+
+
+def _tile_reduce(jobs, stream):
+    arr = (RedJob * len(jobs))(*jobs)
+    _lib.check(_lib.lib().kfac_tile_reduce(arr, len(jobs), stream), 'kfac_tile_reduce')
 
 
 def _ema(state, ws, n, alpha, mode, order):
@@ -148,7 +219,6 @@ def update_factor(state, sources, alpha, out_dtype):
     if alpha == 1:
         return state
     ws = _lib.workspace(dev, n * n).view(n, n)
-    ws.zero_()
     order = accumulate_sources(sources, ws)
     _ema(state, ws, n, alpha, 0, order)
     return state
@@ -159,7 +229,6 @@ def compute_cov(sources, out_dtype=torch.float32):
     n = sources[0].ncols
     dev = sources[0].x.device
     ws = _lib.workspace(dev, n * n).view(n, n)
-    ws.zero_()
     order = accumulate_sources(sources, ws)
     out = torch.empty(n, n, dtype=out_dtype, device=dev)
     _ema(out, ws, n, 0.0, 1, order)
@@ -198,6 +267,7 @@ def update_factors_grouped(items, alpha):
     grouped, rest = [], []
     for k, (state, sources, out_dtype) in enumerate(items):
         if alpha != 1 and all(_vec_eligible(s) for s in sources) and \
+                len(sources) <= MAX_CONTRIB and \
                 len({(s.x.dtype, s.x.shape[1], s.geom.kh * s.geom.kw) for s in sources}) == 1:
             grouped.append(k)
         else:
@@ -207,10 +277,11 @@ def update_factors_grouped(items, alpha):
         out[k] = update_factor(state, sources, alpha, out_dtype)
     if not grouped:
         return out
+    _check_red_layout()
     sizes = [items[k][1][0].ncols for k in grouped]
     total = sum(n * n for n in sizes)
+    # no memset: tile_reduce writes every upper-triangle element the EMA reads
     arena = _lib.workspace(dev, total, tag='syrk_grouped')
-    arena.zero_()
     psize = L.kfac_syrk_problem_size()
     by_dtype = {}
     ws_of = {}
@@ -220,9 +291,12 @@ def update_factors_grouped(items, alpha):
         off += n * n
         for s in items[k][1]:
             by_dtype.setdefault(s.x.dtype, []).append((k, s))
+    contribs = {k: [] for k in grouped}
+    launches = []
     for dtype, probs in by_dtype.items():
         raw = ctypes.create_string_buffer(psize * len(probs))
         blocks = 0
+        nbs = []
         for i, (k, s) in enumerate(probs):
             x = s.x
             B, C, H, W = x.shape
@@ -236,9 +310,24 @@ def update_factors_grouped(items, alpha):
                 int(s.has_bias), s.scale, _lib.c_vp(ws_ptr), n, SPLIT_ROWS)
             if nb <= 0:
                 raise RuntimeError('grouped SYRK rejected an eligible source')
+            nbs.append(nb)
             blocks += nb
+        launches.append((dtype, probs, raw, nbs))
+    # partial tiles of every (problem, split, tile pair): one arena, then the
+    # fixed-order tile reduction per factor (sources in order, splits in order)
+    tot_parts = sum(sum(nbs) for _, _, _, nbs in launches) * TILE * TILE
+    parts = _lib.workspace(dev, tot_parts, tag='syrk_parts_grouped')
+    poff = 0
+    for dtype, probs, raw, nbs in launches:
+        for i, ((k, s), nb) in enumerate(zip(probs, nbs)):
+            ptr = parts.data_ptr() + 4 * poff
+            L.kfac_syrk_problem_set_part(ctypes.byref(raw, i * psize), _lib.c_vp(ptr))
+            contribs[k].append((ptr, nb // _tile_pairs(ws_of[k][1])))
+            poff += nb * TILE * TILE
         _lib.check(L.kfac_syrk_grouped(raw, len(probs), _lib.DTYPE_CODE[dtype], stream),
                    'kfac_syrk_grouped')
+    _tile_reduce([_red_job(arena.data_ptr() + 4 * ws_of[k][0], ws_of[k][1], ws_of[k][1],
+                           contribs[k]) for k in grouped], stream)
     jobs = (EmaJob * len(grouped))()
     a1, a2 = alpha / (1.0 - alpha), 1.0 - alpha
     for j, k in enumerate(grouped):

@@ -1,0 +1,72 @@
+"""Deterministic factor covariances (csrc/factors.hip: per-split partial
+tiles reduced in a fixed order, no f32 atomics): the same activations give
+bitwise-equal factors, on the grouped (bf16 channels_last) and per-factor
+(fp32 NCHW) paths, and both match an fp64 reference."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributed_kfac_pytorch_amd.ops import factors
+
+pytestmark = pytest.mark.gpu
+
+
+class _Geom(object):
+    def __init__(self, k, s, p):
+        self.kh = self.kw = k
+        self.sh = self.sw = s
+        self.ph = self.pw = p
+        self.dh = self.dw = 1
+
+
+def _ref_cov(x, k, s, p, has_bias):
+    cols = F.unfold(x.double(), k, padding=p, stride=s)          # (B, C*k*k, L)
+    P = cols.transpose(1, 2).reshape(-1, cols.shape[1])
+    if has_bias:
+        P = torch.cat([P, torch.ones(P.shape[0], 1, dtype=P.dtype, device=P.device)], 1)
+    return P.t() @ P / P.shape[0]
+
+
+@pytest.mark.parametrize('dtype,cl', [(torch.bfloat16, True), (torch.float32, False)])
+def test_factor_update_bitwise_reproducible(dtype, cl):
+    g = torch.Generator(device='cuda').manual_seed(5)
+    x = torch.randn(16, 64, 28, 28, device='cuda', generator=g).to(dtype)
+    if cl:
+        x = x.contiguous(memory_format=torch.channels_last)
+    geom = _Geom(3, 1, 1)
+    n = 64 * 9 + 1
+    src = factors.FactorSource(x, geom, True, 1.0)
+    rows = src.rows[0]
+    src.scale = 1.0 / rows
+    outs = []
+    for _ in range(3):
+        st = torch.zeros(n, n, device='cuda')
+        if cl:
+            st = factors.update_factors_grouped([(st, [src], torch.float32)], 0.0)[0]
+        else:
+            st = factors.update_factor(st, [src], 0.0, torch.float32)
+        outs.append(st.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    ref = _ref_cov(x, 3, 1, 1, True)
+    err = ((outs[0].double() - ref).norm() / ref.norm()).item()
+    assert err < (2e-3 if dtype == torch.bfloat16 else 1e-5), err
+
+
+def test_multi_source_factor_reproducible():
+    """Several sources of one factor (gradient accumulation): the partials of
+    every (source, split) are summed in a fixed order."""
+    g = torch.Generator(device='cuda').manual_seed(6)
+    xs = [torch.randn(8, 32, 14, 14, device='cuda', generator=g).to(torch.bfloat16)
+          .contiguous(memory_format=torch.channels_last) for _ in range(3)]
+    geom = _Geom(3, 1, 1)
+    srcs = [factors.FactorSource(x, geom, False, 1.0 / (8 * 14 * 14 * 3)) for x in xs]
+    n = 32 * 9
+    a = factors.update_factors_grouped([(torch.zeros(n, n, device='cuda'), srcs,
+                                         torch.float32)], 0.0)[0].clone()
+    b = factors.update_factors_grouped([(torch.zeros(n, n, device='cuda'), srcs,
+                                         torch.float32)], 0.0)[0].clone()
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    ref = sum(_ref_cov(x, 3, 1, 1, False) for x in xs) / 3
+    assert ((a.double() - ref).norm() / ref.norm()).item() < 2e-3

@@ -10,7 +10,8 @@ from distributed_kfac_pytorch_amd.models import resnet_cifar
 pytestmark = pytest.mark.gpu
 
 
-def _train(use_graphs, steps=25, precision='fp32', segmented=False, set_to_none=False, lag=0):
+def _train(use_graphs, steps=25, precision='fp32', segmented=False, set_to_none=False, lag=0,
+           amp=True):
     torch.manual_seed(0)
     m = resnet_cifar.resnet20().cuda().to(memory_format=torch.channels_last)
     opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9)
@@ -25,7 +26,7 @@ def _train(use_graphs, steps=25, precision='fp32', segmented=False, set_to_none=
 
     def step_fn():
         opt.zero_grad(set_to_none=set_to_none)
-        with torch.autocast('cuda', dtype=torch.bfloat16):
+        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=amp):
             loss = F.cross_entropy(m(x), y)
         loss.backward()
         pre.step()
@@ -74,6 +75,25 @@ def test_graphed_matches_eager():
     for a, b in zip(le, lg):
         assert abs(a - b) < 2e-2 * max(1.0, abs(a)), (le, lg)
     assert diff < max(5e-3, 20 * noise), (diff, noise, le, lg)
+
+
+def test_graphed_equals_eager_deterministic():
+    """With the deterministic SYRK (partial tiles, fixed-order reduction) and
+    MIOpen's deterministic algorithms in fp32, eager runs are bitwise
+    reproducible and the graphed run matches them to 1e-6 (no noise budget)."""
+    prev = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        le, pe, _ = _train(False, steps=14, amp=False)
+        le2, pe2, _ = _train(False, steps=14, amp=False)
+        lg, pg, sg = _train(True, steps=14, amp=False)
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = prev
+    assert sg.replays > 0
+    assert le == le2 and _pdiff(pe, pe2) == 0.0, (le, le2)
+    for a, b in zip(le, lg):
+        assert abs(a - b) <= 1e-6 * max(1.0, abs(a)), (le, lg)
+    assert _pdiff(pe, pg) <= 1e-6, _pdiff(pe, pg)
 
 
 def test_segmented_graphs_match_eager():
