@@ -129,6 +129,13 @@ class CommBackend(object):
             o.copy_(tensor)
         return None
 
+    def allgather_into(self, output, tensor, group=None, async_op=True):
+        """output = concat of every group rank's `tensor` (group-rank order);
+        `tensor` may be this rank's slice of `output` (in place)."""
+        if tensor.data_ptr() != output.data_ptr() or tensor.numel() != output.numel():
+            output.view(-1)[:tensor.numel()].copy_(tensor.view(-1))
+        return None
+
     def barrier(self):
         return None
 
@@ -208,6 +215,13 @@ class TorchBackend(CommBackend):
             outputs[0].copy_(tensor)
             return None
         work = dist.all_gather(outputs, tensor, async_op=async_op, **kw)
+        return Handle(work) if async_op else None
+
+    def allgather_into(self, output, tensor, group=None, async_op=True):
+        skip, kw, _ = self._resolve(group)
+        if skip:
+            return super().allgather_into(output, tensor)
+        work = dist.all_gather_into_tensor(output, tensor, async_op=async_op, **kw)
         return Handle(work) if async_op else None
 
     def barrier(self):

@@ -8,10 +8,15 @@ FactorAllreduce   X1+X2: the upper triangles of every
                   on the wire and turns 2 x #layers NCCL calls into a handful.
                   Buckets are issued back to back (async) and each bucket is
                   unpacked as soon as its own handle completes.
-broadcast_eigendata  X3/X4: one broadcast per owner region of the plan's
-                  eigen arena within the owner's inverse group.
-broadcast_gradients  X5: one broadcast per inverse block within this rank's
-                  gradient group (MEM_OPT / HYBRID_OPT).
+broadcast_eigendata  X3/X4: ONE in-place all-gather of the plan's eigen arena
+                  (equal per-owner slots) over this rank's inverse group:
+                  every owner's region reaches every member in one RCCL call
+                  with all ranks' xGMI links busy, instead of one broadcast
+                  per owner (round 1) or per layer (reference,
+                  kfac/layers/base.py:129-196).
+broadcast_gradients  X5: ONE in-place all-gather of the grad arena's block
+                  slots over this rank's gradient group (MEM_OPT /
+                  HYBRID_OPT; reference kfac/layers/base.py:160-196).
 All calls are asynchronous collectives whose completion only orders the
 current HIP stream behind RCCL's stream: no host synchronisation.
 """
@@ -123,26 +128,17 @@ class FactorAllreduce(object):
 
 def broadcast_eigendata(plan):
     backend = comm.backend
-    if backend.size() == 1 or plan.eig_arena is None:
+    if backend.size() == 1 or plan.eig_arena is None or len(plan.eig_ranks) <= 1:
         return
-    handles = []
-    for owner in sorted(plan.eig_regions):
-        s, e = plan.eig_regions[owner]
-        if e <= s:
-            continue
-        handles.append(backend.broadcast(plan.eig_arena[s:e], src=owner,
-                                         group=plan.eig_group(owner)))
-    backend.sync(handles)
+    s, e = plan.eig_slot_of(plan.rank)
+    backend.sync(backend.allgather_into(plan.eig_arena, plan.eig_arena[s:e],
+                                        group=plan.eig_group(plan.rank)))
 
 
 def broadcast_gradients(plan):
     backend = comm.backend
     if backend.size() == 1 or plan.grad_group.size <= 1:
         return
-    handles = []
-    for b, (s, e) in enumerate(plan.grad_blocks):
-        if e <= s:
-            continue
-        handles.append(backend.broadcast(plan.grad_arena[s:e], src=plan.grad_block_src(b),
-                                         group=plan.grad_group))
-    backend.sync(handles)
+    s, e = plan.grad_slot_of(plan.rank // plan.gw)
+    backend.sync(backend.allgather_into(plan.grad_arena, plan.grad_arena[s:e],
+                                        group=plan.grad_group))

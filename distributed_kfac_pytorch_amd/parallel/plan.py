@@ -6,15 +6,17 @@ Everything the per-step collectives need is laid out here so that each
 collective is ONE call on ONE contiguous buffer:
 
   grad arena   f32, every layer's (nG x nA) preconditioned gradient, ordered
-               by the inverse group ("block") of the layer's owner.  In
-               MEM_OPT / HYBRID_OPT the gradient broadcast of block b inside
-               gradient group k is a single broadcast of a contiguous range
-               from rank b*gw + k -- no packing.
+               by the inverse group ("block") of the layer's owner, each block
+               in an equal, padded slot.  In MEM_OPT / HYBRID_OPT the gradient
+               distribution inside gradient group k (ranks b*gw + k, b = block)
+               is ONE in-place all-gather of the slots: block b's rank
+               contributes slot b.
   eigen arena  inv_dtype, the QA/QG/dGdA (or dA, dG / A_inv, G_inv) of every
-               layer whose owner sits in this rank's inverse group, ordered
-               by owner.  COMM_OPT / HYBRID_OPT eigendata distribution is one
-               broadcast per owner rank (W roots drive their xGMI links
-               concurrently) instead of 2-3 broadcasts per layer.
+               layer whose owner sits in this rank's inverse group, one equal
+               padded slot per group rank (LPT balances the slots).  COMM_OPT
+               / HYBRID_OPT eigendata distribution is ONE in-place all-gather
+               over the inverse group (every rank's xGMI links busy at once)
+               instead of one broadcast per owner or 2-3 per layer.
 Layer tensors (`layer.pgrad_buffer`, `layer.state['QA']`, ...) become views
 into these arenas.
 """
@@ -70,21 +72,21 @@ class ExecutionPlan(object):
     def _build_grad_arena(self):
         nblocks = self.world // self.gw
         order = sorted(range(len(self.layers)), key=lambda i: (self.a_locs[i] // self.gw, i))
-        total = sum(_numel(self.layers[i].grad_shape) for i in order)
-        self.grad_arena = torch.zeros(max(total, 1), dtype=torch.float32, device=self.device)
-        self.grad_blocks = [[0, 0] for _ in range(nblocks)]
-        off = 0
-        cur_block = None
+        sizes = [0] * nblocks
+        for i in order:
+            sizes[self.a_locs[i] // self.gw] += _numel(self.layers[i].grad_shape)
+        # equal slots (64-element aligned): the distribution is one all-gather
+        self.grad_slot = max(1, (max(sizes) + 63) // 64 * 64)
+        self.grad_arena = torch.zeros(nblocks * self.grad_slot, dtype=torch.float32,
+                                      device=self.device)
+        self.grad_blocks = [[b * self.grad_slot, b * self.grad_slot] for b in range(nblocks)]
         for i in order:
             layer = self.layers[i]
             b = self.a_locs[i] // self.gw
-            if b != cur_block:
-                self.grad_blocks[b][0] = off
-                cur_block = b
+            off = self.grad_blocks[b][1]
             n = _numel(layer.grad_shape)
             layer.pgrad_buffer = self.grad_arena[off:off + n].view(*layer.grad_shape)
-            off += n
-            self.grad_blocks[b][1] = off
+            self.grad_blocks[b][1] = off + n
         self.grad_group_index = self.rank % self.gw
         self.grad_group = self.allocator.get_grad_group(self.rank)
 
@@ -93,19 +95,24 @@ class ExecutionPlan(object):
 
     # ------------------------------------------------------------ eigendata
     def _build_eig_arena(self):
-        my_group = set(self.allocator.get_inv_ranks(self.rank))
+        self.eig_ranks = sorted(self.allocator.get_inv_ranks(self.rank))
+        my_group = set(self.eig_ranks)
         per_owner = {}
         for i, layer in enumerate(self.layers):
             for key, shape, factor in _eig_items(layer, self.use_eigen, self.prediv):
                 owner = self.a_locs[i] if factor == 'A' else self.g_locs[i]
                 if owner in my_group:
                     per_owner.setdefault(owner, []).append((layer, key, shape))
-        total = sum(_numel(s) for items in per_owner.values() for _, _, s in items)
-        self.eig_arena = torch.zeros(max(total, 1), dtype=self.inv_dtype, device=self.device)
-        off = 0
-        for owner in sorted(per_owner):
-            start = off
-            for layer, key, shape in per_owner[owner]:
+        sizes = [sum(_numel(s) for _, _, s in per_owner.get(o, [])) for o in self.eig_ranks]
+        # one equal, 64-element aligned slot per group rank (group-rank order =
+        # sorted global ranks): the distribution is one in-place all-gather
+        self.eig_slot = max(1, (max(sizes) + 63) // 64 * 64)
+        self.eig_arena = torch.zeros(len(self.eig_ranks) * self.eig_slot, dtype=self.inv_dtype,
+                                     device=self.device)
+        for gi, owner in enumerate(self.eig_ranks):
+            off = start = gi * self.eig_slot
+            self.eig_regions[owner] = (start, start)
+            for layer, key, shape in per_owner.get(owner, []):
                 n = _numel(shape)
                 view = self.eig_arena[off:off + n].view(*shape)
                 old = layer.state.get(key)
@@ -114,6 +121,14 @@ class ExecutionPlan(object):
                 layer.state[key] = view
                 off += n
             self.eig_regions[owner] = (start, off)
+
+    def eig_slot_of(self, rank):
+        """(start, end) of `rank`'s slot in the eigen arena."""
+        gi = self.eig_ranks.index(rank)
+        return gi * self.eig_slot, (gi + 1) * self.eig_slot
+
+    def grad_slot_of(self, block):
+        return block * self.grad_slot, (block + 1) * self.grad_slot
 
     def eig_group(self, owner):
         return self.allocator.get_inv_group(owner)

@@ -28,6 +28,31 @@ def _init(rank, world, port):
     comm.init_comm_backend()
 
 
+def _count_collectives(pre):
+    """Record how many backend collectives each eigendata / gradient
+    distribution issues: {'eig': [n per inverse step], 'grad': [n per step]}."""
+    from distributed_kfac_pytorch_amd import comm
+    backend = comm.backend
+    count = [0]
+    for name in ('broadcast', 'allgather_into', 'allreduce', 'allgather', 'reduce'):
+        fn = getattr(backend, name)
+
+        def wrapped(*a, _fn=fn, **k):
+            count[0] += 1
+            return _fn(*a, **k)
+        setattr(backend, name, wrapped)
+    calls = {'eig': [], 'grad': []}
+    for attr, key in (('broadcast_inverses', 'eig'), ('broadcast_gradients', 'grad')):
+        orig = getattr(pre, attr)
+
+        def wrapped(_orig=orig, _key=key):
+            c0 = count[0]
+            _orig()
+            calls[_key].append(count[0] - c0)
+        setattr(pre, attr, wrapped)
+    return calls
+
+
 def kfac_strategy(rank, world, port, out_dir, cfg):
     """Identical data on every rank: the K-FAC result must equal world=1."""
     _init(rank, world, port)
@@ -42,8 +67,9 @@ def kfac_strategy(rank, world, port, out_dir, cfg):
                     precompute_outer_eigen=cfg.get('prediv', True),
                     use_eigen_decomp=cfg.get('eigen', True),
                     inverse_lag=cfg.get('lag', 0))
+    calls = _count_collectives(pre)
     grads, factors = run_steps(model, pre, data, cfg['steps'])
-    torch.save({'grads': grads, 'factors': factors},
+    torch.save({'grads': grads, 'factors': factors, 'calls': calls},
                os.path.join(out_dir, 'rank{}.pt'.format(rank)))
     dist.barrier()
     dist.destroy_process_group()

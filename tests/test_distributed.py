@@ -97,6 +97,19 @@ def test_strategy_equivalence(tmp_path, world, cfg):
         else:
             for gs, g0 in zip(res['grads'], res0['grads']):
                 assert all(torch.equal(a, b) for a, b in zip(gs, g0)), r
+        # one collective per distribution (round 2): the eigendata of every
+        # owner in ONE all-gather per inverse step, the MEM/HYBRID gradients
+        # in ONE all-gather per step
+        calls = res['calls']
+        gw = max(1, int(round(world * {'COMM_OPT': 1.0, 'MEM_OPT': 0.0}.get(
+            cfg['method'], cfg.get('fraction', 0.25)))))
+        if cfg['method'] != 'MEM_OPT':
+            # inverse groups of gw ranks: one all-gather when gw > 1
+            assert calls['eig'] and all(c == (1 if gw > 1 else 0) for c in calls['eig']), calls
+        if cfg['method'] != 'COMM_OPT':
+            # gradient groups of world / gw ranks
+            assert calls['grad'] and all(c == (1 if gw < world else 0)
+                                         for c in calls['grad']), calls
 
 
 def test_distribute_layer_factors_without_prediv(tmp_path):
