@@ -36,6 +36,7 @@ from distributed_kfac_pytorch_amd.models import resnet  # noqa: E402
 from distributed_kfac_pytorch_amd.parallel import launch  # noqa: E402
 from distributed_kfac_pytorch_amd import graphs  # noqa: E402
 from distributed_kfac_pytorch_amd.parallel import grad_sync as grad_sync_mod  # noqa: E402
+from distributed_kfac_pytorch_amd.parallel import overlap  # noqa: E402
 
 METRIC = 'images/sec (whole node) ResNet-50 K-FAC+SGD'
 
@@ -78,6 +79,10 @@ def parse():
     ap.add_argument('--inverse-lag', type=int, default=0,
                     help='KFAC(inverse_lag=L): eigendecompositions of an inverse step run on a '
                          'side stream and take effect L steps later (0 = reference schedule)')
+    ap.add_argument('--overlap-grad-comm', type=int, default=1,
+                    help='world > 1 with graphs: backward in two graph segments, the top '
+                         "half's gradient all-reduce overlapped with the bottom half's backward "
+                         '(parallel/overlap.py)')
     ap.add_argument('--ddp', action='store_true',
                     help='eager torch DDP instead of the graphed flat-arena all-reduce')
     return ap.parse_args()
@@ -102,7 +107,8 @@ def step_kind(pre):
     return 'plain'
 
 
-def time_sgd_only(args, model, opt, pre, forward_backward, grad_sync, use_graphs, device):
+def time_sgd_only(args, model, opt, pre, forward_backward, grad_sync, use_graphs, device,
+                  communicate=None):
     """The same training step without K-FAC (hooks removed, plain SGD update),
     timed over the same number of steps: the baseline for kfac_step_ms."""
     pre.remove_hooks()
@@ -113,7 +119,7 @@ def time_sgd_only(args, model, opt, pre, forward_backward, grad_sync, use_graphs
     if grad_sync is not None:
         step = graphs.GraphedTrainStep(None, None, [opt], enabled=use_graphs,
                                        forward_backward=forward_backward,
-                                       communicate=grad_sync, update=update)
+                                       communicate=communicate or grad_sync, update=update)
     else:
         def train_step():
             loss = forward_backward()
@@ -156,6 +162,12 @@ def main():
     grad_sync = None
     if args.ddp or not use_graphs:
         model = launch.wrap_ddp(model, device, broadcast_buffers=False)
+    elif world > 1 and args.overlap_grad_comm and hasattr(model, 'forward_bottom'):
+        # backward in two graph segments; the top half's all-reduce runs
+        # while the bottom half's backward replays (parallel/overlap.py)
+        grad_sync = overlap.SplitBackward(
+            model, lambda out: F.cross_entropy(out, y, label_smoothing=0.1), lambda: x,
+            autocast=torch.bfloat16)
     elif world > 1:
         # one flat-arena all-reduce between graph replays (parallel/grad_sync.py)
         grad_sync = grad_sync_mod.GradientAllreduce(model)
@@ -201,10 +213,16 @@ def main():
         update()
         return loss
 
+    split = isinstance(grad_sync, overlap.SplitBackward)
+    fb_segments = grad_sync.segments if split else forward_backward
+    comm_segments = grad_sync.communicate if split else grad_sync
     if grad_sync is not None:
+        # phased_update: MEM_OPT / HYBRID_OPT plain steps replay as two graphs
+        # around the gradient all-gather instead of running eagerly
         step = graphs.GraphedTrainStep(None, pre, [opt], enabled=use_graphs,
-                                       forward_backward=forward_backward,
-                                       communicate=grad_sync, update=update)
+                                       forward_backward=fb_segments,
+                                       communicate=comm_segments, update=update,
+                                       phased_update=True)
     else:
         step = graphs.GraphedTrainStep(train_step, pre, [opt], enabled=use_graphs)
 
@@ -253,8 +271,8 @@ def main():
     phases = pre.timer.summary() if (pre is not None and args.profile_phases) else None
     sgd_ms = None
     if pre is not None and args.sgd_delta:
-        sgd_ms = time_sgd_only(args, model, opt, pre, forward_backward, grad_sync, use_graphs,
-                               device)
+        sgd_ms = time_sgd_only(args, model, opt, pre, fb_segments, grad_sync, use_graphs,
+                               device, communicate=comm_segments)
     if rank == 0:
         rec = {
             'metric': METRIC if pre is not None else 'images/sec (whole node) ResNet-50 SGD-only',
@@ -281,7 +299,8 @@ def main():
                            'inverse_lag': args.inverse_lag},
                        'hip_graphs': use_graphs,
                        'grad_allreduce': 'ddp' if grad_sync is None and world > 1 else
-                                         ('flat-arena' if world > 1 else None),
+                                         (('split-backward-overlap' if split else 'flat-arena')
+                                          if world > 1 else None),
                        'final_loss': round(float(loss.item()), 4)},
         }
         if per_kind:

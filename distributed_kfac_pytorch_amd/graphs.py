@@ -19,9 +19,20 @@ Two modes:
                   backward segment is a graph per kind; `communicate` (the
                   data-parallel gradient all-reduce, parallel/grad_sync.py)
                   runs eagerly between replays -- no collective is ever
-                  captured; `update` (preconditioner.step() + optimizer.step())
+                  captured.  `forward_backward` / `communicate` may be equal-
+                  length LISTS (a backward split into segments,
+                  parallel/overlap.py): segment i's graph replays, then
+                  communicate[i] issues its (async) collective, which runs
+                  while segment i+1 replays; the first segment returns the
+                  loss.  `update` (preconditioner.step() + optimizer.step())
                   is a graph only when it issues no collective for that kind
-                  (one rank, or K-FAC COMM_OPT plain steps), else eager.
+                  (one rank, or K-FAC COMM_OPT plain steps).  With
+                  `phased_update=True` (update == preconditioner.step() +
+                  optimizer.step()), a plain step that does communicate
+                  (MEM_OPT / HYBRID_OPT gradient all-gather) runs as two
+                  graphs -- KFAC.step_precondition, then KFAC.step_finish +
+                  optimizer.step() -- with KFAC.step_communicate eager between
+                  them; factor / inverse steps with collectives stay eager.
 
 Step kinds follow the K-FAC schedule (`factor_update_freq`, `inv_update_freq`,
 reference kfac/preconditioner.py:494-514); the K-FAC step counter that a graph
@@ -64,13 +75,23 @@ def _world_size():
 
 class GraphedTrainStep(object):
     def __init__(self, step_fn=None, preconditioner=None, optimizers=(), warmup=2, enabled=True,
-                 forward_backward=None, communicate=None, update=None):
+                 forward_backward=None, communicate=None, update=None, phased_update=False):
         if step_fn is None and (forward_backward is None or update is None):
             raise ValueError('give step_fn, or forward_backward and update')
         self.step_fn = step_fn
+        if isinstance(forward_backward, (list, tuple)):
+            comms = list(communicate) if isinstance(communicate, (list, tuple)) else \
+                [None] * (len(forward_backward) - 1) + [communicate]
+            if len(comms) != len(forward_backward):
+                raise ValueError('communicate must match forward_backward segment by segment')
+            self.fbs, self.comms = list(forward_backward), comms
+        else:
+            self.fbs, self.comms = [forward_backward], [communicate]
         self.fb, self.comm, self.update = forward_backward, communicate, update
         self.segmented = step_fn is None
         self.pre = preconditioner
+        # 'force' phases the update even when it issues no collective (tests)
+        self.phased_update = phased_update
         if preconditioner is not None and enabled:
             # the whole step is graphed: KFAC's own precondition-tail graph
             # is redundant
@@ -167,14 +188,28 @@ class GraphedTrainStep(object):
             return out
         if not self.segmented:
             return self._run_segment('step', kind, self.step_fn, advances=True)
-        loss = self._run_segment('fb', kind, self.fb, advances=False)
-        if self.comm is not None:
-            self.comm()
-        if self._update_capturable(kind):
+        loss = None
+        for i, (fb, cm) in enumerate(zip(self.fbs, self.comms)):
+            out = self._run_segment('fb' if i == 0 else 'fb%d' % i, kind, fb, advances=False)
+            if i == 0:
+                loss = out
+            if cm is not None:
+                cm()
+        if self.phased_update and kind == 'plain' and self.pre is not None and \
+                (self.phased_update == 'force' or not self._update_capturable(kind)):
+            self._run_segment('upd_pre', kind, self.pre.step_precondition, advances=False)
+            self.pre.step_communicate()
+            self._run_segment('upd_post', kind, self._finish, advances=True)
+        elif self._update_capturable(kind):
             self._run_segment('update', kind, self.update, advances=True)
         else:
             self.update()
         return loss
+
+    def _finish(self):
+        self.pre.step_finish()
+        for opt in self.optimizers:
+            opt.step()
 
     def _eager(self):
         if not self.enabled:
@@ -193,9 +228,13 @@ class GraphedTrainStep(object):
     def _eager_body(self):
         if not self.segmented:
             return self.step_fn()
-        loss = self.fb()
-        if self.comm is not None:
-            self.comm()
+        loss = None
+        for i, (fb, cm) in enumerate(zip(self.fbs, self.comms)):
+            out = fb()
+            if i == 0:
+                loss = out
+            if cm is not None:
+                cm()
         self.update()
         return loss
 

@@ -108,10 +108,25 @@ class ResNet(nn.Module):
         return nn.Sequential(*mods)
 
     def forward(self, x):
+        return self.forward_top(self.forward_bottom(x))
+
+    # the two halves of the network for a backward split at the layer2 /
+    # layer3 boundary (parallel/overlap.py): the top half holds ~90% of the
+    # parameters, whose gradients are complete first in backward
+    def forward_bottom(self, x):
         x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
-        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
-        x = torch.flatten(self.avgpool(x), 1)
-        return self.fc(x)
+        return self.layer2(self.layer1(x))
+
+    def forward_top(self, x):
+        x = self.layer4(self.layer3(x))
+        return self.fc(torch.flatten(self.avgpool(x), 1))
+
+    def split_parameters(self):
+        """(bottom, top) parameter lists of forward_bottom / forward_top."""
+        bottom = [self.conv1, self.bn1, self.layer1, self.layer2]
+        top = [self.layer3, self.layer4, self.fc]
+        return ([p for m in bottom for p in m.parameters()],
+                [p for m in top for p in m.parameters()])
 
 
 def resnet18(**kw):

@@ -10,8 +10,11 @@ hooks, so a forward+backward segment can be captured into a hipGraph and the
 all-reduce issued between graph replays (graphs.GraphedTrainStep, segmented
 mode); DDP's reducer, whose hooks run during backward, cannot.
 
-Trade-off vs DDP: no overlap of the all-reduce with backward (it runs after
-backward), in exchange for zero host launch overhead in forward/backward.
+Overlap with backward: `start()` issues the all-reduce asynchronously (RCCL's
+stream, joined later by `finish()`), so with a backward split into graph
+segments (parallel/overlap.py) the all-reduce of the gradients a segment
+completed runs while the next segment replays -- one GradientAllreduce per
+segment's parameters (`params=`).
 On construction parameters and buffers are broadcast from rank 0 (what DDP
 does), so ranks may initialise their models independently.
 
@@ -25,11 +28,13 @@ __all__ = ['GradientAllreduce']
 
 
 class GradientAllreduce(object):
-    def __init__(self, model, group=None, broadcast_from=0, average=True):
+    def __init__(self, model, group=None, broadcast_from=0, average=True, params=None):
         self.group = group
         self.average = average
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        params = [p for p in model.parameters() if p.requires_grad]
+        if params is None:
+            params = model.parameters()
+        params = [p for p in params if p.requires_grad]
         by_dtype = {}
         for p in params:
             by_dtype.setdefault(p.dtype, []).append(p)
@@ -48,7 +53,7 @@ class GradientAllreduce(object):
                 self.views.append((p, view))
                 off += n
             self.arenas.append(arena)
-        if self.world > 1:
+        if self.world > 1 and broadcast_from is not None:
             with torch.no_grad():
                 for t in list(model.parameters()) + list(model.buffers()):
                     dist.broadcast(t.data, src=broadcast_from, group=group)
@@ -84,16 +89,25 @@ class GradientAllreduce(object):
                     view.copy_(g)
                 p.grad = view
 
-    def __call__(self):
+    def start(self):
+        """Issue the all-reduce of every arena asynchronously -> handles."""
         if not self.check_views():
             self.rebind()
         if self.world <= 1:
-            return
-        for arena in self.arenas:
-            # SUM + scale (ReduceOp.AVG needs ncclAvg support in the RCCL build)
-            dist.all_reduce(arena, op=dist.ReduceOp.SUM, group=self.group)
+            return []
+        # SUM + scale (ReduceOp.AVG needs ncclAvg support in the RCCL build)
+        return [(dist.all_reduce(arena, op=dist.ReduceOp.SUM, group=self.group, async_op=True),
+                 arena) for arena in self.arenas]
+
+    def finish(self, handles):
+        """Order the current stream behind the all-reduces; average."""
+        for work, arena in handles:
+            work.wait()
             if self.average:
                 arena.mul_(1.0 / self.world)
+
+    def __call__(self):
+        self.finish(self.start())
 
 
 def _dense_strides(t):

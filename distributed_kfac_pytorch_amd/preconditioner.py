@@ -484,6 +484,36 @@ class KFAC(optim.Optimizer):
         p['step'] += 1
         return loss
 
+    # ------------------------------------------------- phased plain steps
+    # A plain step (no factor or inverse update) split at its one collective:
+    # graphs.GraphedTrainStep(phased_update=True) replays the two compute
+    # phases as hipGraphs and issues the MEM_OPT / HYBRID_OPT gradient
+    # all-gather eagerly between them, so those steps are no longer eager.
+    # step() == step_precondition(); step_communicate(); step_finish().
+    def is_plain_step(self):
+        p = self.param_groups[0]
+        return (self.workers_assigned and self._pending_inv is None
+                and p['step'] % p['factor_update_freq'] != 0
+                and p['step'] % p['inv_update_freq'] != 0)
+
+    @torch.no_grad()
+    def step_precondition(self):
+        if not self.is_plain_step():
+            raise RuntimeError('step_precondition() is for plain steps only; use step()')
+        self.compute_preconditioned_gradients(damping=self.param_groups[0]['damping'])
+
+    @torch.no_grad()
+    def step_communicate(self):
+        if self.comm_method in (CommMethod.MEM_OPT, CommMethod.HYBRID_OPT):
+            self.broadcast_gradients()
+
+    @torch.no_grad()
+    def step_finish(self):
+        p = self.param_groups[0]
+        scale = None if p['kl_clip'] is None else self._compute_grad_scale()
+        self.update_gradients(scale)
+        p['step'] += 1
+
     # ------------------------------------------------------------ hipGraphs
     def _precondition_and_apply(self):
         p = self.param_groups[0]

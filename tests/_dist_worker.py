@@ -151,3 +151,36 @@ def comm_check(rank, world, port, out_dir, cfg):
     # no barrier on the error path: the failing check is itself collective, so
     # every rank raised at the same phase
     dist.destroy_process_group()
+
+
+def split_backward(rank, world, port, out_dir, cfg):
+    """parallel/overlap.SplitBackward (two backward segments, two async
+    all-reduces) vs one backward + one flat-arena all-reduce: identical."""
+    _init(rank, world, port)
+    import copy
+    import torch.nn.functional as F
+    from distributed_kfac_pytorch_amd.models import resnet
+    from distributed_kfac_pytorch_amd.parallel.grad_sync import GradientAllreduce
+    from distributed_kfac_pytorch_amd.parallel.overlap import SplitBackward
+    torch.manual_seed(0)
+    m1 = resnet.resnet_tiny(num_classes=10)
+    m2 = copy.deepcopy(m1)
+    g = torch.Generator().manual_seed(rank)
+    x = torch.randn(4, 3, 32, 32, generator=g)
+    y = torch.randint(0, 10, (4,), generator=g)
+    sb = SplitBackward(m1, lambda out: F.cross_entropy(out, y), lambda: x)
+    loss1 = None
+    for i, (seg, cm) in enumerate(zip(sb.segments, sb.communicate)):
+        out = seg()
+        loss1 = out if i == 0 else loss1
+        cm()
+    ga = GradientAllreduce(m2)
+    ga.zero_grad()
+    loss2 = F.cross_entropy(m2(x), y)
+    loss2.backward()
+    ga()
+    same = all(torch.equal(p.grad, q.grad) for p, q in zip(m1.parameters(), m2.parameters()))
+    torch.save({'same': same, 'loss': (loss1.item(), loss2.item())},
+               os.path.join(out_dir, 'rank{}.pt'.format(rank)))
+    dist.barrier()
+    dist.destroy_process_group()

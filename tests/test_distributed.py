@@ -169,3 +169,14 @@ def test_comm_consistency_check(tmp_path, method, mode):
         assert all(e is not None and 'factor all-reduce' in e and '.A' in e for e in errs), errs
     else:
         assert all(e is not None and 'eigendata broadcast' in e and '0:' in e for e in errs), errs
+
+
+def test_split_backward_overlap_equals_single(tmp_path):
+    """The overlapped gradient all-reduce (backward in two segments, the top
+    half's all-reduce issued before the bottom half's backward) gives exactly
+    the gradients of one backward + one flat-arena all-reduce."""
+    _spawn(_dist_worker.split_backward, 2, tmp_path, {})
+    for r in range(2):
+        res = torch.load(os.path.join(str(tmp_path), 'rank{}.pt'.format(r)), weights_only=True)
+        assert res['same'], res
+        assert res['loss'][0] == res['loss'][1]

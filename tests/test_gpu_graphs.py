@@ -138,3 +138,55 @@ def test_graphed_lagged_inverses_match_eager(segmented):
         assert abs(a - b) < max(3e-2 * max(1.0, abs(a)), 4 * abs(a - a2)), (le, le2, lg)
     noise, diff = _pdiff(pe, pe2), _pdiff(pe, pg)
     assert diff < max(1e-2, 20 * noise), (diff, noise)
+
+
+def _train_split(use_graphs, steps=12, phased=False):
+    """resnet_tiny, fp32, deterministic: backward in two graph segments
+    (parallel/overlap.SplitBackward) and optionally the phased K-FAC update."""
+    from distributed_kfac_pytorch_amd.models import resnet
+    from distributed_kfac_pytorch_amd.parallel.overlap import SplitBackward
+    torch.manual_seed(0)
+    m = resnet.resnet_tiny(num_classes=10).cuda().to(memory_format=torch.channels_last)
+    opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9)
+    pre = kfac.KFAC(m, factor_update_freq=2, inv_update_freq=10, lr=0.05,
+                    compute_factor_in_hook=True)
+    g = torch.Generator(device='cuda').manual_seed(3)
+    xs = [torch.randn(8, 3, 32, 32, device='cuda', generator=g) for _ in range(steps)]
+    ys = [torch.randint(0, 10, (8,), device='cuda', generator=g) for _ in range(steps)]
+    x = torch.empty_like(xs[0]).contiguous(memory_format=torch.channels_last)
+    y = torch.empty_like(ys[0])
+    sb = SplitBackward(m, lambda out: F.cross_entropy(out, y), lambda: x)
+
+    def update():
+        pre.step()
+        opt.step()
+    step = graphs.GraphedTrainStep(None, pre, [opt], warmup=1, enabled=use_graphs,
+                                   forward_backward=sb.segments, communicate=sb.communicate,
+                                   update=update, phased_update='force' if phased else False)
+    losses = []
+    for i in range(steps):
+        x.copy_(xs[i])
+        y.copy_(ys[i])
+        losses.append(step().item())
+    return losses, [p.detach().clone() for p in m.parameters()], step
+
+
+@pytest.mark.parametrize('phased', [False, True])
+def test_split_backward_segments_graphed(phased):
+    """Two backward graph segments (the overlapped all-reduce layout) and the
+    phased K-FAC update (the MEM/HYBRID layout) replay exactly like eager."""
+    prev = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        le, pe, _ = _train_split(False, phased=phased)
+        lg, pg, sg = _train_split(True, phased=phased)
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = prev
+    assert sg.replays > 0
+    keys = {k[0] for k in sg.graphs}
+    assert {'fb', 'fb1'} <= keys, keys
+    if phased:
+        assert {'upd_pre', 'upd_post'} <= keys, keys
+    for a, b in zip(le, lg):
+        assert abs(a - b) <= 1e-6 * max(1.0, abs(a)), (le, lg)
+    assert _pdiff(pe, pg) <= 1e-6, _pdiff(pe, pg)
