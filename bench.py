@@ -79,6 +79,10 @@ def parse():
     ap.add_argument('--inverse-lag', type=int, default=0,
                     help='KFAC(inverse_lag=L): eigendecompositions of an inverse step run on a '
                          'side stream and take effect L steps later (0 = reference schedule)')
+    ap.add_argument('--assignment-strategy', default='measured',
+                    choices=['measured', 'compute', 'memory'],
+                    help="LPT cost of a factor's inverse: 'measured' = the MI355X fused-solver "
+                         "table (preconditioner.MEASURED_COST_MS), 'compute' = n^3 (reference)")
     ap.add_argument('--overlap-grad-comm', type=int, default=1,
                     help='world > 1 with graphs: backward in two graph segments, the top '
                          "half's gradient all-reduce overlapped with the bottom half's backward "
@@ -182,6 +186,7 @@ def main():
                         inv_update_freq=args.kfac_update_freq, kl_clip=args.kl_clip, lr=base_lr,
                         comm_method=method, grad_worker_fraction=args.grad_worker_fraction,
                         distribute_layer_factors=False, eigen_solver=args.eigen_solver,
+                        assignment_strategy=args.assignment_strategy,
                         profile=args.profile_phases, precond_precision=args.precond_precision,
                         compute_factor_in_hook=grad_sync is not None,
                         inverse_lag=args.inverse_lag,

@@ -119,6 +119,30 @@ def _inverse_executor():
     return _INV_EXECUTOR
 
 
+# Measured cost of one factor's eigendecomposition on MI355X with the fused
+# solver (reduction + divide and conquer + back-transformation), fitted to
+# probe timings of (n, batch) classes: T(n, b) = a n + b (c2 n^2 + c3 n^3) ms
+# (profiles/r2_eig_cost_fit.log).  The per-column term dominates: the
+# reduction is a latency-bound chain of n columns, so the reference's n^3
+# (kfac/preconditioner.py:625-631) overstates big factors ~5x against small.
+MEASURED_COST_MS = (1.622e-2, 1.963e-7, 1.389e-10)
+
+
+def measured_cost(n):
+    a, c2, c3 = MEASURED_COST_MS
+    return a * n + c2 * n * n + c3 * n ** 3
+
+
+def assignment_cost(strategy):
+    """n -> LPT cost of a factor: 'compute' n^3 and 'memory' n^2 (reference
+    semantics, kfac/preconditioner.py:625-631), 'measured' the MI355X table,
+    or a user callable."""
+    if callable(strategy):
+        return strategy
+    return {'compute': lambda n: n ** 3, 'memory': lambda n: n ** 2,
+            'measured': measured_cost}[strategy]
+
+
 class KFAC(optim.Optimizer):
     def __init__(self, model, damping=0.001, factor_decay=0.95, factor_update_freq=10,
                  inv_update_freq=100, kl_clip=0.001, lr=0.1, accumulate_data=False,
@@ -147,8 +171,10 @@ class KFAC(optim.Optimizer):
         if inv_update_freq % factor_update_freq != 0:
             warnings.warn('It is suggested that inv_update_freq be a multiple of '
                           'factor_update_freq')
-        if assignment_strategy not in ('compute', 'memory'):
-            raise ValueError('assignment_strategy must be "compute" or "memory"')
+        if not callable(assignment_strategy) and \
+                assignment_strategy not in ('compute', 'memory', 'measured'):
+            raise ValueError('assignment_strategy must be "compute", "memory", "measured" or '
+                             'a callable n -> cost')
         if not isinstance(comm_method, CommMethod):
             raise ValueError('comm_method must be a kfac.CommMethod')
         if comm_method in (CommMethod.MEM_OPT, CommMethod.HYBRID_OPT) and \
@@ -872,7 +898,7 @@ class KFAC(optim.Optimizer):
         """LPT-balance inverse work over ranks and lay out the execution plan."""
         if len(self.layers) == 0:
             return
-        cost = (lambda n: n ** 3) if self.assignment_strategy == 'compute' else (lambda n: n ** 2)
+        cost = assignment_cost(self.assignment_strategy)
         a_sizes = [l.state['A'].shape[0] for l in self.layers]
         g_sizes = [l.state['G'].shape[0] for l in self.layers]
         a_times = [cost(n) for n in a_sizes]
