@@ -297,6 +297,7 @@ def main():
                        'image_size': S, 'seq_len': None, 'parallelism': 'dp{}'.format(world),
                        'kfac': None if pre is None else {
                            'comm_method': args.comm_method,
+                           'assignment_strategy': args.assignment_strategy,
                            'factor_update_freq': args.kfac_cov_update_freq,
                            'inv_update_freq': args.kfac_update_freq,
                            'damping': args.damping, 'kl_clip': args.kl_clip,
