@@ -44,6 +44,8 @@ struct PatchArgs {
   float* ws;              // f32 workspace, row-major, leading dim ldw
   int ldw;
   float* part;            // nullptr: f32 atomics into ws; else [split][tile][BT*BT] partials
+  const float* dscale;    // nullptr, or a device factor on `scale` (AMP: finite(g) / s^2;
+                          // 0 drops the source without letting its NaN / Inf through)
 };
 
 constexpr int BT = 128;   // output tile
@@ -110,6 +112,9 @@ __device__ __forceinline__ void decompose_row(const PatchArgs& p, long long row,
 __device__ __forceinline__ void store_tile(const PatchArgs& p, const f32x16_t (&acc)[2][2],
                                            int tile, int split, int ti, int tj, bool diag, int wr,
                                            int wc, int lr, int lh) {
+  const float ds = p.dscale != nullptr ? *p.dscale : 1.f;
+  const float sc = p.scale * ds;
+  const bool drop = (ds == 0.f);
   if (p.part != nullptr) {
     const int tp = p.ntiles * (p.ntiles + 1) / 2;
     float* dst = p.part + ((long long)split * tp + tile) * (BT * BT);
@@ -121,7 +126,7 @@ __device__ __forceinline__ void store_tile(const PatchArgs& p, const f32x16_t (&
         for (int r = 0; r < 16; ++r) {
           const int lrow = wr * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
           const int lcol = wc * 64 + n * 32 + lr;
-          dst[lrow * BT + lcol] = p.scale * acc[m][n][r];
+          dst[lrow * BT + lcol] = drop ? 0.f : sc * acc[m][n][r];
         }
     return;
   }
@@ -133,8 +138,8 @@ __device__ __forceinline__ void store_tile(const PatchArgs& p, const f32x16_t (&
       for (int r = 0; r < 16; ++r) {
         int row = ti * BT + wr * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
         int col = tj * BT + wc * 64 + n * 32 + lr;
-        if (row < p.ncols && col < p.ncols && (!diag || row <= col))
-          atomicAdd(p.ws + (long long)row * p.ldw + col, p.scale * acc[m][n][r]);
+        if (!drop && row < p.ncols && col < p.ncols && (!diag || row <= col))
+          atomicAdd(p.ws + (long long)row * p.ldw + col, sc * acc[m][n][r]);
       }
 }
 
@@ -505,7 +510,7 @@ struct SyrkProblem {
 
 // Tables travel BY VALUE in the kernel arguments (< 4 KB), so a launch is
 // capturable into a hipGraph with its problem pointers baked in (no H2D copy).
-constexpr int MAX_SYRK_PROBLEMS = 24;
+constexpr int MAX_SYRK_PROBLEMS = 22;
 struct SyrkBatch {
   int count, pad[3];
   SyrkProblem prob[MAX_SYRK_PROBLEMS];
@@ -536,6 +541,7 @@ struct EmaJob {
   int n, ldw, kcols, C, kk, sdtype, row_begin, pad;
   float a1, a2;
   int mode, pad2;
+  const float* keep;     // nullptr, or device flag: 0 leaves the factor untouched (AMP)
 };
 
 // Reference column order (c, i, j) -> internal order (i, j, c) of syrk_vec.
@@ -549,8 +555,10 @@ __device__ __forceinline__ int perm_col(int x, int kcols, int C, int kk) {
 template <int SDT>
 __global__ __launch_bounds__(256) void factor_ema_perm_kernel(
     typename DTypeTraits<SDT>::raw_t* __restrict__ state, const float* __restrict__ ws,
-    int n, int ldw, float a1, float a2, int mode, int kcols, int C, int kk) {
+    int n, int ldw, float a1, float a2, int mode, int kcols, int C, int kk,
+    const float* __restrict__ keep) {
   typedef DTypeTraits<SDT> Tr;
+  if (keep != nullptr && *keep == 0.f) return;
   const int i = blockIdx.y;
   const int pi = perm_col(i, kcols, C, kk);
   for (int j = blockIdx.x * 256 + threadIdx.x; j < n; j += gridDim.x * 256) {
@@ -565,6 +573,7 @@ __global__ __launch_bounds__(256) void factor_ema_perm_kernel(
 template <int SDT>
 __device__ __forceinline__ void ema_perm_row(const EmaJob& J, int i) {
   typedef DTypeTraits<SDT> Tr;
+  if (J.keep != nullptr && *J.keep == 0.f) return;
   typename Tr::raw_t* state = (typename Tr::raw_t*)J.state;
   const int pi = perm_col(i, J.kcols, J.C, J.kk);
   for (int j = threadIdx.x; j < J.n; j += 256) {
@@ -576,7 +585,7 @@ __device__ __forceinline__ void ema_perm_row(const EmaJob& J, int i) {
   }
 }
 
-constexpr int MAX_EMA_JOBS = 60;
+constexpr int MAX_EMA_JOBS = 56;
 struct EmaBatch {
   int count, pad[3];
   EmaJob job[MAX_EMA_JOBS];
@@ -605,8 +614,9 @@ __global__ __launch_bounds__(256) void factor_ema_grouped_kernel(const EmaBatch*
 template <int SDT>
 __global__ __launch_bounds__(256) void factor_ema_kernel(
     typename DTypeTraits<SDT>::raw_t* __restrict__ state, const float* __restrict__ ws,
-    int n, int ldw, float a1, float a2, int mode) {
+    int n, int ldw, float a1, float a2, int mode, const float* __restrict__ keep) {
   typedef DTypeTraits<SDT> Tr;
+  if (keep != nullptr && *keep == 0.f) return;
   __shared__ float tile[32][33];
   const int bi = blockIdx.y, bj = blockIdx.x;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
@@ -673,9 +683,11 @@ __global__ __launch_bounds__(256) void triu_unpack_kernel(
 KFAC_API int kfac_syrk_patch(int dtype, const void* x, long long sb, long long sc, long long sh,
                              long long sw, int B, int C, int H, int W, int kh, int kw, int sth,
                              int stw, int ph, int pw, int dh, int dw, int has_bias, float scale,
-                             float* ws, int ldw, int max_blocks, float* part, hipStream_t stream) {
+                             float* ws, int ldw, int max_blocks, float* part,
+                             const float* dscale, hipStream_t stream) {
   PatchArgs p;
   p.part = part;
+  p.dscale = dscale;
   p.x = x; p.sb = sb; p.sc = sc; p.sh = sh; p.sw = sw;
   p.B = B; p.C = C; p.H = H; p.W = W;
   p.kh = kh; p.kw = kw; p.sth = sth; p.stw = stw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
@@ -719,13 +731,15 @@ KFAC_API int kfac_syrk_patch(int dtype, const void* x, long long sb, long long s
 KFAC_API int kfac_syrk_vec(int dtype, const void* x, long long sb, long long sc, long long sh,
                            long long sw, int B, int C, int H, int W, int kh, int kw, int sth,
                            int stw, int ph, int pw, int dh, int dw, int has_bias, float scale,
-                           float* ws, int ldw, int max_blocks, float* part, hipStream_t stream) {
+                           float* ws, int ldw, int max_blocks, float* part,
+                           const float* dscale, hipStream_t stream) {
   if (!(dtype == KDT_BF16 || dtype == KDT_F16)) return 0;
   if (sc != 1 || (C % 8) || (sb % 8) || (H > 1 && (sh % 8)) || (W > 1 && (sw % 8)) ||
       (((uintptr_t)x) & 15))
     return 0;
   PatchArgs p;
   p.part = part;
+  p.dscale = dscale;
   p.x = x; p.sb = sb; p.sc = sc; p.sh = sh; p.sw = sw;
   p.B = B; p.C = C; p.H = H; p.W = W;
   p.kh = kh; p.kw = kw; p.sth = sth; p.stw = stw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
@@ -757,33 +771,33 @@ KFAC_API int kfac_syrk_vec(int dtype, const void* x, long long sb, long long sc,
 
 KFAC_API int kfac_factor_ema_perm(int sdtype, void* state, const float* ws, int n, int ldw,
                                   float alpha, int mode, int kcols, int C, int kk,
-                                  hipStream_t stream) {
+                                  const float* keep, hipStream_t stream) {
   float a1 = 0.f, a2 = 1.f;
   if (mode == 0) { a1 = alpha / (1.f - alpha); a2 = 1.f - alpha; }
   dim3 grid((n + 255) / 256 < 8 ? (n + 255) / 256 : 8, n), block(256);
   if (sdtype == KDT_F32)
-    hipLaunchKernelGGL(factor_ema_perm_kernel<KDT_F32>, grid, block, 0, stream, (float*)state, ws, n, ldw, a1, a2, mode, kcols, C, kk);
+    hipLaunchKernelGGL(factor_ema_perm_kernel<KDT_F32>, grid, block, 0, stream, (float*)state, ws, n, ldw, a1, a2, mode, kcols, C, kk, keep);
   else if (sdtype == KDT_BF16)
-    hipLaunchKernelGGL(factor_ema_perm_kernel<KDT_BF16>, grid, block, 0, stream, (uint16_t*)state, ws, n, ldw, a1, a2, mode, kcols, C, kk);
+    hipLaunchKernelGGL(factor_ema_perm_kernel<KDT_BF16>, grid, block, 0, stream, (uint16_t*)state, ws, n, ldw, a1, a2, mode, kcols, C, kk, keep);
   else if (sdtype == KDT_F16)
-    hipLaunchKernelGGL(factor_ema_perm_kernel<KDT_F16>, grid, block, 0, stream, (uint16_t*)state, ws, n, ldw, a1, a2, mode, kcols, C, kk);
+    hipLaunchKernelGGL(factor_ema_perm_kernel<KDT_F16>, grid, block, 0, stream, (uint16_t*)state, ws, n, ldw, a1, a2, mode, kcols, C, kk, keep);
   else
     return -1;
   return (int)hipGetLastError();
 }
 
 KFAC_API int kfac_factor_ema(int sdtype, void* state, const float* ws, int n, int ldw, float alpha,
-                             int mode, hipStream_t stream) {
+                             int mode, const float* keep, hipStream_t stream) {
   float a1 = 0.f, a2 = 1.f;
   if (mode == 0) { a1 = alpha / (1.f - alpha); a2 = 1.f - alpha; }
   int nb = (n + 31) / 32;
   dim3 grid(nb, nb), block(256);
   if (sdtype == KDT_F32)
-    hipLaunchKernelGGL(factor_ema_kernel<KDT_F32>, grid, block, 0, stream, (float*)state, ws, n, ldw, a1, a2, mode);
+    hipLaunchKernelGGL(factor_ema_kernel<KDT_F32>, grid, block, 0, stream, (float*)state, ws, n, ldw, a1, a2, mode, keep);
   else if (sdtype == KDT_BF16)
-    hipLaunchKernelGGL(factor_ema_kernel<KDT_BF16>, grid, block, 0, stream, (uint16_t*)state, ws, n, ldw, a1, a2, mode);
+    hipLaunchKernelGGL(factor_ema_kernel<KDT_BF16>, grid, block, 0, stream, (uint16_t*)state, ws, n, ldw, a1, a2, mode, keep);
   else if (sdtype == KDT_F16)
-    hipLaunchKernelGGL(factor_ema_kernel<KDT_F16>, grid, block, 0, stream, (uint16_t*)state, ws, n, ldw, a1, a2, mode);
+    hipLaunchKernelGGL(factor_ema_kernel<KDT_F16>, grid, block, 0, stream, (uint16_t*)state, ws, n, ldw, a1, a2, mode, keep);
   else
     return -1;
   return (int)hipGetLastError();
@@ -836,6 +850,7 @@ KFAC_API int kfac_syrk_problem_init(SyrkProblem* P, int block_begin, int dtype, 
     return 0;
   PatchArgs& p = P->p;
   p.part = nullptr;      // kfac_syrk_problem_set_part
+  p.dscale = nullptr;    // kfac_syrk_problem_set_dscale
   p.x = x; p.sb = sb; p.sc = sc; p.sh = sh; p.sw = sw;
   p.B = B; p.C = C; p.H = H; p.W = W;
   p.kh = kh; p.kw = kw; p.sth = sth; p.stw = stw; p.ph = ph; p.pw = pw; p.dh = dh; p.dw = dw;
@@ -930,6 +945,9 @@ KFAC_API long long kfac_syrk_splits(int vec, long long M, int ncols, int max_blo
 }
 
 KFAC_API void kfac_syrk_problem_set_part(SyrkProblem* P, float* part) { P->p.part = part; }
+KFAC_API void kfac_syrk_problem_set_dscale(SyrkProblem* P, const float* dscale) {
+  P->p.dscale = dscale;
+}
 
 KFAC_API int kfac_red_job_size() { return (int)sizeof(RedJob); }
 KFAC_API int kfac_red_max_contrib() { return MAX_CONTRIB; }

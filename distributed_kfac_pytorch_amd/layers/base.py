@@ -372,7 +372,14 @@ class KFACLayer(object):
     def save_grad_outputs(self, grad_output):
         g = grad_output[0].detach()
         if self.grad_scaler is not None:
-            g = (g, self.grad_scaler.get_scale())
+            # the loss scale as a DEVICE tensor (get_scale() is a host read that
+            # breaks hipGraph capture); a copy, update() may change it later
+            if g.is_cuda and hasattr(self.grad_scaler, '_get_scale_async') and \
+                    self.grad_scaler._get_scale_async() is not None:
+                sc = self.grad_scaler._get_scale_async().detach().reshape(1).float().clone()
+            else:
+                sc = self.grad_scaler.get_scale()
+            g = (g, sc)
         if self.accumulate_data:
             self.g_outputs.append(g)
         else:
@@ -383,28 +390,38 @@ class KFACLayer(object):
 
     def take_factor_job(self, which):
         """Consume the saved hook data of factor `which` ('A' or 'G') and
-        return (sources, out_dtype) for the GPU factor kernels, or None when
-        there is nothing to add.  G applies the AMP unscale / non-finite
-        filter of the reference (base.py:392-417) to the source scales."""
+        return (sources, out_dtype, keep) for the GPU factor kernels, or None
+        when there is nothing to add.  G applies the AMP unscale / non-finite
+        filter of the reference (base.py:392-417) ON THE DEVICE: each source's
+        scale gets a device factor finite(g) / s^2 (0 drops an overflowed
+        source without a host read) and `keep` (any source finite) leaves the
+        factor untouched when none is -- graph-capturable under GradScaler."""
         if which == 'A':
             if len(self.a_inputs) == 0:
                 return None
             inputs, self.a_inputs = self.a_inputs, []
-            return self._a_sources(inputs), self._factor_out_dtype(inputs[0])
-        kept, unscale = self._take_g_outputs()
-        if not kept:
+            return self._a_sources(inputs), self._factor_out_dtype(inputs[0]), None
+        outputs, self.g_outputs = self.g_outputs, []
+        if not outputs:
             return None
-        srcs = self._g_sources(kept)
-        for s, u in zip(srcs, unscale):
-            s.scale /= (u * u)
-        return srcs, self._factor_out_dtype(kept[0])
+        if self.grad_scaler is None:
+            return self._g_sources(outputs), self._factor_out_dtype(outputs[0]), None
+        gs = [g for g, _ in outputs]
+        srcs = self._g_sources(gs)
+        keep = None
+        for s, (g, sc) in zip(srcs, outputs):
+            fin = torch.isfinite(g).all().reshape(1)
+            sc = sc if torch.is_tensor(sc) else torch.full((1,), float(sc), device=g.device)
+            s.dscale = torch.where(fin, 1.0 / (sc * sc), torch.zeros_like(sc))
+            keep = fin if keep is None else (keep | fin)
+        return srcs, self._factor_out_dtype(gs[0]), keep.float()
 
     def _take_g_outputs(self):
         outputs, self.g_outputs = self.g_outputs, []
         if self.grad_scaler is None:
             return outputs, [1.0] * len(outputs)
         kept, unscale = [], []
-        for g, s in outputs:
+        for g, s in outputs:     # CPU reference path (host checks are free here)
             if torch.isfinite(g).all():
                 kept.append(g)
                 unscale.append(float(s))
@@ -418,7 +435,7 @@ class KFACLayer(object):
         if len(self.a_inputs) == 0:
             return
         if _lib.use_native(self.a_inputs[0]):
-            srcs, dtype = self.take_factor_job('A')
+            srcs, dtype, _ = self.take_factor_job('A')
             self.state['A'] = factor_ops.update_factor(self.state['A'], srcs, alpha, dtype)
             return
         inputs, self.a_inputs = self.a_inputs, []
@@ -436,7 +453,8 @@ class KFACLayer(object):
         if _lib.use_native(first[0] if isinstance(first, tuple) else first):
             job = self.take_factor_job('G')
             if job is not None:
-                self.state['G'] = factor_ops.update_factor(self.state['G'], job[0], alpha, job[1])
+                self.state['G'] = factor_ops.update_factor(self.state['G'], job[0], alpha, job[1],
+                                                           keep=job[2])
             return
         kept, unscale = self._take_g_outputs()
         if len(kept) == 0:

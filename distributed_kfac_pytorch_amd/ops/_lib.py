@@ -54,13 +54,14 @@ class DcRecord(ctypes.Structure):
 _SIGS = {
     'kfac_syrk_patch': [c_int, c_vp, c_ll, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_int, c_int,
                         c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_vp, c_int,
-                        c_int, c_vp, c_vp],
-    'kfac_factor_ema': [c_int, c_vp, c_vp, c_int, c_int, c_f, c_int, c_vp],
+                        c_int, c_vp, c_vp, c_vp],
+    'kfac_factor_ema': [c_int, c_vp, c_vp, c_int, c_int, c_f, c_int, c_vp, c_vp],
     'kfac_syrk_vec': [c_int, c_vp, c_ll, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_int, c_int,
                       c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_vp, c_int,
-                      c_int, c_vp, c_vp],
+                      c_int, c_vp, c_vp, c_vp],
     'kfac_syrk_splits': [c_int, c_ll, c_int, c_int],
     'kfac_syrk_problem_set_part': [c_vp, c_vp],
+    'kfac_syrk_problem_set_dscale': [c_vp, c_vp],
     'kfac_red_job_size': [],
     'kfac_red_max_contrib': [],
     'kfac_tile_reduce': [c_vp, c_int, c_vp],
@@ -72,7 +73,7 @@ _SIGS = {
     'kfac_syrk_grouped': [c_vp, c_int, c_int, c_vp],
     'kfac_ema_grouped': [c_vp, c_int, c_vp],
     'kfac_factor_ema_perm': [c_int, c_vp, c_vp, c_int, c_int, c_f, c_int, c_int, c_int, c_int,
-                             c_vp],
+                             c_vp, c_vp],
     'kfac_triu_pack': [c_int, c_vp, c_vp, c_int, c_vp],
     'kfac_triu_unpack': [c_int, c_vp, c_vp, c_int, c_f, c_vp],
     'kfac_grouped_kl_dot': [ctypes.POINTER(MatRecord), c_int, c_vp, c_vp],
@@ -118,7 +119,7 @@ _SIGS = {
 
 _RESTYPES = {'kfac_sytrd_ws_floats': c_ll, 'kfac_sytrd_forget': None, 'kfac_dc_ws_bytes': c_ll,
              'kfac_reduce_ws_floats': c_ll, 'kfac_syrk_splits': c_ll,
-             'kfac_syrk_problem_set_part': None}
+             'kfac_syrk_problem_set_part': None, 'kfac_syrk_problem_set_dscale': None}
 
 
 def _load():

@@ -27,10 +27,13 @@ POINTWISE = Geometry(1, 1, 1, 1, 0, 0, 1, 1)
 
 class FactorSource(object):
     """A (B, C, H, W)-strided tensor viewed as an implicit patch matrix."""
-    __slots__ = ('x', 'geom', 'has_bias', 'scale', 'ncols')
+    __slots__ = ('x', 'geom', 'has_bias', 'scale', 'ncols', 'dscale')
 
-    def __init__(self, x4d, geom, has_bias, scale):
+    def __init__(self, x4d, geom, has_bias, scale, dscale=None):
         self.x, self.geom, self.has_bias, self.scale = x4d, geom, has_bias, float(scale)
+        # optional device f32 scalar multiplying `scale` (AMP: finite(g) / s^2,
+        # 0 drops the source; no host read)
+        self.dscale = dscale
         self.ncols = x4d.shape[1] * geom.kh * geom.kw + (1 if has_bias else 0)
 
     @property
@@ -103,6 +106,8 @@ def _check_red_layout():
     L = _lib.lib()
     if L.kfac_red_job_size() != ctypes.sizeof(RedJob) or L.kfac_red_max_contrib() != 8:
         raise RuntimeError('RedJob layout mismatch with the native library')
+    if L.kfac_ema_job_size() != ctypes.sizeof(EmaJob):
+        raise RuntimeError('EmaJob layout mismatch with the native library')
 
 
 def accumulate_sources(sources, ws, allow_vec=True):
@@ -151,7 +156,8 @@ def accumulate_sources(sources, ws, allow_vec=True):
                 raise ValueError('factor source has {} columns, workspace {}'.format(s.ncols, n))
             r = L.kfac_syrk_vec(_lib.DTYPE_CODE[x.dtype], _lib.ptr(x), sb, sc, sh, sw, B, C, H, W,
                                 g.kh, g.kw, g.sh, g.sw, g.ph, g.pw, g.dh, g.dw, int(s.has_bias),
-                                s.scale, _lib.ptr(ws), ws.stride(0), 0, part, stream)
+                                s.scale, _lib.ptr(ws), ws.stride(0), 0, part,
+                                _dptr(s.dscale), stream)
             if r != 1:
                 raise RuntimeError('kfac_syrk_vec failed ({})'.format(r))
             kk = g.kh * g.kw
@@ -176,7 +182,7 @@ def accumulate_sources(sources, ws, allow_vec=True):
         _lib.check(L.kfac_syrk_patch(
             _lib.DTYPE_CODE[x.dtype], _lib.ptr(x), sb, sc, sh, sw, B, C, H, W,
             g.kh, g.kw, g.sh, g.sw, g.ph, g.pw, g.dh, g.dw, int(s.has_bias), s.scale,
-            _lib.ptr(ws), ws.stride(0), 0, part, stream), 'kfac_syrk_patch')
+            _lib.ptr(ws), ws.stride(0), 0, part, _dptr(s.dscale), stream), 'kfac_syrk_patch')
     if det:
         _tile_reduce([_red_job(ws.data_ptr(), ws.stride(0), n, contribs)], stream)
     return None
@@ -190,21 +196,27 @@ def _tile_reduce(jobs, stream):
     _lib.check(_lib.lib().kfac_tile_reduce(arr, len(jobs), stream), 'kfac_tile_reduce')
 
 
-def _ema(state, ws, n, alpha, mode, order):
+def _dptr(t):
+    return None if t is None else _lib.ptr(t)
+
+
+def _ema(state, ws, n, alpha, mode, order, keep=None):
+    """keep: None or a device f32 flag; 0 leaves the factor untouched (AMP:
+    no finite source this step, the reference skips the update)."""
     L = _lib.lib()
     dev = ws.device
     if order is None:
         _lib.check(L.kfac_factor_ema(_lib.DTYPE_CODE[state.dtype], _lib.ptr(state), _lib.ptr(ws),
-                                     n, n, float(alpha), mode, _lib.stream(dev)),
+                                     n, n, float(alpha), mode, _dptr(keep), _lib.stream(dev)),
                    'kfac_factor_ema')
     else:
         kcols, C, kk = order
         _lib.check(L.kfac_factor_ema_perm(_lib.DTYPE_CODE[state.dtype], _lib.ptr(state),
                                           _lib.ptr(ws), n, n, float(alpha), mode, kcols, C, kk,
-                                          _lib.stream(dev)), 'kfac_factor_ema_perm')
+                                          _dptr(keep), _lib.stream(dev)), 'kfac_factor_ema_perm')
 
 
-def update_factor(state, sources, alpha, out_dtype):
+def update_factor(state, sources, alpha, out_dtype, keep=None):
     """Running-average factor update on the GPU.
 
     state: existing factor (n x n, any of f32/bf16/f16) or None (-> identity).
@@ -220,7 +232,7 @@ def update_factor(state, sources, alpha, out_dtype):
         return state
     ws = _lib.workspace(dev, n * n).view(n, n)
     order = accumulate_sources(sources, ws)
-    _ema(state, ws, n, alpha, 0, order)
+    _ema(state, ws, n, alpha, 0, order, keep)
     return state
 
 
@@ -242,7 +254,7 @@ class EmaJob(ctypes.Structure):
                 ('C', ctypes.c_int), ('kk', ctypes.c_int), ('sdtype', ctypes.c_int),
                 ('row_begin', ctypes.c_int), ('pad', ctypes.c_int),
                 ('a1', ctypes.c_float), ('a2', ctypes.c_float),
-                ('mode', ctypes.c_int), ('pad2', ctypes.c_int)]
+                ('mode', ctypes.c_int), ('pad2', ctypes.c_int), ('keep', ctypes.c_void_p)]
 
 
 SPLIT_ROWS = 2048   # patch rows per block of the grouped SYRK
@@ -251,7 +263,8 @@ SPLIT_ROWS = 2048   # patch rows per block of the grouped SYRK
 def update_factors_grouped(items, alpha):
     """Running-average update of MANY factors in a fixed number of launches.
 
-    items: list of (state_or_None, sources, out_dtype).  Returns the list of
+    items: list of (state_or_None, sources, out_dtype[, keep]) -- keep: None or
+    a device f32 flag (0: leave the factor as it is).  Returns the list of
     updated states (new identity-initialised tensors where state was None).
     Every factor whose sources all qualify for the channels-contiguous path
     goes through ONE grouped SYRK launch per input dtype plus ONE grouped EMA
@@ -265,7 +278,8 @@ def update_factors_grouped(items, alpha):
     stream = _lib.stream(dev)
     out = [None] * len(items)
     grouped, rest = [], []
-    for k, (state, sources, out_dtype) in enumerate(items):
+    items = [tuple(it) + (None,) * (4 - len(it)) for it in items]
+    for k, (state, sources, out_dtype, _) in enumerate(items):
         if alpha != 1 and all(_vec_eligible(s) for s in sources) and \
                 len(sources) <= MAX_CONTRIB and \
                 len({(s.x.dtype, s.x.shape[1], s.geom.kh * s.geom.kw) for s in sources}) == 1:
@@ -273,8 +287,8 @@ def update_factors_grouped(items, alpha):
         else:
             rest.append(k)
     for k in rest:
-        state, sources, out_dtype = items[k]
-        out[k] = update_factor(state, sources, alpha, out_dtype)
+        state, sources, out_dtype, keep = items[k]
+        out[k] = update_factor(state, sources, alpha, out_dtype, keep)
     if not grouped:
         return out
     _check_red_layout()
@@ -322,6 +336,7 @@ def update_factors_grouped(items, alpha):
         for i, ((k, s), nb) in enumerate(zip(probs, nbs)):
             ptr = parts.data_ptr() + 4 * poff
             L.kfac_syrk_problem_set_part(ctypes.byref(raw, i * psize), _lib.c_vp(ptr))
+            L.kfac_syrk_problem_set_dscale(ctypes.byref(raw, i * psize), _dptr(s.dscale))
             contribs[k].append((ptr, nb // _tile_pairs(ws_of[k][1])))
             poff += nb * TILE * TILE
         _lib.check(L.kfac_syrk_grouped(raw, len(probs), _lib.DTYPE_CODE[dtype], stream),
@@ -331,7 +346,7 @@ def update_factors_grouped(items, alpha):
     jobs = (EmaJob * len(grouped))()
     a1, a2 = alpha / (1.0 - alpha), 1.0 - alpha
     for j, k in enumerate(grouped):
-        state, sources, out_dtype = items[k]
+        state, sources, out_dtype, keep = items[k]
         n = sizes[j]
         if state is None:
             state = torch.eye(n, dtype=out_dtype, device=dev)
@@ -345,5 +360,6 @@ def update_factors_grouped(items, alpha):
         J.n, J.ldw, J.kcols, J.C, J.kk = n, n, C * kk, C, kk
         J.sdtype = _lib.DTYPE_CODE[state.dtype]
         J.a1, J.a2, J.mode = a1, a2, 0
+        J.keep = None if keep is None else keep.data_ptr()
     _lib.check(L.kfac_ema_grouped(jobs, len(grouped), stream), 'kfac_ema_grouped')
     return out

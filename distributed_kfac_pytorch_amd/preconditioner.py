@@ -821,7 +821,7 @@ class KFAC(optim.Optimizer):
                 for which in ('A', 'G'):
                     job = layer.take_factor_job(which)
                     if job is not None:
-                        items.append((layer.state[which], job[0], job[1]))
+                        items.append((layer.state[which], job[0], job[1], job[2]))
                         refs.append((layer, which))
             for (layer, which), st in zip(refs, factor_ops.update_factors_grouped(items, alpha)):
                 layer.state[which] = st

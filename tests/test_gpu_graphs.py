@@ -190,3 +190,62 @@ def test_split_backward_segments_graphed(phased):
     for a, b in zip(le, lg):
         assert abs(a - b) <= 1e-6 * max(1.0, abs(a)), (le, lg)
     assert _pdiff(pe, pg) <= 1e-6, _pdiff(pe, pg)
+
+
+def _train_fp16(use_graphs, steps=14, overflow_at=None):
+    """fp16 autocast + GradScaler + fused SGD (found_inf consumed on the
+    device): K-FAC's G unscale / non-finite filter is device-side, so the
+    whole step -- scaler.unscale_, KFAC.step, scaler.step, scaler.update --
+    is capturable."""
+    torch.manual_seed(0)
+    m = resnet_cifar.resnet20().cuda().to(memory_format=torch.channels_last)
+    opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9, fused=True)
+    scaler = torch.amp.GradScaler('cuda', init_scale=2.0 ** 12)
+    pre = kfac.KFAC(m, factor_update_freq=2, inv_update_freq=10, lr=0.05, grad_scaler=scaler)
+    g = torch.Generator(device='cuda').manual_seed(3)
+    xs = [torch.randn(16, 3, 32, 32, device='cuda', generator=g) for _ in range(steps)]
+    ys = [torch.randint(0, 10, (16,), device='cuda', generator=g) for _ in range(steps)]
+    x = torch.empty_like(xs[0]).contiguous(memory_format=torch.channels_last)
+    y = torch.empty_like(ys[0])
+    mult = torch.ones((), device='cuda')     # 1e30 at overflow_at: inf gradients in fp16
+
+    def step_fn():
+        opt.zero_grad(set_to_none=False)
+        with torch.autocast('cuda', dtype=torch.float16):
+            loss = F.cross_entropy(m(x), y)
+        scaler.scale(loss * mult).backward()
+        scaler.unscale_(opt)
+        pre.step()
+        scaler.step(opt)
+        scaler.update()
+        return loss
+
+    step = graphs.GraphedTrainStep(step_fn, pre, [opt], warmup=1, enabled=use_graphs)
+    losses = []
+    for i in range(steps):
+        x.copy_(xs[i])
+        y.copy_(ys[i])
+        mult.fill_(1e30 if i == overflow_at else 1.0)
+        losses.append(step().item())
+    return losses, [p.detach().clone() for p in m.parameters()], step, pre
+
+
+def test_fp16_gradscaler_step_captures():
+    le, pe, _, _ = _train_fp16(False)
+    lg, pg, sg, pre = _train_fp16(True)
+    assert sg.replays > 0 and {'plain', 'factor'} <= {k[1] for k in sg.graphs}, sg.graphs.keys()
+    assert all(torch.isfinite(p).all() for p in pg)
+    for a, b in zip(le, lg):
+        assert abs(a - b) < 3e-2 * max(1.0, abs(a)), (le, lg)
+    assert _pdiff(pe, pg) < 2e-2
+
+
+def test_fp16_overflow_step_filtered_on_device():
+    """An overflowing step (inf gradients, replayed from a graph) leaves the
+    parameters and the G factors finite: the scaler skips the update and
+    K-FAC's device-side filter drops the non-finite G contribution."""
+    _, pg, sg, pre = _train_fp16(True, steps=14, overflow_at=12)   # step 12: a factor step
+    assert sg.replays > 0
+    assert all(torch.isfinite(p).all() for p in pg)
+    for l in pre.layers:
+        assert torch.isfinite(l.state['G']).all() and torch.isfinite(l.state['A']).all()
