@@ -45,6 +45,12 @@ class ReduceRecord(ctypes.Structure):
                 ('ws', c_vp), ('n', c_ll)]
 
 
+class CholRecord(ctypes.Structure):
+    """Mirror of csrc/chol.hip KfacCholRecord."""
+    _fields_ = [('F', ctypes.c_void_p), ('ldf', ctypes.c_longlong), ('out', ctypes.c_void_p),
+                ('ldo', ctypes.c_longlong), ('ws', ctypes.c_void_p), ('n', ctypes.c_longlong)]
+
+
 class DcRecord(ctypes.Structure):
     # csrc/eig_dc.hip KfacDcRecord
     _fields_ = [('d', c_vp), ('e', c_vp), ('dout', c_vp), ('Zout', c_vp), ('ldz', c_ll),
@@ -60,6 +66,9 @@ _SIGS = {
                       c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_vp, c_int,
                       c_int, c_vp, c_vp, c_vp],
     'kfac_syrk_splits': [c_int, c_ll, c_int, c_int],
+    'kfac_chol_inverse_batched': [c_vp, c_int, c_f, c_int, c_vp],
+    'kfac_chol_ws_bytes': [c_int],
+    'kfac_chol_info_offset': [c_int],
     'kfac_syrk_problem_set_part': [c_vp, c_vp],
     'kfac_syrk_problem_set_dscale': [c_vp, c_vp],
     'kfac_red_job_size': [],
@@ -119,6 +128,7 @@ _SIGS = {
 
 _RESTYPES = {'kfac_sytrd_ws_floats': c_ll, 'kfac_sytrd_forget': None, 'kfac_dc_ws_bytes': c_ll,
              'kfac_reduce_ws_floats': c_ll, 'kfac_syrk_splits': c_ll,
+             'kfac_chol_ws_bytes': c_ll, 'kfac_chol_info_offset': c_ll,
              'kfac_syrk_problem_set_part': None, 'kfac_syrk_problem_set_dscale': None}
 
 

@@ -542,16 +542,65 @@ def symeig_many(mats, clip=0.0, solver='auto'):
     return outs
 
 
+_CHOL_BUFS = {}
+
+
+def _chol_buffers(dev, n, b):
+    key = (str(dev), n, b)
+    bufs = _CHOL_BUFS.get(key)
+    if bufs is None:
+        wsb = int(_lib.lib().kfac_chol_ws_bytes(n))
+        bufs = dict(out=torch.empty(b, n, n, dtype=torch.float32, device=dev), wsb=wsb,
+                    ws=torch.zeros(b * wsb, dtype=torch.uint8, device=dev),
+                    info_off=int(_lib.lib().kfac_chol_info_offset(n)))
+        _CHOL_BUFS[key] = bufs
+    return bufs
+
+
 def inverse_many(mats, damping, check=True):
     """(F + damping I)^-1 for symmetric positive definite F (Cholesky), the
     reference's inverse path (kfac/layers/utils.py:76-96).
 
-    One batched potrf + potri per size class (ResNet-50: ~12 classes for 108
-    factors) instead of two library calls per matrix, and `cholesky_ex`: the
-    factorisation status of every class is checked with ONE host read at the
-    end instead of a device sync per matrix.  Results are views of the
-    per-class batch."""
+    GPU: every factor in ONE ragged launch sequence of the hand-written
+    batched Cholesky / triangular inverse / X^T X product (csrc/chol.hip,
+    damping fused into the first copy, a cached hipGraph); the factorisation
+    status of all factors is checked with ONE host read at the end.  Results
+    are views of persistent per-size-class buffers (callers copy them).
+    CPU: torch.linalg.cholesky_ex + cholesky_inverse per size class."""
     outs = [None] * len(mats)
+    if mats and _lib.use_native(mats[0]):
+        dev = mats[0].device
+        classes = {}
+        for i, A in enumerate(mats):
+            classes.setdefault(A.shape[0], []).append(i)
+        recs = (_lib.CholRecord * len(mats))()
+        infos = []
+        k = 0
+        keep = []
+        for n, idx in sorted(classes.items(), key=lambda kv: -kv[0]):
+            B = _chol_buffers(dev, n, len(idx))
+            for j, i in enumerate(idx):
+                F = mats[i].float().contiguous()
+                keep.append(F)
+                r = recs[k]
+                r.F, r.ldf = F.data_ptr(), F.stride(0)
+                r.out, r.ldo = B['out'][j].data_ptr(), n
+                r.ws, r.n = B['ws'].data_ptr() + j * B['wsb'], n
+                outs[i] = B['out'][j]
+                k += 1
+            infos.append(B['ws'].view(len(idx), B['wsb'])[:, B['info_off']:B['info_off'] + 4])
+        stream = _lib.stream(dev)
+        _lib.check(_lib.lib().kfac_chol_inverse_batched(recs, len(mats), float(damping), 1,
+                                                         stream), 'kfac_chol_inverse_batched')
+        cur = torch.cuda.current_stream(dev)
+        for F in keep:
+            F.record_stream(cur)
+        if check:
+            bad = torch.cat([i.contiguous().view(torch.int32).reshape(-1) for i in infos]).ne(0)
+            if bool(bad.any()):
+                raise torch.linalg.LinAlgError(
+                    'Cholesky of a damped factor failed (not positive definite)')
+        return outs
     groups = {}
     for i, A in enumerate(mats):
         groups.setdefault((A.shape[0], A.dtype, A.device), []).append(i)
