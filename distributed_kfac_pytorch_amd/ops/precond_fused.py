@@ -146,19 +146,25 @@ class _Operand(object):
 
 
 class _LayerBufs(object):
-    def __init__(self, layer, x3, device):
+    def __init__(self, layer, x3, device, inverse=False):
         self.layer = layer
         nG, nA = layer.grad_shape
         self.nG, self.nA = nG, nA
-        self.QG = _Operand(nG, nG, x3, device)
+        # inverse path (use_eigen_decomp=False): QGt holds G_inv and QA holds
+        # A_inv (both symmetric), V = (G_inv Grad) A_inv in two stages
         self.QGt = _Operand(nG, nG, x3, device)
         self.QA = _Operand(nA, nA, x3, device)
-        self.QAt = _Operand(nA, nA, x3, device)
         self.Gct = _Operand(nA, nG, x3, device)
         self.T1 = _Operand(nG, nA, x3, device)
+        self.prediv = layer.prediv_eigenvalues and not inverse
+        if inverse:
+            self.QG = self.QAt = self.T2t = self.T3 = None
+            self.Dt = None
+            return
+        self.QG = _Operand(nG, nG, x3, device)
+        self.QAt = _Operand(nA, nA, x3, device)
         self.T2t = _Operand(nA, nG, x3, device)
         self.T3 = _Operand(nG, nA, x3, device)
-        self.prediv = layer.prediv_eigenvalues
         self.Dt = torch.zeros(nA, nG, dtype=torch.float32, device=device) if self.prediv else None
 
 
@@ -172,7 +178,9 @@ class FusedPreconditioner(object):
         self.prec = PRECISIONS[precision]
         self.x3 = precision == 'bf16x3'
         self.device = self.layers[0].module.weight.device if self.layers else None
-        self.bufs = [_LayerBufs(l, self.x3, self.device) for l in self.layers]
+        # the damped-inverse path (K9): V = G_inv Grad A_inv, two grouped stages
+        self.inverse = bool(self.layers) and not self.layers[0].use_eigen_decomp
+        self.bufs = [_LayerBufs(l, self.x3, self.device, self.inverse) for l in self.layers]
         self._gather_sig = None
         self._stage_tables = None
         # superseded device tables stay alive: a captured graph may use them
@@ -186,13 +194,16 @@ class FusedPreconditioner(object):
         if self._stage_tables is not None:
             self._retired_tables.append(self._stage_tables)
         stages = []
-        for stage in range(4):
+        for stage in ((0, 3) if self.inverse else range(4)):
             probs = []
             for b in self.bufs:
                 st = b.layer.state
                 r = PGemmRec()
                 r.epi = EPI_STORE
-                if stage == 0:      # T1[g][a] = QGt . Gct
+                if stage == 3 and self.inverse:     # V[g][a] = T1 . A_inv (+ KL dot)
+                    A, B, C, M, N, K = b.T1, b.QA, None, b.nG, b.nA, b.nA
+                    r.epi = EPI_FINAL
+                elif stage == 0:    # T1[g][a] = QGt . Gct  (inverse path: G_inv . Gct)
                     A, B, C, M, N, K = b.QGt, b.Gct, b.T1, b.nG, b.nA, b.nG
                 elif stage == 1:    # T2t[a][g] = (QAt . T1) (.) Dt
                     A, B, C, M, N, K = b.QAt, b.T1, b.T2t, b.nA, b.nG, b.nA
@@ -240,7 +251,7 @@ class FusedPreconditioner(object):
         # launches (the count depends on the tile shapes), summed in a fixed
         # order (deterministic: every rank derives the same clip scale); the
         # result is slot 0.  A grown buffer retires the old one (graphs).
-        self._kl_slots = sum(tiles for _, _, _, tiles in stages[3])
+        self._kl_slots = sum(tiles for _, _, _, tiles in stages[-1])
         if self.kl_buf is None or self.kl_buf.numel() < 1 + self._kl_slots:
             if self.kl_buf is not None:
                 self._retired_tables.append(self.kl_buf)
@@ -267,6 +278,17 @@ class FusedPreconditioner(object):
         keep = []
         for b in self.bufs:
             st = b.layer.state
+            if self.inverse:
+                Ai, Gi = st['A_inv'], st['G_inv']
+                if Ai.dim() == 1:       # symmetry-aware comm keeps packed triangles
+                    from ..layers import utils as lutils
+                    Ai = lutils.fill_triu((b.nA, b.nA), Ai)
+                    Gi = lutils.fill_triu((b.nG, b.nG), Gi)
+                Ai, Gi = Ai.float().contiguous(), Gi.float().contiguous()
+                keep += [Ai, Gi]
+                add(jobs, Gi, b.QGt, False)
+                add(jobs, Ai, b.QA, False)
+                continue
             QA = st['QA'].float().contiguous()
             QG = st['QG'].float().contiguous()
             keep += [QA, QG]
@@ -351,10 +373,11 @@ class FusedPreconditioner(object):
         stream = _lib.stream(self.device)
         recs = self._gather_table()
         _lib.check(L.kfac_gather_grad(self.prec, recs, len(recs), stream), 'kfac_gather_grad')
+        final = len(self._stage_tables) - 1
         for i, launches in enumerate(self._stage_tables):
             slot = 1
             for tile, table, count, tiles in launches:
-                kl = _lib.c_vp(self.kl_buf.data_ptr() + 8 * slot) if (with_kl and i == 3) \
+                kl = _lib.c_vp(self.kl_buf.data_ptr() + 8 * slot) if (with_kl and i == final) \
                     else None
                 _lib.check(L.kfac_pgemm(self.prec, tile, _lib.ptr(table), count, tiles, kl,
                                         stream), 'kfac_pgemm')

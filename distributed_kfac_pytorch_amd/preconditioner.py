@@ -838,10 +838,10 @@ class KFAC(optim.Optimizer):
 
     def _build_fused(self):
         """The grouped MFMA preconditioning chain (ops/precond_fused.py) for
-        every layer this rank preconditions, on the GPU eigen path."""
+        every layer this rank preconditions, on the GPU: 4 grouped stages on
+        the eigen path, 2 (G_inv Grad A_inv) on the damped-inverse path."""
         self.fused = None
-        if not (self.fused_precondition and self.use_eigen_decomp and self.layers and
-                self.inv_dtype == torch.float32):
+        if not (self.fused_precondition and self.layers and self.inv_dtype == torch.float32):
             return
         if not self.layers[0].module.weight.is_cuda:
             return

@@ -39,8 +39,11 @@ def test_gpu_matches_cpu(channels_last, prediv):
 
 
 def test_gpu_inverse_path():
+    """use_eigen_decomp=False: hand-written batched Cholesky inverse
+    (csrc/chol.hip) and the 2-stage grouped pgemm chain G_inv Grad A_inv."""
     g_cpu, _, _ = _run('cpu', use_eigen_decomp=False)
-    g_gpu, _, _ = _run('cuda', use_eigen_decomp=False)
+    g_gpu, _, pre = _run('cuda', use_eigen_decomp=False)
+    assert pre.fused is not None and pre.fused.inverse and len(pre.fused._stage_tables) == 2
     for gs, cs in zip(g_gpu, g_cpu):
         for x, y in zip(gs, cs):
             assert (x.cpu() - y).norm() / max(y.norm(), 1e-12) < 2e-3
