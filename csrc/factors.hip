@@ -160,6 +160,13 @@ struct RedBatch {
 };
 static_assert(sizeof(RedBatch) <= 4096, "kernel arguments are limited to 4 KB");
 
+// Each workgroup takes 1024 elements (a float4 per thread) of one tile pair:
+// RED_WG = 16 workgroups per tile pair.  The split loop loads 8 partials at
+// a time (independent, in flight together) and adds them in order: the
+// summation order (contribution, split) is fixed, so the result is
+// deterministic.
+constexpr int RED_WG = (BT * BT) / 1024;
+
 __global__ __launch_bounds__(256) void tile_reduce_kernel(const RedBatch* __restrict__ batch) {
   const RedJob* t = batch->job;
   int lo = 0, hi = batch->count - 1;
@@ -169,20 +176,33 @@ __global__ __launch_bounds__(256) void tile_reduce_kernel(const RedBatch* __rest
     if (t[mid].block_begin <= b) lo = mid; else hi = mid - 1;
   }
   const RedJob& J = t[lo];
-  const int tile = b - J.block_begin;
+  const int loc = b - J.block_begin;
+  const int tile = loc / RED_WG, part = loc - tile * RED_WG;
   int tt = tile, ti = 0, rem = J.ntiles;
   while (tt >= rem) { tt -= rem; ++ti; --rem; }
   const int tj = ti + tt;
   const int tp = J.ntiles * (J.ntiles + 1) / 2;
-  for (int e = threadIdx.x; e < BT * BT; e += 256) {
-    const int row = ti * BT + e / BT, col = tj * BT + (e & (BT - 1));
-    float acc = 0.f;
-    for (int c = 0; c < J.ncontrib; ++c) {
-      const float* pc = J.part[c] + (long long)tile * (BT * BT) + e;
-      for (int sp = 0; sp < J.splits[c]; ++sp) acc += pc[(long long)sp * tp * (BT * BT)];
+  const int e = part * 1024 + threadIdx.x * 4;          // 4 consecutive elements of a row
+  const long long sstride = (long long)tp * (BT * BT) / 4;   // float4 stride between splits
+  fx4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < J.ncontrib; ++c) {
+    const AS1 fx4* pc = (const AS1 fx4*)(gptr(J.part[c]) + (long long)tile * (BT * BT) + e);
+    const int ns = J.splits[c];
+    int sp = 0;
+    for (; sp + 8 <= ns; sp += 8) {
+      fx4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = pc[(long long)(sp + u) * sstride];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
     }
-    if (row <= col && col < J.ncols) J.ws[(long long)row * J.ldw + col] = acc;
+    for (; sp < ns; ++sp) acc += pc[(long long)sp * sstride];
   }
+  const int row = ti * BT + e / BT, col0 = tj * BT + (e & (BT - 1));
+  AS1 float* w = gptr(J.ws) + (long long)row * J.ldw + col0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    if (row <= col0 + u && col0 + u < J.ncols) w[u] = acc[u];
 }
 
 // LANE_COLS = true when channels are the unit-stride dim (NHWC / Linear):
@@ -965,7 +985,7 @@ KFAC_API int kfac_tile_reduce(const void* host_jobs, int count, hipStream_t stre
       b.job[k] = t[base + k];
       if (b.job[k].ncontrib > MAX_CONTRIB) return -2;
       b.job[k].block_begin = blocks;
-      blocks += b.job[k].ntiles * (b.job[k].ntiles + 1) / 2;
+      blocks += RED_WG * (b.job[k].ntiles * (b.job[k].ntiles + 1) / 2);
     }
     if (blocks == 0) continue;
     int terr = 0;

@@ -113,7 +113,7 @@ def test_factor_ema(sdtype):
     sym = torch.triu(ws) + torch.triu(ws, 1).t()
     want = (0.95 * state.float() + 0.05 * sym)
     _lib.check(_lib.lib().kfac_factor_ema(_lib.DTYPE_CODE[sdtype], _lib.ptr(state), _lib.ptr(ws),
-                                          n, n, 0.95, 0, _lib.stream()), 'ema')
+                                          n, n, 0.95, 0, None, _lib.stream()), 'ema')
     tol = 1e-5 if sdtype == torch.float32 else 2e-2
     assert torch.allclose(state.float(), want, atol=tol, rtol=tol)
     assert torch.equal(state, state.t())
