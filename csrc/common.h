@@ -74,6 +74,13 @@ __device__ __forceinline__ T gld_if(const AS1 T* p, long long i, bool ok, T z) {
   const T v = p[ok ? i : 0];
   return ok ? v : z;
 }
+// 32-bit element offset: the load becomes `global_load v, v_off, s[base]` (one
+// offset VGPR instead of a 64-bit address pair); callers guarantee i < 2^32
+template <class T>
+__device__ __forceinline__ T gld_if32(const AS1 T* p, unsigned i, bool ok, T z) {
+  const T v = p[ok ? i : 0u];
+  return ok ? v : z;
+}
 
 // Wave sums on the VALU (no LDS round trips): DPP quad_perm / half-mirror /
 // mirror inside each 16-lane row, then the gfx950 permlane16/32 swaps across

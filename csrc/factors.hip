@@ -403,10 +403,15 @@ __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int 
   const uint16_t* x = (const uint16_t*)p.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  // loader role: operand (0 = A tile ti, 1 = B tile tj), row group, column chunk
+  // loader role: operand (0 = A tile ti, 1 = B tile tj), row group, column chunk.
+  // Row group fastest: the 8 lanes of one ds_write_b128 lane group store the
+  // same LDS rows at 8 different k offsets = 32 distinct banks.  (Column chunk
+  // fastest put them 8 LDS rows apart = 288 dwords = the same 4 banks: 8-way
+  // conflicts, 72 % of the kernel's LDS cycles, profiles/README.md.)  A wave's
+  // global loads still read 128 contiguous bytes per patch row.
   const int op = tid >> 7;
-  const int rg = (tid & 127) >> 4;      // rows rg*8 .. rg*8+7 of the k-step
-  const int cc = tid & 15;              // columns cc*8 .. cc*8+7 of the tile
+  const int rg = tid & 7;               // rows rg*8 .. rg*8+7 of the k-step
+  const int cc = (tid & 127) >> 3;      // columns cc*8 .. cc*8+7 of the tile
   const bool loader = !(diag && op == 1);
   const int gcol = (op ? tj : ti) * BT + cc * 8;
   // chunk kind: 0 = data, 1 = bias (first column of the chunk is the ones column), 2 = zero

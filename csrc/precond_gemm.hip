@@ -22,8 +22,8 @@
 //                f32 accumulation: ~1e-5 relative error on the preconditioned
 //                gradient (fp32 GEMMs: ~1e-6, plain bf16: ~5e-3), at ~5x the
 //                f32 MFMA rate.
-//   PREC_F32     operands fp32, exact v_mfma_f32_32x32x2_f32 (bitwise an fmaf
-//                chain), the reference's fp32 semantics.
+//   PREC_F32     operands fp32, exact v_mfma_f32_32x32x2_f32 (exact f32
+//                products, f32 accumulation), the reference's fp32 semantics.
 // Auxiliary launches: `gather_grad` builds Gct planes from the .grad tensors
 // (any memory layout, bias as the last K-FAC column), `split_copy` builds the
 // QA/QG/QAt/QGt planes and Dt after each inverse update.
@@ -52,6 +52,7 @@ __device__ __forceinline__ int find_problem(const PGemm* __restrict__ t, int cou
 }
 
 typedef unsigned u32x4n __attribute__((ext_vector_type(4)));   // AS1 loads
+typedef float fx2 __attribute__((ext_vector_type(2)));         // ds_read_b64 fragments
 
 __device__ __forceinline__ void split_bf16(float x, uint16_t& h, uint16_t& l) {
   h = f32_to_bf16_bits(x);
@@ -70,7 +71,8 @@ __device__ __forceinline__ void split_bf16(float x, uint16_t& h, uint16_t& l) {
 constexpr int TK = 32;
 
 // WPE: minimum waves per SIMD the register allocator must allow (1 = no
-// constraint).  WPE 6 fits three 8-wave workgroups per CU (80 VGPRs).
+// constraint).  WPE 2 caps VGPR + AGPR at 256: two 4-wave workgroups per CU,
+// one computing while the other waits at its k-step barrier.
 // DBUF: two LDS images -- the next k-step is stored into the idle image
 // right after the MFMAs, one barrier per k-step instead of two.
 template <int PREC, int BM, int BN, int WM, int WN, int WPE = 1, bool DBUF = false>
@@ -118,28 +120,41 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   constexpr int ESZ = X3 ? 2 : 4;
   // branch-free: rows past the problem read row m0 / n0 (in range) and are
   // zeroed by a select, so every load of a k-step issues back to back
+  // per-thread 32-bit byte offsets of its chunks (operands < 4 GiB, checked
+  // on the host); the k-step advances the uniform base pointer
   u32x4n ra[QA], rb[QB];
+  unsigned offa[QA], offb[QB];
+  bool oka[QA], okb[QB];
+#pragma unroll
+  for (int q = 0; q < QA; ++q) {
+    const int c = tid + NT * q;
+    const int row = (c % (BM * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
+    oka[q] = m0 + row < M;
+    offa[q] = ((unsigned)(oka[q] ? m0 + row : m0) * (unsigned)lda + kof) * ESZ;
+  }
+#pragma unroll
+  for (int q = 0; q < QB; ++q) {
+    const int c = tid + NT * q;
+    const int row = (c % (BN * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
+    okb[q] = n0 + row < N;
+    offb[q] = ((unsigned)(okb[q] ? n0 + row : n0) * (unsigned)ldb + kof) * ESZ;
+  }
   const u32x4n z4 = {0u, 0u, 0u, 0u};
   auto load = [&](int k0) {
+    const long long kb = (long long)k0 * ESZ;
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
-      const int c = tid + NT * q;
-      const int plane = c / (BM * CPR), row = (c % (BM * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
-      const int gm = m0 + row;
-      const bool ok = gm < M;
-      const AS1 unsigned char* base = plane ? Al : Ah;
-      const u32x4n v = *(const AS1 u32x4n*)(base + ((long long)(ok ? gm : m0) * lda + k0 + kof) * ESZ);
-      ra[q] = ok ? v : z4;
+      const int plane = (tid + NT * q) / (BM * CPR);
+      const AS1 unsigned char* base = (plane ? Al : Ah) + kb;
+      const u32x4n v = *(const AS1 u32x4n*)(base + offa[q]);
+      ra[q] = oka[q] ? v : z4;
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
-      const int c = tid + NT * q;
-      const int plane = c / (BN * CPR), row = (c % (BN * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
-      const int gn = n0 + row;
-      const bool ok = gn < N;
-      const AS1 unsigned char* base = plane ? Bl : Bh;
-      const u32x4n v = *(const AS1 u32x4n*)(base + ((long long)(ok ? gn : n0) * ldb + k0 + kof) * ESZ);
-      rb[q] = ok ? v : z4;
+      const int plane = (tid + NT * q) / (BN * CPR);
+      const AS1 unsigned char* base = (plane ? Bl : Bh) + kb;
+      const u32x4n v = *(const AS1 u32x4n*)(base + offb[q]);
+      rb[q] = okb[q] ? v : z4;
     }
   };
   // LDS image: [A hi | A lo | B hi | B lo] rows of LDB16 bf16 (X3) or [A | B] rows of LDF32 f32
@@ -149,14 +164,14 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
       const int c = tid + NT * q;
       const int plane = c / (BM * CPR), row = (c % (BM * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
       if (X3) *(u32x4n*)((uint16_t*)img + (plane * BM + row) * LDB16 + kof) = ra[q];
-      else *(u32x4n*)((float*)img + row * LDF32 + kof) = ra[q];
+      else *(u32x4n*)((float*)img + row * LDF32 + kof) = (row & 16) ? ra[q].zwxy : ra[q];
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
       const int c = tid + NT * q;
       const int plane = c / (BN * CPR), row = (c % (BN * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
       if (X3) *(u32x4n*)((uint16_t*)img + (2 * BM + plane * BN + row) * LDB16 + kof) = rb[q];
-      else *(u32x4n*)((float*)img + (BM + row) * LDF32 + kof) = rb[q];
+      else *(u32x4n*)((float*)img + (BM + row) * LDF32 + kof) = (row & 16) ? rb[q].zwxy : rb[q];
     }
   };
 
@@ -211,20 +226,34 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
         }
       }
     } else {
+      // Fragments are read 8 bytes at a time: lane half lh covers k in
+      // [16 lh, 16 lh + 16), pair m feeds two MFMAs (k = 16 lh + 2m and +1).
+      // Rows with bit 4 set hold each 16-byte chunk with its halves swapped
+      // (store above), so lanes lr and lr + 16 -- same bank with the 36-float
+      // row stride -- read disjoint banks: conflict-free ds_read_b64 (the
+      // one-float-per-lane reads of the plain k mapping were 4-way conflicted,
+      // SQ_LDS_BANK_CONFLICT = 66 % of LDS cycles, profiles/README.md)
       const float* sA = (const float*)cur;
       const float* sB = sA + BM * LDF32;
+      const int swz = (lr & 16) >> 3;
 #pragma unroll
-      for (int kk = 0; kk < TK / 2; ++kk) {
-        float b[NJ];
+      for (int m = 0; m < TK / 4; ++m) {
+        const int kof = (16 * lh + 2 * m) ^ swz;
+        fx2 b[NJ], a[MI];
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) b[j] = sB[(brow0 + j * 32 + lr) * LDF32 + kk * 2 + lh];
+        for (int j = 0; j < NJ; ++j) b[j] = *(const fx2*)(sB + (brow0 + j * 32 + lr) * LDF32 + kof);
 #pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          const float a = sA[(arow0 + i * 32 + lr) * LDF32 + kk * 2 + lh];
+        for (int i = 0; i < MI; ++i) a[i] = *(const fx2*)(sA + (arow0 + i * 32 + lr) * LDF32 + kof);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
           for (int j = 0; j < NJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b[j], acc[i][j], 0, 0, 0);
-        }
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
       }
     }
     if constexpr (DBUF) {
@@ -247,7 +276,10 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   const AS1 float* const Gf = (const AS1 float*)P.g_hi;
   const AS1 uint16_t* const Gh = (const AS1 uint16_t*)P.g_hi;
   const AS1 uint16_t* const Gl = (const AS1 uint16_t*)P.g_lo;
-  const long long ldc = P.ldc, ldd = P.ldd, ldg = P.ldg;
+  // 32-bit element offsets (every operand < 2^32 elements, checked on the
+  // host): one offset VGPR per access instead of a 64-bit address pair keeps
+  // the epilogue from setting the kernel's register budget
+  const unsigned ldc = (unsigned)P.ldc, ldd = (unsigned)P.ldd, ldg = (unsigned)P.ldg;
   const float damping = P.damping;
   float kl_part = 0.f;
   // one straight-line loop nest per epilogue kind (a run-time kind test per
@@ -267,20 +299,20 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
           aux[r] = 0.f;
           aux2[r] = 0.f;
           if constexpr (E == EPI_HADAMARD) {
-            aux[r] = gld_if(Dm, (long long)m * ldd + n, ok, 0.f);
+            aux[r] = gld_if32(Dm, (unsigned)m * ldd + n, ok, 0.f);
           } else if constexpr (E == EPI_HADAMARD_VEC) {
-            aux[r] = gld_if(Vm, m, ok, 0.f);
-            aux2[r] = gld_if(Vn, n, ok, 0.f);
+            aux[r] = gld_if32(Vm, (unsigned)m, ok, 0.f);
+            aux2[r] = gld_if32(Vn, (unsigned)n, ok, 0.f);
           } else if constexpr (E == EPI_FINAL) {
-            const long long go = (long long)n * ldg + m;
+            const unsigned go = (unsigned)n * ldg + m;
             if constexpr (X3) {
-              aux[r] = bf16_bits_to_f32(gld_if(Gh, go, ok, (uint16_t)0));
-              aux2[r] = bf16_bits_to_f32(gld_if(Gl, go, ok, (uint16_t)0));
+              aux[r] = bf16_bits_to_f32(gld_if32(Gh, go, ok, (uint16_t)0));
+              aux2[r] = bf16_bits_to_f32(gld_if32(Gl, go, ok, (uint16_t)0));
             } else {
-              aux[r] = gld_if(Gf, go, ok, 0.f);
+              aux[r] = gld_if32(Gf, go, ok, 0.f);
             }
           } else if constexpr (E == EPI_SUB) {
-            aux[r] = gld_if((const AS1 float*)Cf, (long long)m * ldc + n, ok, 0.f);
+            aux[r] = gld_if32((const AS1 float*)Cf, (unsigned)m * ldc + n, ok, 0.f);
           }
         }
 #pragma unroll
@@ -288,7 +320,7 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
           const int m = m0 + arow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
           if (m >= M || n >= N) continue;
           float v = acc[i][j][r];
-          const long long o = (long long)m * ldc + n;
+          const unsigned o = (unsigned)m * ldc + n;
           if constexpr (E == EPI_HADAMARD) v *= aux[r];
           if constexpr (E == EPI_HADAMARD_VEC) v /= (aux2[r] * aux[r] + damping);
           if constexpr (E == EPI_FINAL) {
@@ -459,8 +491,10 @@ KFAC_API int kfac_pgemm_record_size() { return (int)sizeof(PGemm); }
 KFAC_API int kfac_gather_record_size() { return (int)sizeof(GatherJob); }
 KFAC_API int kfac_split_record_size() { return (int)sizeof(SplitJob); }
 
-// tile: 0 = 128 x 128 (4 waves), 1 = 256 x 256 (8 waves), 2 = 64 x 64 (4 waves),
-// 3 = 128 x 128 (8 waves), 4 = 128 x 64 (4 waves);
+// tile: 0 = 128 x 128 (4 waves, registers capped for 2 waves per SIMD: 2.83 vs
+// 3.03 ms fp32 chain, 1.49 vs 1.56 ms bf16x3 against the uncapped 272-register
+// build = tile 8, profiles/r2_pgemm_occupancy.log), 1 = 256 x 256 (8 waves),
+// 2 = 64 x 64 (4 waves), 3 = 128 x 128 (8 waves), 4 = 128 x 64 (4 waves);
 // the table (ops/precond_fused.py) holds the problems of that tile class.
 KFAC_API int kfac_pgemm(int prec, int tile, const void* dev_table, int count, int total_tiles,
                         double* kl, hipStream_t stream) {
@@ -476,11 +510,11 @@ KFAC_API int kfac_pgemm(int prec, int tile, const void* dev_table, int count, in
     case 5: hipLaunchKernelGGL((pgemm_kernel<P, 128, 128, 4, 4>), g, dim3(1024), 0, stream, t, count, kl); break; \
     case 6: hipLaunchKernelGGL((pgemm_kernel<P, 256, 128, 4, 2>), g, dim3(512), 0, stream, t, count, kl); break; \
     case 7: hipLaunchKernelGGL((pgemm_kernel<P, 128, 256, 2, 4>), g, dim3(512), 0, stream, t, count, kl); break; \
-    case 8: hipLaunchKernelGGL((pgemm_kernel<P, 128, 128, 4, 2, 6>), g, dim3(512), 0, stream, t, count, kl); break; \
-    case 9: hipLaunchKernelGGL((pgemm_kernel<P, 128, 128, 4, 2, 5>), g, dim3(512), 0, stream, t, count, kl); break; \
+    case 8: hipLaunchKernelGGL((pgemm_kernel<P, 128, 128, 2, 2, 1>), g, dim3(256), 0, stream, t, count, kl); break; \
+    case 9: hipLaunchKernelGGL((pgemm_kernel<P, 128, 128, 2, 2, 2, true>), g, dim3(256), 0, stream, t, count, kl); break; \
     case 10: hipLaunchKernelGGL((pgemm_kernel<P, 128, 128, 4, 2, 1, true>), g, dim3(512), 0, stream, t, count, kl); break; \
     case 11: hipLaunchKernelGGL((pgemm_kernel<P, 128, 128, 4, 4, 1, true>), g, dim3(1024), 0, stream, t, count, kl); break; \
-    default: hipLaunchKernelGGL((pgemm_kernel<P, 128, 128, 2, 2>), g, dim3(256), 0, stream, t, count, kl); break; \
+    default: hipLaunchKernelGGL((pgemm_kernel<P, 128, 128, 2, 2, 2>), g, dim3(256), 0, stream, t, count, kl); break; \
   }
   if (prec == PREC_BF16X3) {
     KFAC_PGEMM_LAUNCH(PREC_BF16X3)

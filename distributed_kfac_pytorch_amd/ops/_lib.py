@@ -186,6 +186,18 @@ def check(err, name):
         raise RuntimeError('{} failed with HIP error {}'.format(name, err))
 
 
+# The grouped MFMA GEMM (csrc/precond_gemm.hip) addresses every operand with
+# 32-bit offsets: a factor dimension n (padded row length <= n + 63) must keep
+# n x ld x 4 bytes below 4 GiB.
+PGEMM_MAX_N = 32704
+
+
+def check_pgemm_extent(n, what='factor'):
+    if n > PGEMM_MAX_N:
+        raise ValueError('{} dimension {} exceeds the native kernels\' limit of {} '
+                         '(32-bit operand offsets)'.format(what, n, PGEMM_MAX_N))
+
+
 # Replace captured memset nodes by fill kernels (csrc/graph_fix.hip); 0 = keep
 # them (A/B runs of the ROCm 7.2 memset-node issue)
 FIX_GRAPH_MEMSETS = os.environ.get('KFAC_GRAPH_FIX_MEMSETS', '1') != '0'

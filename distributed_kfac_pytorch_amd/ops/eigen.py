@@ -512,6 +512,7 @@ def symeig_many(mats, clip=0.0, solver='auto'):
                 d = torch.clamp(d, min=clip)
             outs.append((Q, d))
         return outs
+    _lib.check_pgemm_extent(max(A.shape[0] for A in mats))
     # fused default: EVERY factor rides the ragged launch sequence (a small
     # factor's reduction columns run alongside the big ones', its divide and
     # conquer is one or two levels); the batched LDS Jacobi is the small-n
@@ -569,6 +570,7 @@ def inverse_many(mats, damping, check=True):
     CPU: torch.linalg.cholesky_ex + cholesky_inverse per size class."""
     outs = [None] * len(mats)
     if mats and _lib.use_native(mats[0]):
+        _lib.check_pgemm_extent(max(A.shape[0] for A in mats))
         dev = mats[0].device
         classes = {}
         for i, A in enumerate(mats):

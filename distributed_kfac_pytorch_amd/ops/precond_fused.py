@@ -181,6 +181,8 @@ class FusedPreconditioner(object):
         # the damped-inverse path (K9): V = G_inv Grad A_inv, two grouped stages
         self.inverse = bool(self.layers) and not self.layers[0].use_eigen_decomp
         self.bufs = [_LayerBufs(l, self.x3, self.device, self.inverse) for l in self.layers]
+        for b in self.bufs:
+            _lib.check_pgemm_extent(max(b.nG, b.nA), 'layer')
         self._gather_sig = None
         self._stage_tables = None
         # superseded device tables stay alive: a captured graph may use them
