@@ -9,7 +9,7 @@
 // no library call.  The algorithm is modelled step by step (same buffers and
 // index conventions) in scripts/models/dc_model.py:
 //
-//   leaf     one workgroup per leaf (<= 64 rows): the torn leaf block as a
+//   leaf     one workgroup per leaf (<= LEAF = 32 rows): the torn leaf block as a
 //            dense matrix in LDS, cyclic parallel Jacobi in fp64, ascending
 //   prep     one workgroup per merge: z from the children's boundary columns,
 //            the 4 ascending runs of the two children merged by rank (binary
@@ -47,7 +47,10 @@
 
 namespace {
 
-constexpr int LEAF = 64;
+// leaf rows: the fp64 cyclic Jacobi leaf costs ~rounds x sweeps LDS barriers
+// (rows - 1 rounds per sweep); 32-row leaves halve the rounds for one more,
+// cheap, merge level (ResNet-50 inverse update 159 -> 157 ms)
+constexpr int LEAF = 32;
 constexpr int PADK = 36;          // zero columns past k in U / ZpT rows (GEMM k-steps)
 constexpr int LDS_M_MAX = 4800;   // merges up to this size scan in LDS (32 B per row)
 constexpr double EPS32 = 5.9604644775390625e-08;   // 2^-24 (LAPACK slamch 'E')

@@ -10,8 +10,11 @@ compiler):
 
   'plain'   no factor update, no inverse update       -> replayed graph(s)
   'factor'  factor update (hooks + SYRK + EMA)         -> replayed graph(s)
-  'eager'   inverse-update steps (rocSOLVER D&C with host-side work, eigendata
-            broadcast) and the very first steps        -> run eagerly
+  'eager'   inverse-update steps (eigensolver launch sequences, eigendata
+            broadcast) and the very first steps        -> the update runs
+            eagerly; once the factor-step forward/backward graphs exist an
+            inverse step replays them (it is a factor step too) and only
+            the update is eager
 
 Two modes:
   single-segment  `step_fn` does everything (one process): one graph per kind.
@@ -92,6 +95,8 @@ class GraphedTrainStep(object):
         self.pre = preconditioner
         # 'force' phases the update even when it issues no collective (tests)
         self.phased_update = phased_update
+        # inverse-update steps replay the factor-step forward/backward graph(s)
+        self.graph_inverse_fb = True
         if preconditioner is not None and enabled:
             # the whole step is graphed: KFAC's own precondition-tail graph
             # is redundant
@@ -170,8 +175,43 @@ class GraphedTrainStep(object):
         return kind == 'plain' and pre.comm_method == CommMethod.COMM_OPT
 
     # ------------------------------------------------------------ execution
+    def _inverse_fb_graphed(self):
+        """An inverse-update step is also a factor step: its forward/backward
+        (factor SYRK + EMA inside the captured hooks) can replay the 'factor'
+        fb graph(s); only the update (eigensolves, eigendata distribution,
+        preconditioning, optimizer) then runs eagerly.  Needs every factor fb
+        segment captured already, workers assigned and no lagged solve due."""
+        pre = self.pre
+        if not (self.graph_inverse_fb and self.segmented and pre is not None
+                and pre.workers_assigned):
+            return False
+        p = pre.param_groups[0]
+        if p['step'] % p['factor_update_freq'] != 0:
+            return False
+        if getattr(pre, 'inverse_apply_due', None) is not None and pre.inverse_apply_due():
+            return False
+        return all(self._key('fb' if i == 0 else 'fb%d' % i, 'factor') in self.graphs
+                   for i in range(len(self.fbs)))
+
     def __call__(self):
         kind = self._kind()
+        if self.enabled and kind == 'eager' and self._inverse_fb_graphed():
+            self.eager_steps += 1
+            loss = None
+            for i, (fb, cm) in enumerate(zip(self.fbs, self.comms)):
+                out = self._run_segment('fb' if i == 0 else 'fb%d' % i, 'factor', fb,
+                                        advances=False)
+                if i == 0:
+                    loss = out
+                if cm is not None:
+                    cm()
+            cur = torch.cuda.current_stream()
+            self.side.wait_stream(cur)
+            with torch.cuda.stream(self.side):
+                self.update()
+            cur.wait_stream(self.side)
+            torch.cuda.synchronize()
+            return loss
         if not self.enabled or kind == 'eager':
             self.eager_steps += 1
             out = self._eager()

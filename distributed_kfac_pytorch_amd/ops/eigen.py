@@ -318,18 +318,50 @@ def _large_fused(mats, clip, stream, use_graph=True):
     group (_fused_groups) the fused one-launch-per-column reduction over all
     its matrices (csrc/eig_reduce.hip), the batched divide and conquer over
     all its matrices (csrc/eig_dc.hip), then the compact-WY back-
-    transformation per size class (csrc/eig_library.hip); the second group
+    transformation per size class (csrc/eig_library.hip); every further group
     on a side stream.  No library solver, no host round trip; each stage is
-    a cached hipGraph."""
+    a cached hipGraph.
+
+    The side groups are ENQUEUED from worker threads: a reduction graph holds
+    one node per column (9358 for the 4608 batch), more packets than a HW
+    queue holds, so hipGraphLaunch blocks its host thread until the GPU has
+    drained most of it.  Issued from one thread, the second group only
+    reached its stream when the first group was nearly done (kernel trace:
+    the two reductions ran back to back, 109 + 62 ms); from its own thread
+    it is enqueued at once and the chains overlap."""
     dev = mats[0].device
     groups = _fused_groups(mats)
     outs = [None] * len(mats)
     streams = [stream] + _side_streams(dev, len(groups) - 1)
     for s in streams[1:]:
         s.wait_stream(stream)
-    for slot, (g, st) in enumerate(zip(groups, streams)):
+
+    def run(slot):
+        g, st = groups[slot], streams[slot]
         for i, r in zip(g, _fused_group([mats[i] for i in g], clip, st, use_graph, slot)):
             outs[i] = r
+
+    key = (str(dev), use_graph, tuple(tuple(mats[i].shape[0] for i in g) for g in groups))
+    if len(groups) > 1 and FUSED_THREADS and key in _FUSED_PLANNED:
+        pool = _thread_pool(len(groups) - 1)
+        didx = dev.index if dev.index is not None else torch.cuda.current_device()
+
+        def side(slot):
+            torch.cuda.set_device(didx)
+            run(slot)
+        futs = [pool.submit(side, slot) for slot in range(1, len(groups))]
+        try:
+            run(0)
+        finally:
+            for f in futs:
+                f.result()     # re-raises a worker's error
+    else:
+        # first call of a group layout: plans are built and captured (on
+        # private capture streams), serially
+        for slot in range(len(groups)):
+            run(slot)
+        _FUSED_PLANNED.add(key)
+    del _INFOS[:-256]
     for g, st in zip(groups[1:], streams[1:]):
         stream.wait_stream(st)
         for i in g:
@@ -337,6 +369,18 @@ def _large_fused(mats, clip, stream, use_graph=True):
             outs[i][0].record_stream(stream)
             outs[i][1].record_stream(stream)
     return outs
+
+
+FUSED_THREADS = bool(int(os.environ.get('KFAC_EIG_FUSED_THREADS', '1')))
+_FUSED_PLANNED = set()
+_POOL = [None]
+
+
+def _thread_pool(k):
+    from concurrent.futures import ThreadPoolExecutor
+    if _POOL[0] is None or _POOL[0]._max_workers < k:
+        _POOL[0] = ThreadPoolExecutor(max_workers=max(k, 3), thread_name_prefix='kfac-eig')
+    return _POOL[0]
 
 
 def _fused_group(mats, clip, stream, use_graph, slot=0):
@@ -385,7 +429,6 @@ def _fused_group(mats, clip, stream, use_graph, slot=0):
                 D.clamp_(min=clip)
             for i, m in enumerate(idx):
                 outs[m] = (Q[i], D[i])
-        del _INFOS[:-256]
     return outs
 
 

@@ -45,17 +45,22 @@ def main():
                 ('tri1000', {'TRIDIAG_MIN_N': 1000}), ('tri500', {'TRIDIAG_MIN_N': 500}),
                 ('tri240', {'TRIDIAG_MIN_N': 240}), ('tri193', {'TRIDIAG_MIN_N': 193}),
                 ('stedc', {'SOLVER': 'stedc'}), ('stedc_tri193', {'SOLVER': 'stedc', 'TRIDIAG_MIN_N': 193}),
-                ('w2', {'W': 2}), ('w1', {'W': 1})]
+                ('w2', {'W': 2}), ('w1', {'W': 1}),
+                ('nothreads', {'TH': False}), ('fs1', {'FS': 1}), ('fs3', {'FS': 3}),
+                ('fs4', {'FS': 4})]
     if len(sys.argv) > 1:
         variants = [v for v in variants if v[0] in sys.argv[1:]]
     res = {}
     base = dict(SPLIT_N=eigen.SPLIT_N, TRIDIAG_MIN_N=eigen.TRIDIAG_MIN_N,
-                SOLVER=eigen.TRIDIAG_SOLVER, LARGE=eigen.LARGE_PATH)
+                SOLVER=eigen.TRIDIAG_SOLVER, LARGE=eigen.LARGE_PATH,
+                FS=eigen.FUSED_STREAMS, TH=eigen.FUSED_THREADS)
     for name, cfg in variants:
         eigen.LARGE_PATH = cfg.get('LARGE', base['LARGE'])
         eigen.TRIDIAG_SOLVER = cfg.get('SOLVER', base['SOLVER'])
         eigen.SPLIT_N = cfg.get('SPLIT_N', base['SPLIT_N'])
         eigen.TRIDIAG_MIN_N = cfg.get('TRIDIAG_MIN_N', base['TRIDIAG_MIN_N'])
+        eigen.FUSED_STREAMS = cfg.get('FS', base['FS'])
+        eigen.FUSED_THREADS = cfg.get('TH', base['TH'])
         if 'W' in cfg:
             os.environ['KFAC_EIGH_WORKERS'] = str(cfg['W'])
         else:
