@@ -112,7 +112,7 @@ def step_kind(pre):
 
 
 def time_sgd_only(args, model, opt, pre, forward_backward, grad_sync, use_graphs, device,
-                  communicate=None):
+                  communicate=None, stream=None):
     """The same training step without K-FAC (hooks removed, plain SGD update),
     timed over the same number of steps: the baseline for kfac_step_ms."""
     pre.remove_hooks()
@@ -123,13 +123,15 @@ def time_sgd_only(args, model, opt, pre, forward_backward, grad_sync, use_graphs
     if grad_sync is not None:
         step = graphs.GraphedTrainStep(None, None, [opt], enabled=use_graphs,
                                        forward_backward=forward_backward,
-                                       communicate=communicate or grad_sync, update=update)
+                                       communicate=communicate or grad_sync, update=update,
+                                       stream=stream)
     else:
         def train_step():
             loss = forward_backward()
             update()
             return loss
-        step = graphs.GraphedTrainStep(train_step, None, [opt], enabled=use_graphs)
+        step = graphs.GraphedTrainStep(train_step, None, [opt], enabled=use_graphs,
+                                       stream=stream)
     for _ in range(3):
         step()
     step.prepare()
@@ -276,8 +278,11 @@ def main():
     phases = pre.timer.summary() if (pre is not None and args.profile_phases) else None
     sgd_ms = None
     if pre is not None and args.sgd_delta:
+        # same capture stream as the K-FAC run: the model's AccumulateGrad
+        # nodes live on it (a new stream makes every backward sync across)
         sgd_ms = time_sgd_only(args, model, opt, pre, fb_segments, grad_sync, use_graphs,
-                               device, communicate=comm_segments)
+                               device, communicate=comm_segments,
+                               stream=getattr(step, 'side', None))
     if rank == 0:
         rec = {
             'metric': METRIC if pre is not None else 'images/sec (whole node) ResNet-50 SGD-only',

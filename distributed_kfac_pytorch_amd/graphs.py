@@ -78,7 +78,8 @@ def _world_size():
 
 class GraphedTrainStep(object):
     def __init__(self, step_fn=None, preconditioner=None, optimizers=(), warmup=2, enabled=True,
-                 forward_backward=None, communicate=None, update=None, phased_update=False):
+                 forward_backward=None, communicate=None, update=None, phased_update=False,
+                 stream=None):
         if step_fn is None and (forward_backward is None or update is None):
             raise ValueError('give step_fn, or forward_backward and update')
         self.step_fn = step_fn
@@ -128,7 +129,8 @@ class GraphedTrainStep(object):
         self.eager_steps = 0
         # warm-up and capture share one side stream, so the autograd
         # AccumulateGrad nodes created in warm-up live on the capture stream
-        self.side = torch.cuda.Stream() if self.enabled else None
+        # (`stream`: reuse another GraphedTrainStep's, for the same model)
+        self.side = (stream or torch.cuda.Stream()) if self.enabled else None
 
     # ------------------------------------------------------------ schedule
     def _kind(self):
