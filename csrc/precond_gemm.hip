@@ -24,6 +24,13 @@
 //                f32 MFMA rate.
 //   PREC_F32     operands fp32, exact v_mfma_f32_32x32x2_f32 (exact f32
 //                products, f32 accumulation), the reference's fp32 semantics.
+//   PREC_BF16X6  operands as three bf16 planes (hi, mid, lo: 24 mantissa bits,
+//                the fp32 significand), six bf16 MFMAs per product (all terms
+//                above 2^-24 relative: lo.hi + hi.lo + mid.mid + mid.hi +
+//                hi.mid + hi.hi), f32 accumulation: fp32-level error at the
+//                bf16 MFMA rate.  The three planes of an operand are one
+//                allocation (plane stride = lo - hi), so records keep two
+//                pointers per operand.
 // Auxiliary launches: `gather_grad` builds Gct planes from the .grad tensors
 // (any memory layout, bias as the last K-FAC column), `split_copy` builds the
 // QA/QG/QAt/QGt planes and Dt after each inverse update.
@@ -58,6 +65,33 @@ __device__ __forceinline__ void split_bf16(float x, uint16_t& h, uint16_t& l) {
   h = f32_to_bf16_bits(x);
   l = f32_to_bf16_bits(x - bf16_bits_to_f32(h));
 }
+// x = hi + mid + lo to the fp32 significand (each remainder is exact in f32)
+__device__ __forceinline__ void split_bf16_3(float x, uint16_t& h, uint16_t& m, uint16_t& l) {
+  h = f32_to_bf16_bits(x);
+  const float r = x - bf16_bits_to_f32(h);
+  m = f32_to_bf16_bits(r);
+  l = f32_to_bf16_bits(r - bf16_bits_to_f32(m));
+}
+// store a value as the planes of precision PREC at element o of (hi, lo)
+template <int PREC>
+__device__ __forceinline__ void store_planes(void* hi, void* lo, long long o, float v) {
+  if (PREC == PREC_BF16X3) {
+    uint16_t h, l;
+    split_bf16(v, h, l);
+    ((uint16_t*)hi)[o] = h;
+    ((uint16_t*)lo)[o] = l;
+  } else if (PREC == PREC_BF16X6) {
+    uint16_t h, m, l;
+    split_bf16_3(v, h, m, l);
+    uint16_t* H = (uint16_t*)hi;
+    uint16_t* M = (uint16_t*)lo;
+    H[o] = h;
+    M[o] = m;
+    (M + (M - H))[o] = l;
+  } else {
+    ((float*)hi)[o] = v;
+  }
+}
 
 // Tile geometry: BM x BN output tile per workgroup of WM x WN waves (each
 // wave owns a (BM/WM) x (BN/WN) sub-tile of 32x32 MFMA tiles), TK = 32 deep
@@ -78,13 +112,15 @@ constexpr int TK = 32;
 template <int PREC, int BM, int BN, int WM, int WN, int WPE = 1, bool DBUF = false>
 __global__ __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(WPE)))
 void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict__ kl) {
-  constexpr bool X3 = (PREC == PREC_BF16X3);
+  constexpr bool X3 = (PREC == PREC_BF16X3), X6 = (PREC == PREC_BF16X6);
+  constexpr bool SPL = X3 || X6;                  // split-bf16 planes
   constexpr int NT = 64 * WM * WN;                // threads
   constexpr int MI = BM / WM / 32, NJ = BN / WN / 32;
   constexpr int LDB16 = TK + 8;   // 80-byte rows: conflict-free ds_read_b128 (guide: LDS banking)
   constexpr int LDF32 = TK + 4;   // 16-byte aligned chunk writes
   // one LDS array (guide: a second __shared__ object can de-pipeline loads)
-  constexpr int LDS_BYTES = X3 ? (2 * (BM + BN) * LDB16 * 2) : ((BM + BN) * LDF32 * 4);
+  constexpr int PL = X6 ? 3 : (X3 ? 2 : 1);       // planes
+  constexpr int LDS_BYTES = SPL ? (PL * (BM + BN) * LDB16 * 2) : ((BM + BN) * LDF32 * 4);
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES * (DBUF ? 2 : 1)];
 
   const int pi = find_problem(table, count, blockIdx.x);
@@ -112,12 +148,19 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
 
   // ---- loader: 16-byte chunks.  bf16 planes: per operand 2 planes x rows x 4
   // chunks (8 elements); f32: rows x 8 chunks (4 elements)
-  constexpr int CPR = X3 ? TK / 8 : TK / 4;       // chunks per row and plane
-  constexpr int PL = X3 ? 2 : 1;                  // planes
+  constexpr int CPR = SPL ? TK / 8 : TK / 4;      // chunks per row and plane
   constexpr int CA = PL * BM * CPR, CB = PL * BN * CPR;
   constexpr int QA = CA / NT, QB = CB / NT;
   static_assert(CA % NT == 0 && CB % NT == 0, "loader split");
-  constexpr int ESZ = X3 ? 2 : 4;
+  // a chunk round stays in one plane: the plane index is a compile-time
+  // constant (a run-time one turns the 3-way pointer select into a scratch
+  // lookup table)
+  constexpr bool PLANE_CT = (BM * CPR) % NT == 0 && (BN * CPR) % NT == 0;
+  static_assert(!X6 || PLANE_CT, "3-plane loader needs whole chunk rounds per plane");
+  constexpr int ESZ = SPL ? 2 : 4;
+  // third plane (X6): one plane stride past the second
+  const AS1 unsigned char* const A2 = Al + (Al - Ah);
+  const AS1 unsigned char* const B2 = Bl + (Bl - Bh);
   // branch-free: rows past the problem read row m0 / n0 (in range) and are
   // zeroed by a select, so every load of a k-step issues back to back
   // per-thread 32-bit byte offsets of its chunks (operands < 4 GiB, checked
@@ -144,33 +187,35 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
     const long long kb = (long long)k0 * ESZ;
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
-      const int plane = (tid + NT * q) / (BM * CPR);
-      const AS1 unsigned char* base = (plane ? Al : Ah) + kb;
+      const int plane = PLANE_CT ? NT * q / (BM * CPR) : (tid + NT * q) / (BM * CPR);
+      const AS1 unsigned char* base = (X6 ? (plane == 0 ? Ah : (plane == 1 ? Al : A2))
+                                          : (plane ? Al : Ah)) + kb;
       const u32x4n v = *(const AS1 u32x4n*)(base + offa[q]);
       ra[q] = oka[q] ? v : z4;
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
-      const int plane = (tid + NT * q) / (BN * CPR);
-      const AS1 unsigned char* base = (plane ? Bl : Bh) + kb;
+      const int plane = PLANE_CT ? NT * q / (BN * CPR) : (tid + NT * q) / (BN * CPR);
+      const AS1 unsigned char* base = (X6 ? (plane == 0 ? Bh : (plane == 1 ? Bl : B2))
+                                          : (plane ? Bl : Bh)) + kb;
       const u32x4n v = *(const AS1 u32x4n*)(base + offb[q]);
       rb[q] = okb[q] ? v : z4;
     }
   };
-  // LDS image: [A hi | A lo | B hi | B lo] rows of LDB16 bf16 (X3) or [A | B] rows of LDF32 f32
+  // LDS image: [A planes | B planes] rows of LDB16 bf16 (X3 / X6) or [A | B] rows of LDF32 f32
   auto store = [&](unsigned char* img) {
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
       const int c = tid + NT * q;
       const int plane = c / (BM * CPR), row = (c % (BM * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
-      if (X3) *(u32x4n*)((uint16_t*)img + (plane * BM + row) * LDB16 + kof) = ra[q];
+      if (SPL) *(u32x4n*)((uint16_t*)img + (plane * BM + row) * LDB16 + kof) = ra[q];
       else *(u32x4n*)((float*)img + row * LDF32 + kof) = (row & 16) ? ra[q].zwxy : ra[q];
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
       const int c = tid + NT * q;
       const int plane = c / (BN * CPR), row = (c % (BN * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
-      if (X3) *(u32x4n*)((uint16_t*)img + (2 * BM + plane * BN + row) * LDB16 + kof) = rb[q];
+      if (SPL) *(u32x4n*)((uint16_t*)img + (PL * BM + plane * BN + row) * LDB16 + kof) = rb[q];
       else *(u32x4n*)((float*)img + (BM + row) * LDF32 + kof) = (row & 16) ? rb[q].zwxy : rb[q];
     }
   };
@@ -225,6 +270,36 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
           }
         }
       }
+    } else if constexpr (X6) {
+      const uint16_t* sA0 = (const uint16_t*)cur;
+      const uint16_t* sB0 = sA0 + 3 * BM * LDB16;
+#pragma unroll
+      for (int kk = 0; kk < TK / 16; ++kk) {
+        bf16x8_t bp[3][NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int off = (brow0 + j * 32 + lr) * LDB16 + kk * 16 + lh * 8;
+#pragma unroll
+          for (int p = 0; p < 3; ++p) bp[p][j] = *(const bf16x8_t*)(sB0 + p * BN * LDB16 + off);
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int off = (arow0 + i * 32 + lr) * LDB16 + kk * 16 + lh * 8;
+          bf16x8_t ap[3];
+#pragma unroll
+          for (int p = 0; p < 3; ++p) ap[p] = *(const bf16x8_t*)(sA0 + p * BM * LDB16 + off);
+          // smallest terms first: lo.hi, hi.lo, mid.mid, mid.hi, hi.mid, hi.hi
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[2], bp[0][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[0], bp[2][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[1], bp[1][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[1], bp[0][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[0], bp[1][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[0], bp[0][j], acc[i][j], 0, 0, 0);
+          }
+        }
+      }
     } else {
       // Fragments are read 8 bytes at a time: lane half lh covers k in
       // [16 lh, 16 lh + 16), pair m feeds two MFMAs (k = 16 lh + 2m and +1).
@@ -270,12 +345,14 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   AS1 float* const Cf = (AS1 float*)P.c_hi;
   AS1 uint16_t* const Ch = (AS1 uint16_t*)P.c_hi;
   AS1 uint16_t* const Cl = (AS1 uint16_t*)P.c_lo;
+  AS1 uint16_t* const C2 = Cl + (Cl - Ch);        // X6 third plane
   const AS1 float* const Dm = gptr(P.dmat);
   const AS1 float* const Vm = gptr(P.vm);
   const AS1 float* const Vn = gptr(P.vn);
   const AS1 float* const Gf = (const AS1 float*)P.g_hi;
   const AS1 uint16_t* const Gh = (const AS1 uint16_t*)P.g_hi;
   const AS1 uint16_t* const Gl = (const AS1 uint16_t*)P.g_lo;
+  const AS1 uint16_t* const G2 = Gl + (Gl - Gh);
   // 32-bit element offsets (every operand < 2^32 elements, checked on the
   // host): one offset VGPR per access instead of a 64-bit address pair keeps
   // the epilogue from setting the kernel's register budget
@@ -308,6 +385,10 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
             if constexpr (X3) {
               aux[r] = bf16_bits_to_f32(gld_if32(Gh, go, ok, (uint16_t)0));
               aux2[r] = bf16_bits_to_f32(gld_if32(Gl, go, ok, (uint16_t)0));
+            } else if constexpr (X6) {
+              aux[r] = bf16_bits_to_f32(gld_if32(Gh, go, ok, (uint16_t)0));
+              aux2[r] = bf16_bits_to_f32(gld_if32(Gl, go, ok, (uint16_t)0)) +
+                        bf16_bits_to_f32(gld_if32(G2, go, ok, (uint16_t)0));
             } else {
               aux[r] = gld_if32(Gf, go, ok, 0.f);
             }
@@ -335,6 +416,12 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
             split_bf16(v, h, l);
             Ch[o] = h;
             Cl[o] = l;
+          } else if constexpr (X6) {
+            uint16_t h, m1, l;
+            split_bf16_3(v, h, m1, l);
+            Ch[o] = h;
+            Cl[o] = m1;
+            C2[o] = l;
           } else {
             Cf[o] = v;
           }
@@ -432,15 +519,7 @@ __global__ __launch_bounds__(256) void gather_grad_kernel(const GatherBatch* __r
     const int a = a0 + r, g = g0 + tx;
     if (a >= J.nA || g >= J.nG) continue;
     const float v = tile[tx][r];
-    const long long o = (long long)a * J.ldo + g;
-    if (PREC == PREC_BF16X3) {
-      uint16_t h, l;
-      split_bf16(v, h, l);
-      ((uint16_t*)J.o_hi)[o] = h;
-      ((uint16_t*)J.o_lo)[o] = l;
-    } else {
-      ((float*)J.o_hi)[o] = v;
-    }
+    store_planes<PREC>(J.o_hi, J.o_lo, (long long)a * J.ldo + g, v);
   }
 }
 
@@ -471,15 +550,7 @@ __global__ __launch_bounds__(256) void split_copy_kernel(const SplitJob* __restr
     float v;
     if (J.trans) { orow = c0 + r; ocol = r0 + tx; v = tile[tx][r]; if (orow >= J.cols || ocol >= J.rows) continue; }
     else { orow = r0 + r; ocol = c0 + tx; v = tile[r][tx]; if (orow >= J.rows || ocol >= J.cols) continue; }
-    const long long o = (long long)orow * J.ldo + ocol;
-    if (PREC == PREC_BF16X3) {
-      uint16_t h, l;
-      split_bf16(v, h, l);
-      ((uint16_t*)J.o_hi)[o] = h;
-      ((uint16_t*)J.o_lo)[o] = l;
-    } else {
-      ((float*)J.o_hi)[o] = v;
-    }
+    store_planes<PREC>(J.o_hi, J.o_lo, (long long)orow * J.ldo + ocol, v);
   }
 }
 
@@ -518,6 +589,10 @@ KFAC_API int kfac_pgemm(int prec, int tile, const void* dev_table, int count, in
   }
   if (prec == PREC_BF16X3) {
     KFAC_PGEMM_LAUNCH(PREC_BF16X3)
+  } else if (prec == PREC_BF16X6) {
+    // default tile only (the 3-plane image is 60 KB of LDS per workgroup)
+    hipLaunchKernelGGL((pgemm_kernel<PREC_BF16X6, 128, 128, 2, 2, 2>), g, dim3(256), 0, stream, t,
+                       count, kl);
   } else if (prec == PREC_F32) {
     KFAC_PGEMM_LAUNCH(PREC_F32)
   } else {
@@ -547,6 +622,8 @@ KFAC_API int kfac_gather_grad(int prec, const void* host_jobs, int count, hipStr
     if (!d) return terr;
     if (prec == PREC_BF16X3)
       hipLaunchKernelGGL(gather_grad_kernel<PREC_BF16X3>, dim3(tiles), dim3(256), 0, stream, d);
+    else if (prec == PREC_BF16X6)
+      hipLaunchKernelGGL(gather_grad_kernel<PREC_BF16X6>, dim3(tiles), dim3(256), 0, stream, d);
     else
       hipLaunchKernelGGL(gather_grad_kernel<PREC_F32>, dim3(tiles), dim3(256), 0, stream, d);
     int err = (int)hipGetLastError();
@@ -561,6 +638,8 @@ KFAC_API int kfac_split_copy(int prec, const void* dev_jobs, int count, int tota
   const SplitJob* j = (const SplitJob*)dev_jobs;
   if (prec == PREC_BF16X3)
     hipLaunchKernelGGL(split_copy_kernel<PREC_BF16X3>, dim3(total_tiles), dim3(256), 0, stream, j, count);
+  else if (prec == PREC_BF16X6)
+    hipLaunchKernelGGL(split_copy_kernel<PREC_BF16X6>, dim3(total_tiles), dim3(256), 0, stream, j, count);
   else
     hipLaunchKernelGGL(split_copy_kernel<PREC_F32>, dim3(total_tiles), dim3(256), 0, stream, j, count);
   return (int)hipGetLastError();

@@ -16,6 +16,9 @@ Precision (`precision=`):
             product, fp32 accumulation: ~1e-5 relative error on the
             preconditioned gradient (tests/test_gpu_precond_fused.py),
             ~5x the fp32 MFMA rate.
+  'bf16x6'  operands as three bf16 planes (hi, mid, lo = the fp32
+            significand), six bf16 MFMAs per product (every term above 2^-24
+            relative), fp32 accumulation: fp32-level error at the bf16 rate.
   'fp32'    fp32 operands on the exact f32 MFMA (the reference's fp32 math).
 
 Static GEMM tables (all pointers are arena/buffer pointers that never move)
@@ -34,7 +37,8 @@ from . import _lib
 
 __all__ = ['FusedPreconditioner', 'PRECISIONS']
 
-PRECISIONS = {'fp32': 0, 'bf16x3': 1}
+PRECISIONS = {'fp32': 0, 'bf16x3': 1, 'bf16x6': 2}
+PLANES = {'fp32': 1, 'bf16x3': 2, 'bf16x6': 3}
 EPI_STORE, EPI_HADAMARD, EPI_HADAMARD_VEC, EPI_FINAL = 0, 1, 2, 3
 TILE = 128        # small tile class (csrc/precond_gemm.hip)
 BIG_TILE = 256    # big tile class: half the operand traffic per FLOP
@@ -50,7 +54,7 @@ TILE_SHAPES = {0: (128, 128), 1: (256, 256), 2: (64, 64), 3: (128, 128), 4: (128
 # loads now really stay in flight under the MFMAs): 128 x 128 with 4 waves is
 # best in both modes, ResNet-50 chain bf16x3 1.55 ms (8 waves 1.99, round 1
 # best 1.61), fp32 2.98 ms (16 waves 3.35); profiles/r2_pgemm_sweep.log
-TILE_CFG_DEFAULT = {'bf16x3': 0, 'fp32': 0}
+TILE_CFG_DEFAULT = {'bf16x3': 0, 'fp32': 0, 'bf16x6': 0}
 # None: per-precision default; KFAC_PGEMM_TILE_CFG=<id> forces one (experiments, tests)
 TILE_CFG = int(os.environ['KFAC_PGEMM_TILE_CFG']) if os.environ.get('KFAC_PGEMM_TILE_CFG') \
     else None
@@ -61,6 +65,8 @@ def _tile_class(M, N, precision):
     latency bound (few k-steps in flight per CU): 128 x 128 tiles with more
     waves per tile win over bigger tiles; the big class stays available for
     experiments."""
+    if precision == 'bf16x6':
+        return 0      # the one instantiated 3-plane configuration
     if BIG_TILES and M >= 256 and N >= 256:
         return 1
     return TILE_CFG if TILE_CFG is not None else TILE_CFG_DEFAULT[precision]
@@ -126,13 +132,14 @@ def _upload(recs, device):
 
 
 class _Operand(object):
-    """rows x ld operand, k-contiguous, zero-padded along k (planes or fp32)."""
+    """rows x ld operand, k-contiguous, zero-padded along k: fp32, or 2 / 3
+    bf16 planes in ONE allocation (the kernels find plane p at hi + p (lo - hi))."""
     __slots__ = ('t', 'hi', 'lo', 'ld', 'rows')
 
-    def __init__(self, rows, k, x3, device):
+    def __init__(self, rows, k, planes, device):
         self.rows, self.ld = rows, _pad32(k)
-        if x3:
-            self.t = torch.zeros(2, rows, self.ld, dtype=torch.bfloat16, device=device)
+        if planes > 1:
+            self.t = torch.zeros(planes, rows, self.ld, dtype=torch.bfloat16, device=device)
             self.hi, self.lo = self.t[0].data_ptr(), self.t[1].data_ptr()
         else:
             self.t = torch.zeros(rows, self.ld, dtype=torch.float32, device=device)
@@ -141,30 +148,30 @@ class _Operand(object):
     def value(self):
         """fp32 view of the stored matrix (tests / debugging)."""
         if self.t.dim() == 3:
-            return self.t[0].float() + self.t[1].float()
+            return self.t.float().sum(0)
         return self.t.clone()
 
 
 class _LayerBufs(object):
-    def __init__(self, layer, x3, device, inverse=False):
+    def __init__(self, layer, planes, device, inverse=False):
         self.layer = layer
         nG, nA = layer.grad_shape
         self.nG, self.nA = nG, nA
         # inverse path (use_eigen_decomp=False): QGt holds G_inv and QA holds
         # A_inv (both symmetric), V = (G_inv Grad) A_inv in two stages
-        self.QGt = _Operand(nG, nG, x3, device)
-        self.QA = _Operand(nA, nA, x3, device)
-        self.Gct = _Operand(nA, nG, x3, device)
-        self.T1 = _Operand(nG, nA, x3, device)
+        self.QGt = _Operand(nG, nG, planes, device)
+        self.QA = _Operand(nA, nA, planes, device)
+        self.Gct = _Operand(nA, nG, planes, device)
+        self.T1 = _Operand(nG, nA, planes, device)
         self.prediv = layer.prediv_eigenvalues and not inverse
         if inverse:
             self.QG = self.QAt = self.T2t = self.T3 = None
             self.Dt = None
             return
-        self.QG = _Operand(nG, nG, x3, device)
-        self.QAt = _Operand(nA, nA, x3, device)
-        self.T2t = _Operand(nA, nG, x3, device)
-        self.T3 = _Operand(nG, nA, x3, device)
+        self.QG = _Operand(nG, nG, planes, device)
+        self.QAt = _Operand(nA, nA, planes, device)
+        self.T2t = _Operand(nA, nG, planes, device)
+        self.T3 = _Operand(nG, nA, planes, device)
         self.Dt = torch.zeros(nA, nG, dtype=torch.float32, device=device) if self.prediv else None
 
 
@@ -177,10 +184,11 @@ class FusedPreconditioner(object):
         self.precision = precision
         self.prec = PRECISIONS[precision]
         self.x3 = precision == 'bf16x3'
+        self.planes = PLANES[precision]
         self.device = self.layers[0].module.weight.device if self.layers else None
         # the damped-inverse path (K9): V = G_inv Grad A_inv, two grouped stages
         self.inverse = bool(self.layers) and not self.layers[0].use_eigen_decomp
-        self.bufs = [_LayerBufs(l, self.x3, self.device, self.inverse) for l in self.layers]
+        self.bufs = [_LayerBufs(l, self.planes, self.device, self.inverse) for l in self.layers]
         for b in self.bufs:
             _lib.check_pgemm_extent(max(b.nG, b.nA), 'layer')
         self._gather_sig = None
