@@ -1,0 +1,397 @@
+// Fused training-mode BatchNorm (+ residual add) (+ ReLU) for channels_last
+// bf16 activations on gfx950: the ResNet-50 normalisation layers of the
+// headline benchmark.
+//
+// The stock path runs, per BN layer and step, 3 MIOpen forward kernels, a
+// clamp (ReLU) kernel, an add kernel (residual), a num_batches_tracked
+// increment, and in backward 3 MIOpen kernels plus the ReLU mask and the add's
+// gradient split: ~3.6 ms of a 12.3 ms ResNet-50 step at batch 32, memory-bound
+// work at a fraction of HBM bandwidth (profiles/README.md).  Here:
+//
+//   forward   stats     per (channel group, row chunk) block: shifted sums of
+//                       x - x[first row] and their squares (one 16-byte load =
+//                       8 channels per thread), block-reduced in a fixed
+//                       order -> chunk (mean, M2)
+//             finalize  one wave per channel: Chan's parallel merge of the
+//                       chunks in fp64 -> mean, 1/sqrt(var + eps); running
+//                       stats (unbiased var) and num_batches_tracked updated
+//                       in place; scale = w / sigma, shift = b - mean scale
+//             apply     y = relu(x scale + shift [+ z]) in bf16
+//   backward  reduce    per chunk: sum g and sum g x_hat, g = dy masked by
+//                       y > 0 (ReLU) -- x_hat recomputed from x, mean, invstd
+//             finalize  fp64 chunk sums -> dbias, dweight and the dx
+//                       coefficients
+//             apply     dx = (w / sigma) (g - sum g / M - x_hat sum g x_hat / M),
+//                       dz = g for the residual branch
+//
+// Every reduction runs in a fixed order (no atomics): bitwise reproducible.
+// Layout: x[m * C + c], m < M = N H W, C % 8 == 0, 16-byte aligned rows.
+#include "common.h"
+
+namespace {
+
+typedef unsigned u32x4n __attribute__((ext_vector_type(4)));
+
+constexpr int NT = 256;              // threads per block
+constexpr int TARGET_BLOCKS = 2048;  // stats / reduce grid (>> 256 CUs)
+
+__device__ __forceinline__ void unpack8(const u32x4n v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(v[i] << 16);
+    f[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ u32x4n pack8(const float* f) {
+  u32x4n v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    v[i] = (uint32_t)f32_to_bf16_bits(f[2 * i]) | ((uint32_t)f32_to_bf16_bits(f[2 * i + 1]) << 16);
+  return v;
+}
+
+struct Geo {
+  int cb, tpr, rpi, ncg, rows, nchunks;
+};
+
+// channel group width, threads per row, rows per iteration and the row chunks
+// of an (M, C) problem (host and device agree: computed on the host only)
+Geo geometry(long long M, int C) {
+  Geo g;
+  // a power of two (threads per row must divide the block), C % 8 == 0
+  g.cb = 256;
+  while (g.cb > 8 && C % g.cb) g.cb >>= 1;
+  g.tpr = g.cb / 8;
+  g.rpi = NT / g.tpr;
+  g.ncg = C / g.cb;
+  long long per = (M * g.ncg + TARGET_BLOCKS - 1) / TARGET_BLOCKS;
+  if (per < g.rpi) per = g.rpi;
+  per = (per + g.rpi - 1) / g.rpi * g.rpi;
+  g.rows = (int)per;
+  g.nchunks = (int)((M + per - 1) / per);
+  return g;
+}
+
+// sums over this block's chunk of rows for 8 channels per thread, reduced
+// over the block's row lanes into the lanes of row 0 (fixed order)
+__device__ __forceinline__ void block_reduce16(float* acc, float (*red)[17], int rr, int cv,
+                                               int tpr, int rpi) {
+  const int t = rr * tpr + cv;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) red[t][i] = acc[i];
+  __syncthreads();
+  if (rr == 0) {
+    for (int q = 1; q < rpi; ++q) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] += red[q * tpr + cv][i];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- forward
+__global__ __launch_bounds__(NT) void bn_stats_kernel(const uint16_t* __restrict__ x, long long M,
+                                                      int C, Geo g, float* __restrict__ part) {
+  __shared__ float red[NT][17];
+  const int cg = blockIdx.x, chunk = blockIdx.y;
+  const int t = threadIdx.x, cv = t % g.tpr, rr = t / g.tpr;
+  const int c0 = cg * g.cb + cv * 8;
+  const long long m0 = (long long)chunk * g.rows;
+  const long long m1 = m0 + g.rows < M ? m0 + g.rows : M;
+  const AS1 u32x4n* X = (const AS1 u32x4n*)x;
+  float k[8];
+  unpack8(X[(m0 * C + c0) / 8], k);      // shift: the chunk's first row
+  float acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  for (long long m = m0 + rr; m < m1; m += g.rpi) {
+    float f[8];
+    unpack8(X[(m * C + c0) / 8], f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float d = f[i] - k[i];
+      acc[i] += d;
+      acc[8 + i] = fmaf(d, d, acc[8 + i]);
+    }
+  }
+  block_reduce16(acc, red, rr, cv, g.tpr, g.rpi);
+  if (rr == 0) {
+    const float n = (float)(m1 - m0);
+    float* o = part + ((long long)chunk * C + c0) * 2;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float s1 = acc[i], s2 = acc[8 + i];
+      o[2 * i] = k[i] + s1 / n;                       // chunk mean
+      o[2 * i + 1] = fmaxf(s2 - s1 * (s1 / n), 0.f);  // chunk M2
+    }
+  }
+}
+
+// one wave per channel: Chan's merge of the chunk (mean, M2) pairs in fp64
+__global__ __launch_bounds__(NT) void bn_finalize_kernel(
+    const float* __restrict__ part, long long M, int C, Geo g, float eps, float momentum,
+    const float* __restrict__ w, const float* __restrict__ b, float* __restrict__ rmean,
+    float* __restrict__ rvar, long long* __restrict__ nbt, float* __restrict__ save_mean,
+    float* __restrict__ save_invstd, float* __restrict__ scale, float* __restrict__ shift) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt != nullptr) nbt[0] += 1;
+  if (c >= C) return;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  for (int k = lane; k < g.nchunks; k += 64) {
+    const long long r0 = (long long)k * g.rows;
+    const double nb = (double)((M - r0) < g.rows ? (M - r0) : g.rows);
+    const double mb = (double)part[((long long)k * C + c) * 2];
+    const double qb = (double)part[((long long)k * C + c) * 2 + 1];
+    const double nn = n + nb, d = mb - mean;
+    mean += d * nb / nn;
+    m2 += qb + d * d * n * nb / nn;
+    n = nn;
+  }
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const double nb = __shfl_xor(n, off, 64), mb = __shfl_xor(mean, off, 64),
+                 qb = __shfl_xor(m2, off, 64);
+    const double nn = n + nb;
+    if (nn > 0.0) {
+      // symmetric in (a, b): both lanes of a pair compute the same value
+      const double lo_n = (lane & off) ? nb : n, hi_n = (lane & off) ? n : nb;
+      const double lo_m = (lane & off) ? mb : mean, hi_m = (lane & off) ? mean : mb;
+      const double lo_q = (lane & off) ? qb : m2, hi_q = (lane & off) ? m2 : qb;
+      const double d = hi_m - lo_m;
+      mean = lo_m + d * hi_n / nn;
+      m2 = lo_q + hi_q + d * d * lo_n * hi_n / nn;
+    }
+    n = nn;
+  }
+  if (lane == 0) {
+    const double var = m2 / (double)M;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    save_mean[c] = (float)mean;
+    save_invstd[c] = invstd;
+    if (rmean != nullptr) {
+      const double unb = M > 1 ? m2 / (double)(M - 1) : var;
+      rmean[c] = (float)((1.0 - momentum) * (double)rmean[c] + momentum * mean);
+      rvar[c] = (float)((1.0 - momentum) * (double)rvar[c] + momentum * unb);
+    }
+    const float sc = (w ? w[c] : 1.f) * invstd;
+    scale[c] = sc;
+    shift[c] = (b ? b[c] : 0.f) - (float)mean * sc;
+  }
+}
+
+template <bool RELU, bool ADD>
+__global__ __launch_bounds__(NT) void bn_apply_kernel(const uint16_t* __restrict__ x,
+                                                      const uint16_t* __restrict__ z,
+                                                      const float* __restrict__ scale,
+                                                      const float* __restrict__ shift,
+                                                      uint16_t* __restrict__ y, long long nvec,
+                                                      int C) {
+  const AS1 u32x4n* X = (const AS1 u32x4n*)x;
+  const AS1 u32x4n* Z = (const AS1 u32x4n*)z;
+  AS1 u32x4n* Y = (AS1 u32x4n*)y;
+  const int cvec = C / 8;
+  for (long long v = blockIdx.x * (long long)NT + threadIdx.x; v < nvec;
+       v += (long long)gridDim.x * NT) {
+    const int c0 = (int)(v % cvec) * 8;
+    float f[8], o[8];
+    unpack8(X[v], f);
+    const fx4 s0 = *(const AS1 fx4*)(gptr(scale) + c0), s1 = *(const AS1 fx4*)(gptr(scale) + c0 + 4);
+    const fx4 h0 = *(const AS1 fx4*)(gptr(shift) + c0), h1 = *(const AS1 fx4*)(gptr(shift) + c0 + 4);
+    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    float zz[8];
+    if (ADD) unpack8(Z[v], zz);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float r = fmaf(f[i], sc[i], sh[i]);
+      if (ADD) r += zz[i];
+      o[i] = RELU ? fmaxf(r, 0.f) : r;
+    }
+    Y[v] = pack8(o);
+  }
+}
+
+// --------------------------------------------------------------- backward
+template <bool RELU>
+__global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
+    const uint16_t* __restrict__ x, const float* __restrict__ mean,
+    const float* __restrict__ invstd, long long M, int C, Geo g, float* __restrict__ part) {
+  __shared__ float red[NT][17];
+  const int cg = blockIdx.x, chunk = blockIdx.y;
+  const int t = threadIdx.x, cv = t % g.tpr, rr = t / g.tpr;
+  const int c0 = cg * g.cb + cv * 8;
+  const long long m0 = (long long)chunk * g.rows;
+  const long long m1 = m0 + g.rows < M ? m0 + g.rows : M;
+  const AS1 u32x4n* DY = (const AS1 u32x4n*)dy;
+  const AS1 u32x4n* Y = (const AS1 u32x4n*)y;
+  const AS1 u32x4n* X = (const AS1 u32x4n*)x;
+  float mu[8], is[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { mu[i] = mean[c0 + i]; is[i] = invstd[c0 + i]; }
+  float acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  for (long long m = m0 + rr; m < m1; m += g.rpi) {
+    const long long v = (m * C + c0) / 8;
+    float gv[8], xv[8], yv[8];
+    unpack8(DY[v], gv);
+    unpack8(X[v], xv);
+    if (RELU) unpack8(Y[v], yv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float gg = (!RELU || yv[i] > 0.f) ? gv[i] : 0.f;
+      acc[i] += gg;
+      acc[8 + i] = fmaf(gg, (xv[i] - mu[i]) * is[i], acc[8 + i]);
+    }
+  }
+  block_reduce16(acc, red, rr, cv, g.tpr, g.rpi);
+  if (rr == 0) {
+    float* o = part + ((long long)chunk * C + c0) * 2;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      o[2 * i] = acc[i];
+      o[2 * i + 1] = acc[8 + i];
+    }
+  }
+}
+
+// one wave per channel: fp64 chunk sums -> dw, db and (a, k1, k2) of
+// dx = a (g - k1 - x_hat k2)
+__global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(
+    const float* __restrict__ part, long long M, int C, Geo g, const float* __restrict__ w,
+    const float* __restrict__ invstd, float* __restrict__ dw, float* __restrict__ db,
+    float* __restrict__ coef) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+  if (c >= C) return;
+  double sg = 0.0, sgx = 0.0;
+  for (int k = lane; k < g.nchunks; k += 64) {
+    sg += (double)part[((long long)k * C + c) * 2];
+    sgx += (double)part[((long long)k * C + c) * 2 + 1];
+  }
+  sg = wave_reduce_sum_d(sg);
+  sgx = wave_reduce_sum_d(sgx);
+  if (lane == 0) {
+    if (dw) dw[c] = (float)sgx;
+    if (db) db[c] = (float)sg;
+    coef[3 * c] = (w ? w[c] : 1.f) * invstd[c];
+    coef[3 * c + 1] = (float)(sg / (double)M);
+    coef[3 * c + 2] = (float)(sgx / (double)M);
+  }
+}
+
+template <bool RELU, bool ADD>
+__global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
+    const uint16_t* __restrict__ x, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ coef,
+    uint16_t* __restrict__ dx, uint16_t* __restrict__ dz, long long nvec, int C) {
+  const AS1 u32x4n* DY = (const AS1 u32x4n*)dy;
+  const AS1 u32x4n* Y = (const AS1 u32x4n*)y;
+  const AS1 u32x4n* X = (const AS1 u32x4n*)x;
+  AS1 u32x4n* DX = (AS1 u32x4n*)dx;
+  AS1 u32x4n* DZ = (AS1 u32x4n*)dz;
+  const int cvec = C / 8;
+  for (long long v = blockIdx.x * (long long)NT + threadIdx.x; v < nvec;
+       v += (long long)gridDim.x * NT) {
+    const int c0 = (int)(v % cvec) * 8;
+    float gv[8], xv[8], yv[8], o[8], gz[8];
+    unpack8(DY[v], gv);
+    unpack8(X[v], xv);
+    if (RELU) unpack8(Y[v], yv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = c0 + i;
+      const float gg = (!RELU || yv[i] > 0.f) ? gv[i] : 0.f;
+      const float xh = (xv[i] - mean[c]) * invstd[c];
+      o[i] = coef[3 * c] * (gg - coef[3 * c + 1] - xh * coef[3 * c + 2]);
+      gz[i] = gg;
+    }
+    DX[v] = pack8(o);
+    if (ADD) DZ[v] = pack8(gz);
+  }
+}
+
+int apply_grid(long long nvec) {
+  long long b = (nvec + NT - 1) / NT;
+  return (int)(b < 8192 ? (b > 0 ? b : 1) : 8192);
+}
+
+}  // namespace
+
+// workspace floats of one BN call: chunk partials (2 per channel per chunk)
+// + scale/shift (forward) or the dx coefficients (backward)
+KFAC_API long long kfac_bn_ws_floats(long long M, int C) {
+  const Geo g = geometry(M, C);
+  return 2LL * g.nchunks * C + 3LL * C;
+}
+
+KFAC_API int kfac_bn_forward(const void* x, const void* z, const float* w, const float* b,
+                             float* rmean, float* rvar, long long* nbt, void* y,
+                             float* save_mean, float* save_invstd, float* ws, long long M, int C,
+                             float eps, float momentum, int relu, hipStream_t stream) {
+  if (C % 8 || M <= 0 || ((uintptr_t)x & 15) || ((uintptr_t)y & 15) ||
+      (z && ((uintptr_t)z & 15)))
+    return -2;
+  const Geo g = geometry(M, C);
+  float* part = ws;
+  float* scale = ws + 2LL * g.nchunks * C;
+  float* shift = scale + C;
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(g.ncg, g.nchunks), dim3(NT), 0, stream,
+                     (const uint16_t*)x, M, C, g, part);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 3) / 4), dim3(NT), 0, stream, part, M, C, g,
+                     eps, momentum, w, b, rmean, rvar, nbt, save_mean, save_invstd, scale, shift);
+  const long long nvec = M * C / 8;
+  const dim3 grid(apply_grid(nvec));
+  const uint16_t* X = (const uint16_t*)x;
+  const uint16_t* Z = (const uint16_t*)z;
+  uint16_t* Y = (uint16_t*)y;
+  if (relu && z)
+    hipLaunchKernelGGL((bn_apply_kernel<true, true>), grid, dim3(NT), 0, stream, X, Z, scale, shift, Y, nvec, C);
+  else if (relu)
+    hipLaunchKernelGGL((bn_apply_kernel<true, false>), grid, dim3(NT), 0, stream, X, Z, scale, shift, Y, nvec, C);
+  else if (z)
+    hipLaunchKernelGGL((bn_apply_kernel<false, true>), grid, dim3(NT), 0, stream, X, Z, scale, shift, Y, nvec, C);
+  else
+    hipLaunchKernelGGL((bn_apply_kernel<false, false>), grid, dim3(NT), 0, stream, X, Z, scale, shift, Y, nvec, C);
+  return (int)hipGetLastError();
+}
+
+// dz (the residual branch's gradient) is written when non-null
+KFAC_API int kfac_bn_backward(const void* dy, const void* y, const void* x, const float* w,
+                              const float* save_mean, const float* save_invstd, void* dx,
+                              void* dz, float* dw, float* db, float* ws, long long M, int C,
+                              int relu, hipStream_t stream) {
+  if (C % 8 || M <= 0 || ((uintptr_t)dy & 15) || ((uintptr_t)x & 15) || ((uintptr_t)dx & 15) ||
+      (relu && ((uintptr_t)y & 15)) || (dz && ((uintptr_t)dz & 15)))
+    return -2;
+  const Geo g = geometry(M, C);
+  float* part = ws;
+  float* coef = ws + 2LL * g.nchunks * C;
+  const uint16_t* DY = (const uint16_t*)dy;
+  const uint16_t* Y = (const uint16_t*)y;
+  const uint16_t* X = (const uint16_t*)x;
+  if (relu)
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, dim3(g.ncg, g.nchunks), dim3(NT), 0, stream,
+                       DY, Y, X, save_mean, save_invstd, M, C, g, part);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, dim3(g.ncg, g.nchunks), dim3(NT), 0, stream,
+                       DY, Y, X, save_mean, save_invstd, M, C, g, part);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(NT), 0, stream, part, M, C,
+                     g, w, save_invstd, dw, db, coef);
+  const long long nvec = M * C / 8;
+  const dim3 grid(apply_grid(nvec));
+  uint16_t* DX = (uint16_t*)dx;
+  uint16_t* DZ = (uint16_t*)dz;
+  if (relu && dz)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<true, true>), grid, dim3(NT), 0, stream, DY, Y, X, save_mean, save_invstd, coef, DX, DZ, nvec, C);
+  else if (relu)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false>), grid, dim3(NT), 0, stream, DY, Y, X, save_mean, save_invstd, coef, DX, DZ, nvec, C);
+  else if (dz)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true>), grid, dim3(NT), 0, stream, DY, Y, X, save_mean, save_invstd, coef, DX, DZ, nvec, C);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<false, false>), grid, dim3(NT), 0, stream, DY, Y, X, save_mean, save_invstd, coef, DX, DZ, nvec, C);
+  return (int)hipGetLastError();
+}

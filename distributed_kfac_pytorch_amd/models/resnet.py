@@ -9,10 +9,15 @@ ResNet-50, factor sizes in SURVEY.md section 2.3) is identical.
 
 MI355X notes: the model is memory-format agnostic; `bench.py` runs it in
 `channels_last` under bf16 autocast, which is the layout MIOpen's NHWC
-kernels prefer on gfx950 (measured in profiles/).
+kernels prefer on gfx950 (measured in profiles/).  Every BatchNorm, with the
+ReLU and the residual add that follow it, runs through ops/bn.bn_act: fused
+hand-written kernels (csrc/bn.hip) for bf16 channels_last training batches,
+the stock modules otherwise (same parameters, buffers and state_dict).
 """
 import torch
 import torch.nn as nn
+
+from ..ops.bn import bn_act
 
 __all__ = ['ResNet', 'Bottleneck', 'BasicBlock', 'resnet_tiny', 'resnet18', 'resnet34',
            'resnet50', 'resnet101', 'resnet152', 'get_model']
@@ -24,6 +29,13 @@ def _conv3x3(cin, cout, stride=1):
 
 def _conv1x1(cin, cout, stride=1):
     return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
+
+
+def _downsample(ds, x):
+    """The projection shortcut (1x1 conv + BatchNorm, no ReLU)."""
+    if isinstance(ds, nn.Sequential) and len(ds) == 2 and isinstance(ds[1], nn.BatchNorm2d):
+        return bn_act(ds[0](x), ds[1], relu=False)
+    return ds(x)
 
 
 class BasicBlock(nn.Module):
@@ -39,10 +51,9 @@ class BasicBlock(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        identity = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
-        return self.relu(out + identity)
+        identity = x if self.downsample is None else _downsample(self.downsample, x)
+        out = bn_act(self.conv1(x), self.bn1)
+        return bn_act(self.conv2(out), self.bn2, relu=True, z=identity)
 
 
 class Bottleneck(nn.Module):
@@ -60,11 +71,10 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        identity = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
-        return self.relu(out + identity)
+        identity = x if self.downsample is None else _downsample(self.downsample, x)
+        out = bn_act(self.conv1(x), self.bn1)
+        out = bn_act(self.conv2(out), self.bn2)
+        return bn_act(self.conv3(out), self.bn3, relu=True, z=identity)
 
 
 class ResNet(nn.Module):
@@ -114,7 +124,7 @@ class ResNet(nn.Module):
     # layer3 boundary (parallel/overlap.py): the top half holds ~90% of the
     # parameters, whose gradients are complete first in backward
     def forward_bottom(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(bn_act(self.conv1(x), self.bn1))
         return self.layer2(self.layer1(x))
 
     def forward_top(self, x):

@@ -322,19 +322,28 @@ def _large_fused(mats, clip, stream, use_graph=True):
     on a side stream.  No library solver, no host round trip; each stage is
     a cached hipGraph.
 
-    The side groups are ENQUEUED from worker threads: a reduction graph holds
-    one node per column (9358 for the 4608 batch), more packets than a HW
-    queue holds, so hipGraphLaunch blocks its host thread until the GPU has
-    drained most of it.  Issued from one thread, the second group only
-    reached its stream when the first group was nearly done (kernel trace:
-    the two reductions ran back to back, 109 + 62 ms); from its own thread
-    it is enqueued at once and the chains overlap."""
+    Options measured on ResNet-50 (profiles/r2_eig_streams.log), both off by
+    default: FUSED_THREADS enqueues the side groups from worker threads (a
+    reduction graph holds one node per column, more packets than a HW queue
+    holds, so hipGraphLaunch blocks its host thread until the GPU has drained
+    most of it; from one thread the second group reaches its stream late) --
+    the chains then overlap, but each slows down as much as the overlap gains
+    (both bandwidth-heavy): 157 vs 156 ms.  FUSED_PRIORITY puts the largest
+    factors' chain on a high-priority stream: 162 vs 157 ms.
+    """
     dev = mats[0].device
     groups = _fused_groups(mats)
     outs = [None] * len(mats)
+    caller = stream
+    if FUSED_PRIORITY and len(groups) > 1:
+        # the largest factors' chain sets the critical path: its launches go
+        # to a high-priority queue, so the command processor dispatches them
+        # ahead of the smaller factors' chain, which has slack
+        stream = _priority_stream(dev)
     streams = [stream] + _side_streams(dev, len(groups) - 1)
-    for s in streams[1:]:
-        s.wait_stream(stream)
+    for s in streams:
+        if s is not caller:
+            s.wait_stream(caller)
 
     def run(slot):
         g, st = groups[slot], streams[slot]
@@ -362,16 +371,29 @@ def _large_fused(mats, clip, stream, use_graph=True):
             run(slot)
         _FUSED_PLANNED.add(key)
     del _INFOS[:-256]
-    for g, st in zip(groups[1:], streams[1:]):
-        stream.wait_stream(st)
+    for g, st in zip(groups, streams):
+        if st is caller:
+            continue
+        caller.wait_stream(st)
         for i in g:
             mats[i].record_stream(st)
-            outs[i][0].record_stream(stream)
-            outs[i][1].record_stream(stream)
+            outs[i][0].record_stream(caller)
+            outs[i][1].record_stream(caller)
     return outs
 
 
-FUSED_THREADS = bool(int(os.environ.get('KFAC_EIG_FUSED_THREADS', '1')))
+FUSED_THREADS = bool(int(os.environ.get('KFAC_EIG_FUSED_THREADS', '0')))
+FUSED_PRIORITY = bool(int(os.environ.get('KFAC_EIG_FUSED_PRIORITY', '0')))
+_prio = {}
+
+
+def _priority_stream(device):
+    key = str(device)
+    s = _prio.get(key)
+    if s is None:
+        lo, hi = torch.cuda.Stream.priority_range()
+        s = _prio[key] = torch.cuda.Stream(device=device, priority=hi)
+    return s
 _FUSED_PLANNED = set()
 _POOL = [None]
 

@@ -2,7 +2,4 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 export MIOPEN_FIND_MODE=FAST
-timeout -k 10 400 python3 -u bench.py --steps 20 --warmup 5 > gpurun_out/bench_x6.log 2>&1 && \
-timeout -k 10 400 python3 -u bench.py --steps 20 --warmup 5 --precond-precision fp32 > gpurun_out/bench_f32.log 2>&1 && \
-timeout -k 10 400 python3 -u bench.py --steps 100 --warmup 10 > gpurun_out/bench_x6_100.log 2>&1
-echo rc=$?
+timeout -k 10 400 python3 -u -m pytest -q -x --timeout 300 --timeout-method thread tests/test_gpu_bn.py tests/test_gpu_models.py tests/test_gpu_graphs.py tests/test_gpu_kfac.py > gpurun_out/t_bn.log 2>&1; echo "rc=$?" >> gpurun_out/t_bn.log

@@ -47,13 +47,14 @@ def main():
                 ('stedc', {'SOLVER': 'stedc'}), ('stedc_tri193', {'SOLVER': 'stedc', 'TRIDIAG_MIN_N': 193}),
                 ('w2', {'W': 2}), ('w1', {'W': 1}),
                 ('nothreads', {'TH': False}), ('fs1', {'FS': 1}), ('fs3', {'FS': 3}),
-                ('fs4', {'FS': 4})]
+                ('fs4', {'FS': 4}), ('noprio', {'PR': False}),
+                ('noprio_nothreads', {'PR': False, 'TH': False})]
     if len(sys.argv) > 1:
         variants = [v for v in variants if v[0] in sys.argv[1:]]
     res = {}
     base = dict(SPLIT_N=eigen.SPLIT_N, TRIDIAG_MIN_N=eigen.TRIDIAG_MIN_N,
                 SOLVER=eigen.TRIDIAG_SOLVER, LARGE=eigen.LARGE_PATH,
-                FS=eigen.FUSED_STREAMS, TH=eigen.FUSED_THREADS)
+                FS=eigen.FUSED_STREAMS, TH=eigen.FUSED_THREADS, PR=eigen.FUSED_PRIORITY)
     for name, cfg in variants:
         eigen.LARGE_PATH = cfg.get('LARGE', base['LARGE'])
         eigen.TRIDIAG_SOLVER = cfg.get('SOLVER', base['SOLVER'])
@@ -61,6 +62,7 @@ def main():
         eigen.TRIDIAG_MIN_N = cfg.get('TRIDIAG_MIN_N', base['TRIDIAG_MIN_N'])
         eigen.FUSED_STREAMS = cfg.get('FS', base['FS'])
         eigen.FUSED_THREADS = cfg.get('TH', base['TH'])
+        eigen.FUSED_PRIORITY = cfg.get('PR', base['PR'])
         if 'W' in cfg:
             os.environ['KFAC_EIGH_WORKERS'] = str(cfg['W'])
         else:
