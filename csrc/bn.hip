@@ -12,8 +12,8 @@
 //                       x - x[first row] and their squares (one 16-byte load =
 //                       8 channels per thread), block-reduced in a fixed
 //                       order -> chunk (mean, M2)
-//             finalize  one wave per channel: Chan's parallel merge of the
-//                       chunks in fp64 -> mean, 1/sqrt(var + eps); running
+//             finalize  one wave per channel: the chunks merged in fp64
+//                       about a common shift -> mean, 1/sqrt(var + eps); running
 //                       stats (unbiased var) and num_batches_tracked updated
 //                       in place; scale = w / sigma, shift = b - mean scale
 //             apply     y = relu(x scale + shift [+ z]) in bf16
@@ -33,7 +33,7 @@ namespace {
 typedef unsigned u32x4n __attribute__((ext_vector_type(4)));
 
 constexpr int NT = 256;              // threads per block
-constexpr int TARGET_BLOCKS = 2048;  // stats / reduce grid (>> 256 CUs)
+constexpr int TARGET_BLOCKS = 1024;  // stats / reduce grid (4 per CU; fewer chunk partials)
 
 __device__ __forceinline__ void unpack8(const u32x4n v, float* f) {
 #pragma unroll
@@ -127,7 +127,9 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(const uint16_t* __restrict
   }
 }
 
-// one wave per channel: Chan's merge of the chunk (mean, M2) pairs in fp64
+// one wave per channel: the chunk (mean, M2) pairs merged in fp64 about a
+// common shift (the first chunk's mean): S1 = sum n_k (mean_k - K),
+// S2 = sum M2_k + n_k (mean_k - K)^2 -- FMAs only, no per-chunk divisions
 __global__ __launch_bounds__(NT) void bn_finalize_kernel(
     const float* __restrict__ part, long long M, int C, Geo g, float eps, float momentum,
     const float* __restrict__ w, const float* __restrict__ b, float* __restrict__ rmean,
@@ -137,33 +139,20 @@ __global__ __launch_bounds__(NT) void bn_finalize_kernel(
   const int c = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
   if (blockIdx.x == 0 && threadIdx.x == 0 && nbt != nullptr) nbt[0] += 1;
   if (c >= C) return;
-  double n = 0.0, mean = 0.0, m2 = 0.0;
+  const double K = (double)part[(long long)c * 2];
+  double s1 = 0.0, s2 = 0.0;
+#pragma unroll 8
   for (int k = lane; k < g.nchunks; k += 64) {
     const long long r0 = (long long)k * g.rows;
     const double nb = (double)((M - r0) < g.rows ? (M - r0) : g.rows);
-    const double mb = (double)part[((long long)k * C + c) * 2];
-    const double qb = (double)part[((long long)k * C + c) * 2 + 1];
-    const double nn = n + nb, d = mb - mean;
-    mean += d * nb / nn;
-    m2 += qb + d * d * n * nb / nn;
-    n = nn;
+    const double d = (double)part[((long long)k * C + c) * 2] - K;
+    s1 = fma(nb, d, s1);
+    s2 += (double)part[((long long)k * C + c) * 2 + 1] + nb * d * d;
   }
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const double nb = __shfl_xor(n, off, 64), mb = __shfl_xor(mean, off, 64),
-                 qb = __shfl_xor(m2, off, 64);
-    const double nn = n + nb;
-    if (nn > 0.0) {
-      // symmetric in (a, b): both lanes of a pair compute the same value
-      const double lo_n = (lane & off) ? nb : n, hi_n = (lane & off) ? n : nb;
-      const double lo_m = (lane & off) ? mb : mean, hi_m = (lane & off) ? mean : mb;
-      const double lo_q = (lane & off) ? qb : m2, hi_q = (lane & off) ? m2 : qb;
-      const double d = hi_m - lo_m;
-      mean = lo_m + d * hi_n / nn;
-      m2 = lo_q + hi_q + d * d * lo_n * hi_n / nn;
-    }
-    n = nn;
-  }
+  s1 = wave_reduce_sum_d(s1);
+  s2 = wave_reduce_sum_d(s2);
+  const double mean = K + s1 / (double)M;
+  const double m2 = s2 - s1 * (s1 / (double)M);
   if (lane == 0) {
     const double var = m2 / (double)M;
     const float invstd = (float)(1.0 / sqrt(var + (double)eps));
@@ -267,6 +256,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(
   const int c = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
   if (c >= C) return;
   double sg = 0.0, sgx = 0.0;
+#pragma unroll 8
   for (int k = lane; k < g.nchunks; k += 64) {
     sg += (double)part[((long long)k * C + c) * 2];
     sgx += (double)part[((long long)k * C + c) * 2 + 1];
