@@ -132,3 +132,26 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   v += dpp_d<0x140>(v);
   return swap_sum32_d(swap_sum16_d(v));
 }
+
+// In-register transpose-reduce of 64 values per lane over the wave: lane L
+// ends with the wave sum of value L (63 shuffles, pairwise, fixed order).
+template <int M>
+__device__ __forceinline__ void kfac_butterfly_stage(float (&v)[64], int lane) {
+  const bool up = (lane & M) != 0;
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const float send = up ? v[i] : v[i + M];
+    const float keep = up ? v[i + M] : v[i];
+    v[i] = keep + __shfl_xor(send, M, 64);
+  }
+}
+__device__ __forceinline__ float kfac_butterfly64(float (&v)[64]) {
+  const int lane = threadIdx.x & 63;
+  kfac_butterfly_stage<32>(v, lane);
+  kfac_butterfly_stage<16>(v, lane);
+  kfac_butterfly_stage<8>(v, lane);
+  kfac_butterfly_stage<4>(v, lane);
+  kfac_butterfly_stage<2>(v, lane);
+  kfac_butterfly_stage<1>(v, lane);
+  return v[0];
+}

@@ -134,11 +134,13 @@ __global__ __launch_bounds__(256) void zero_kernel(float4* p, long long n4) {
 }
 
 // Row j of the reduced matrix (== reflector j in column-major) made explicit:
-// zeros up to j, the implicit 1 at j+1, v[1:] after.
-__global__ __launch_bounds__(256) void make_v_kernel(float* A, int lda, long long sA, int n) {
+// zeros up to j, the implicit 1 at j+shift, v[1:] after (shift 1: one-stage
+// tridiagonalisation; 16: the band reduction of csrc/eig_sy2sb.hip).
+__global__ __launch_bounds__(256) void make_v_kernel(float* A, int lda, long long sA, int n,
+                                                     int shift) {
   float* row = A + blockIdx.y * sA + (long long)blockIdx.x * lda;
   const int j = blockIdx.x;
-  for (int i = threadIdx.x; i <= j + 1 && i < n; i += 256) row[i] = (i == j + 1) ? 1.f : 0.f;
+  for (int i = threadIdx.x; i <= j + shift && i < n; i += 256) row[i] = (i == j + shift) ? 1.f : 0.f;
 }
 
 // T_k (upper triangular, ROW-major BT x BT, zero beyond kb) from
@@ -173,7 +175,7 @@ __global__ __launch_bounds__(BT) void larft_kernel(const float* G, float* T, con
 
 struct BtArgs {
   float* A; int lda; long long sA; const float* tau; float* Z; int ldz; long long sZ; int n;
-  int batch; float* Tbuf; float* W1; float* W2; float* Vt;
+  int batch; float* Tbuf; float* W1; float* W2; float* Vt; int shift;
 };
 
 // One recorded operation of the back-transformation.
@@ -297,7 +299,7 @@ int run_plan(const BtArgs& a, const BtPlan& plan, hipStream_t stream) {
       }
       case 3:
         hipLaunchKernelGGL(make_v_kernel, dim3(a.n, a.batch), dim3(256), 0, stream, a.A, a.lda,
-                           a.sA, a.n);
+                           a.sA, a.n, a.shift);
         err = (int)hipGetLastError();
         break;
       default:
@@ -310,7 +312,7 @@ int run_plan(const BtArgs& a, const BtPlan& plan, hipStream_t stream) {
   return 0;
 }
 
-typedef std::tuple<float*, float*, int, int, float*, float*, float*, float*> BtKey;
+typedef std::tuple<float*, float*, int, int, float*, float*, float*, float*, int> BtKey;
 std::mutex g_bt_mu;
 std::map<BtKey, BtPlan> g_bt;
 
@@ -318,7 +320,7 @@ std::map<BtKey, BtPlan> g_bt;
 // stream) of this buffer set; built on first use.  Call it from one thread
 // while no other thread issues library work (kfac_backtransform_prepare).
 BtPlan* plan_for(const BtArgs& a, int* err) {
-  const BtKey key(a.A, a.Z, a.n, a.batch, a.Tbuf, a.W1, a.W2, a.Vt);
+  const BtKey key(a.A, a.Z, a.n, a.batch, a.Tbuf, a.W1, a.W2, a.Vt, a.shift);
   std::lock_guard<std::mutex> lk(g_bt_mu);
   auto it = g_bt.find(key);
   if (it != g_bt.end()) return &it->second;
@@ -354,7 +356,7 @@ KFAC_API int kfac_tridiag_backtransform(float* A, int lda, long long strideA, co
                                         float* Tbuf, float* W1, float* W2, float* Vt,
                                         int use_graph, hipStream_t stream) {
   if (lda % 64 || ldz % 64 || lda != ldz || n < 2) return -2;
-  const BtArgs a{A, lda, strideA, tau, Z, ldz, strideZ, n, batch, Tbuf, W1, W2, Vt};
+  const BtArgs a{A, lda, strideA, tau, Z, ldz, strideZ, n, batch, Tbuf, W1, W2, Vt, 1};
   int err = 0;
   BtPlan* plan = plan_for(a, &err);
   if (!plan) return err ? err : -4;
@@ -366,9 +368,24 @@ KFAC_API int kfac_backtransform_prepare(float* A, int lda, long long strideA, co
                                         float* Z, int ldz, long long strideZ, int n, int batch,
                                         float* Tbuf, float* W1, float* W2, float* Vt) {
   if (lda % 64 || ldz % 64 || lda != ldz || n < 2) return -2;
-  const BtArgs a{A, lda, strideA, tau, Z, ldz, strideZ, n, batch, Tbuf, W1, W2, Vt};
+  const BtArgs a{A, lda, strideA, tau, Z, ldz, strideZ, n, batch, Tbuf, W1, W2, Vt, 1};
   int err = 0;
   return plan_for(a, &err) ? 0 : (err ? err : -4);
+}
+
+// Same, for reflectors that start `shift` rows below their index (the band
+// reduction's Q1: shift 16).
+KFAC_API int kfac_backtransform_shift(float* A, int lda, long long strideA, const float* tau,
+                                      float* Z, int ldz, long long strideZ, int n, int batch,
+                                      float* Tbuf, float* W1, float* W2, float* Vt, int shift,
+                                      int use_graph, hipStream_t stream) {
+  if (lda % 64 || ldz % 64 || lda != ldz || n < 2 || shift < 1) return -2;
+  const BtArgs a{A, lda, strideA, tau, Z, ldz, strideZ, n, batch, Tbuf, W1, W2, Vt, shift};
+  int err = 0;
+  BtPlan* plan = plan_for(a, &err);
+  if (!plan) return err ? err : -4;
+  if (use_graph && plan->exec) return (int)hipGraphLaunch(plan->exec, stream);
+  return run_plan(a, *plan, stream);
 }
 
 // Tridiagonal divide and conquer only, every matrix of the batch (eigenvalues

@@ -1,0 +1,288 @@
+// Back-transformation through the bulge-chasing reflectors (Q2 of the
+// two-stage eigensolver; csrc/eig_sb2st.hip writes them).  Z (eigenvectors
+// of the tridiagonal matrix, one per row) <- Q2 Z.
+//
+// Groups: the 16 sweeps 16 g .. 16 g + 15 at one step j form
+// G(g, j) = H(16g, j) ... H(16g+15, j) = I - V T V^T, V a 31 x 16 window of
+// staggered reflectors starting at row 16 g + 1 + 16 j.  Q2 Z applies the
+// blocks g descending and, inside a block, j ascending; group (g, j) at tick
+// (G-1-g) + j keeps that order and the groups of one tick touch disjoint row
+// windows (scripts/models/two_stage_model.py: apply_q2_ticks), so one launch
+// per tick applies every group of the tick to every eigenvector, for every
+// matrix of the batch (~2 n / 16 launches, captured in a hipGraph).
+//
+//   q2_t      one wave per group: Gram of the window, T (larft, forward)
+//   q2_apply  one workgroup per (group, 256 eigenvectors): a thread holds one
+//             eigenvector's 31-row window in VGPRs; V and T from LDS
+//             (broadcast reads): P = V^T z, P = T P, z -= V P
+#include "common.h"
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace {
+
+constexpr int BW = 16;
+constexpr int WR = 2 * BW - 1;     // window rows
+constexpr int ST = 256;            // eigenvectors per apply workgroup
+constexpr int MAXM = 255;
+
+struct Q2Mat {
+  const float* v2; long long ldv2;
+  float* Z; long long ldz;
+  float* T;                        // [G][jmax][16][16]
+  int n, G, jmax, nstrips;
+};
+
+__device__ inline void map_block(const int* __restrict__ offs, int nact, int* soff, int& mat,
+                                 int& local) {
+  __shared__ int sm;
+  const int t = threadIdx.x, b = blockIdx.x;
+  for (int i = t; i <= nact; i += blockDim.x) soff[i] = offs[i];   // any block size
+  __syncthreads();
+  for (int i = t; i < nact; i += blockDim.x)
+    if (soff[i] <= b && b < soff[i + 1]) sm = i;
+  __syncthreads();
+  mat = sm;
+  local = b - soff[mat];
+}
+
+// does sweep s have a step j (stage 2 task with >= 2 rows)?
+__device__ __forceinline__ bool has_step(int n, int s, int j) {
+  return s <= n - 3 && j * BW <= n - 3 - s;
+}
+
+// reflector i of group (g, j): v[l], l < 16 (v[0] = 1), tau
+__device__ __forceinline__ float refl_v(const Q2Mat& M, int g, int j, int i, int l, float* tau) {
+  const int s = BW * g + i;
+  if (!has_step(M.n, s, j)) { if (tau) *tau = 0.f; return 0.f; }
+  const float* row = M.v2 + (long long)s * M.ldv2 + BW * j;
+  if (tau) *tau = row[0];
+  return l == 0 ? 1.f : row[l];
+}
+
+__global__ __launch_bounds__(64) void q2_t_kernel(const Q2Mat* __restrict__ mats,
+                                                  const int* __restrict__ offs, int nact) {
+  __shared__ int soff[MAXM + 1];
+  __shared__ float V[BW][BW];      // V[i][l] = v_i[l]
+  __shared__ float tau[BW];
+  __shared__ float G[BW][BW + 1];
+  __shared__ float T[BW][BW + 1];
+  int mi, local;
+  map_block(offs, nact, soff, mi, local);
+  const Q2Mat M = mats[mi];
+  const int g = local / M.jmax, j = local % M.jmax;
+  const int lane = threadIdx.x;
+  if (!has_step(M.n, BW * g, j)) return;       // empty group (uniform)
+  for (int e = lane; e < BW * BW; e += 64) {
+    const int i = e / BW, l = e % BW;
+    float t;
+    V[i][l] = refl_v(M, g, j, i, l, &t);
+    if (l == 0) tau[i] = t;
+  }
+  __syncthreads();
+  // G[a][b] = sum_r V_win[r][a] V_win[r][b], V_win[r][i] = v_i[r - i]
+  for (int e = lane; e < BW * BW; e += 64) {
+    const int a = e / BW, b = e % BW;
+    float s = 0.f;
+    for (int r = max(a, b); r < min(a, b) + BW; ++r) s += V[a][r - a] * V[b][r - b];
+    G[a][b] = s;
+  }
+  for (int e = lane; e < BW * (BW + 1); e += 64) (&T[0][0])[e] = 0.f;
+  __syncthreads();
+  for (int i = 0; i < BW; ++i) {
+    const float ti = tau[i];
+    float acc = 0.f;
+    if (lane < i)
+      for (int q = lane; q < i; ++q) acc += T[lane][q] * G[q][i];
+    __syncthreads();
+    if (lane < i) T[lane][i] = -ti * acc;
+    else if (lane == i) T[lane][i] = ti;
+    __syncthreads();
+  }
+  float* const out = M.T + ((long long)g * M.jmax + j) * BW * BW;
+  for (int e = lane; e < BW * BW; e += 64) out[e] = T[e / BW][e % BW];
+}
+
+__global__ __launch_bounds__(ST) void q2_apply_kernel(const Q2Mat* __restrict__ mats,
+                                                      const int* __restrict__ offs,
+                                                      const int* __restrict__ jlo, int nact,
+                                                      int tick) {
+  __shared__ int soff[MAXM + 1];
+  __shared__ float V[BW][BW];
+  __shared__ float T[BW][BW];
+  int mi, local;
+  map_block(offs, nact, soff, mi, local);
+  const Q2Mat M = mats[mi];
+  const int task = local / M.nstrips, strip = local % M.nstrips;
+  const int j = jlo[mi] + task;
+  const int g = M.G - 1 - tick + j;
+  const int tid = threadIdx.x;
+  if (g < 0 || g >= M.G || j >= M.jmax || !has_step(M.n, BW * g, j)) return;   // uniform
+  {
+    const int i = tid / BW, l = tid % BW;
+    V[i][l] = refl_v(M, g, j, i, l, nullptr);
+    T[i][l] = M.T[((long long)g * M.jmax + j) * BW * BW + tid];
+  }
+  __syncthreads();
+  const int e = strip * ST + tid;
+  if (e >= M.n) return;
+  const int row0 = BW * g + 1 + BW * j;
+  const int w = min(WR, M.n - row0);
+  AS1 float* const zr = gptr(M.Z) + (long long)e * M.ldz + row0;
+  float z[WR];
+#pragma unroll
+  for (int r = 0; r < WR; ++r) z[r] = gld_if(zr, r, r < w, 0.f);
+  float p[BW];
+#pragma unroll
+  for (int i = 0; i < BW; ++i) {
+    float s = 0.f;
+#pragma unroll
+    for (int l = 0; l < BW; ++l) s += V[i][l] * z[i + l];
+    p[i] = s;
+  }
+  float q[BW];
+#pragma unroll
+  for (int i = 0; i < BW; ++i) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = i; k < BW; ++k) s += T[i][k] * p[k];
+    q[i] = s;
+  }
+#pragma unroll
+  for (int r = 0; r < WR; ++r) {
+    float s = z[r];
+#pragma unroll
+    for (int i = 0; i < BW; ++i)
+      if (r - i >= 0 && r - i < BW) s -= V[i][r - i] * q[i];
+    if (r < w) zr[r] = s;
+  }
+}
+
+struct Q2Plan {
+  Q2Mat* d_mats = nullptr;
+  int* d_offs = nullptr;      // [ticks + 1][nm + 1]: [0] = T kernel, [1 + t] = tick t
+  int* d_jlo = nullptr;       // [ticks][nm]
+  int count = 0, ticks = 0;
+  std::vector<int> grid, nact;
+  hipGraphExec_t exec = nullptr;
+};
+
+int enqueue(const Q2Plan& P, hipStream_t stream) {
+  const int nm = P.count;
+  if (P.grid[0] > 0)
+    hipLaunchKernelGGL(q2_t_kernel, dim3(P.grid[0]), dim3(64), 0, stream, P.d_mats, P.d_offs,
+                       P.nact[0]);
+  for (int t = 0; t < P.ticks; ++t) {
+    if (P.grid[1 + t] == 0) continue;
+    hipLaunchKernelGGL(q2_apply_kernel, dim3(P.grid[1 + t]), dim3(ST), 0, stream, P.d_mats,
+                       P.d_offs + (size_t)(1 + t) * (nm + 1), P.d_jlo + (size_t)t * nm,
+                       P.nact[1 + t], t);
+  }
+  return (int)hipGetLastError();
+}
+
+std::mutex g_mu;
+std::map<std::string, Q2Plan> g_plans;
+
+inline int q2_G(int n) { return (n - 1 + BW - 1) / BW; }
+inline int q2_jmax(int n) { return n >= 3 ? (n - 3) / BW + 1 : 0; }
+
+}  // namespace
+
+struct KfacQ2Record {
+  const float* v2; long long ldv2; float* Z; long long ldz; float* T; long long n;
+};
+
+// T workspace floats per matrix
+KFAC_API long long kfac_q2_t_floats(int n) {
+  return (long long)std::max(1, q2_G(n)) * std::max(1, q2_jmax(n)) * BW * BW;
+}
+
+// Z (n rows = eigenvectors of the tridiagonal matrix, ldz) <- Q2 Z for every
+// matrix of the batch.
+KFAC_API int kfac_q2_batched(const KfacQ2Record* recs, int count, int use_graph,
+                             hipStream_t stream) {
+  if (count <= 0) return 0;
+  if (count > MAXM) return -5;
+  std::vector<Q2Mat> mats(count);
+  for (int i = 0; i < count; ++i) {
+    const KfacQ2Record& r = recs[i];
+    if (r.n < 2) return -2;
+    Q2Mat& M = mats[i];
+    memset(&M, 0, sizeof(M));
+    M.v2 = r.v2; M.ldv2 = r.ldv2; M.Z = r.Z; M.ldz = r.ldz; M.T = r.T; M.n = (int)r.n;
+    M.G = q2_G(M.n); M.jmax = q2_jmax(M.n); M.nstrips = (M.n + ST - 1) / ST;
+  }
+  const std::string key((const char*)mats.data(), sizeof(Q2Mat) * mats.size());
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_plans.find(key);
+  if (it == g_plans.end()) {
+    Q2Plan P;
+    P.count = count;
+    const int nm = count;
+    for (auto& M : mats) P.ticks = std::max(P.ticks, M.G + M.jmax);
+    std::vector<int> offs((size_t)(P.ticks + 1) * (nm + 1), 0), jl((size_t)std::max(1, P.ticks) * nm, 0);
+    P.grid.assign(P.ticks + 1, 0);
+    P.nact.assign(P.ticks + 1, 0);
+    {
+      int acc = 0;
+      for (int i = 0; i < nm; ++i) {
+        offs[i] = acc;
+        const int c = mats[i].G * mats[i].jmax;
+        if (c > 0) P.nact[0] = i + 1;
+        acc += c;
+      }
+      offs[nm] = acc;
+      P.grid[0] = acc;
+    }
+    for (int t = 0; t < P.ticks; ++t) {
+      int acc = 0;
+      int* of = offs.data() + (size_t)(1 + t) * (nm + 1);
+      for (int i = 0; i < nm; ++i) {
+        const Q2Mat& M = mats[i];
+        // g = G-1-t+j in [0, G), j in [0, jmax)
+        const int lo = std::max(0, t - (M.G - 1));
+        const int hi = std::min(M.jmax - 1, t);
+        const int cnt = hi >= lo ? hi - lo + 1 : 0;
+        of[i] = acc;
+        jl[(size_t)t * nm + i] = lo;
+        if (cnt > 0) P.nact[1 + t] = i + 1;
+        acc += cnt * M.nstrips;
+      }
+      of[nm] = acc;
+      P.grid[1 + t] = acc;
+    }
+    int e = (int)hipMalloc(&P.d_mats, sizeof(Q2Mat) * nm);
+    if (!e) e = (int)hipMemcpy(P.d_mats, mats.data(), sizeof(Q2Mat) * nm, hipMemcpyHostToDevice);
+    if (!e) e = (int)hipMalloc(&P.d_offs, sizeof(int) * offs.size());
+    if (!e) e = (int)hipMemcpy(P.d_offs, offs.data(), sizeof(int) * offs.size(), hipMemcpyHostToDevice);
+    if (!e) e = (int)hipMalloc(&P.d_jlo, sizeof(int) * jl.size());
+    if (!e) e = (int)hipMemcpy(P.d_jlo, jl.data(), sizeof(int) * jl.size(), hipMemcpyHostToDevice);
+    if (e) return e;
+    it = g_plans.emplace(key, P).first;
+  }
+  Q2Plan& P = it->second;
+  hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cst) != hipSuccess) return -3;
+  const bool graph = use_graph && stream != nullptr && cst == hipStreamCaptureStatusNone;
+  if (graph && !P.exec) {
+    static hipStream_t cap = nullptr;
+    if (!cap && hipStreamCreateWithFlags(&cap, hipStreamNonBlocking) != hipSuccess) cap = nullptr;
+    hipGraph_t gr = nullptr;
+    if (cap && hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal) == hipSuccess) {
+      const int e1 = enqueue(P, cap);
+      const hipError_t e2 = hipStreamEndCapture(cap, &gr);
+      if (!e1 && e2 == hipSuccess && gr && hipGraphInstantiate(&P.exec, gr, nullptr, nullptr, 0) != hipSuccess)
+        P.exec = nullptr;
+      if (gr) (void)hipGraphDestroy(gr);
+    }
+    (void)hipGetLastError();
+  }
+  if (graph && P.exec) return (int)hipGraphLaunch(P.exec, stream);
+  return enqueue(P, stream);
+}

@@ -1,0 +1,344 @@
+// Band -> tridiagonal reduction (stage 2 of the two-stage symmetric
+// eigensolver; reference: kfac/layers/utils.py:45-74 calls
+// torch.symeig per factor).  Stage 1 (csrc/eig_sy2sb.hip) leaves a band of
+// half-bandwidth BW = 16; here every sweep s annihilates column s below the
+// subdiagonal with a Householder reflector of length <= BW and chases the
+// bulge it creates down the band, one task (s, j) per step j:
+//
+//   task (s, j):  c = s (j = 0) or s + 1 + (j-1) BW,  rows R = s+1+j BW ..
+//                 s+(j+1) BW.  x = B[R, c] -> reflector (v, tau); B <- H B H
+//                 on the stored lower band: column c, the bulge block
+//                 B[R, c+1 .. r0-1] (left), the diagonal block B[R, R] (both
+//                 sides), the block below B[r1+1 .. r1+BW, R] (right: the next
+//                 bulge).
+//
+// Task (s+1, j) may run once (s, j+2) is done: at tick 3 s + j every task
+// touches a disjoint region (scripts/models/two_stage_model.py checks the
+// wavefront order against the sweep-by-sweep order in fp64).
+//
+// MI355X mapping: one 1024-thread workgroup runs 16 consecutive sweeps, one
+// per wave, in lockstep ticks (wave w runs step t - 3w at tick t, one
+// workgroup barrier per tick) on an LDS-resident window of the band: 1024
+// columns x 2 BW diagonals, circular, 128 KB of the 160 KB LDS.  Block t+4
+// of the band streams in from global memory while tick t computes (two
+// register sets: the loads have a tick to land); columns no sweep of the
+// workgroup will touch again are written back and published with an
+// agent-scope release.  Workgroup g+1 (the next 16 sweeps) trails g by ~48
+// ticks and waits (acquire, bounded spin) for the columns it needs: a
+// pipeline of workgroups down each matrix, every matrix of the batch at
+// once.  A workgroup only ever waits on the previous workgroup of its own
+// matrix, and the launch table orders workgroups by their start tick, so
+// in-order dispatch always makes progress; every spin is bounded (error flag
+// + release of the successor) so a fault cannot leave waves running.
+//
+// Output: d, e of the tridiagonal matrix and the reflectors for the
+// back-transformation (csrc/eig_q2.hip): row s of V2 holds sweep s's steps,
+// step j at [j BW, (j+1) BW): tau in slot 0 (v[0] = 1 is implicit), v[1..].
+#include "common.h"
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace {
+
+constexpr int BW = 16;             // half-bandwidth of the stage-1 band
+constexpr int ND = 2 * BW;         // stored diagonals per column (band + bulge room)
+constexpr int NSW = 16;            // sweeps (waves) per workgroup
+constexpr int WIN = 1024;          // LDS window columns (circular)
+constexpr int LAG = 4;             // band block prefetched LAG ticks ahead
+constexpr int SPIN_MAX = 1 << 22;  // bounded waits (~1 s): a lost predecessor cannot hang the GPU
+
+struct SbMat {
+  float* band;   // n x ND, column-major band: band[c * ND + (r - c)]
+  float* v2;     // n x ldv2 reflector rows
+  float* d;
+  float* e;
+  int* prog;     // [nwg] published retire boundary (columns < prog[g] final)
+  int n, ldv2, nwg, pad;
+};
+struct SbWg { int mat, g; };
+
+__device__ __forceinline__ float& LB(float* Lb, int r, int c) {
+  return Lb[((c & (WIN - 1)) * ND) + (r - c)];
+}
+
+// one bulge-chasing step of sweep s, by one wave; false when the sweep has
+// run off the end of the matrix
+__device__ bool sb_task(float* Lb, int n, int s, int j, AS1 float* v2row, int lane) {
+  const int c = j == 0 ? s : s + 1 + (j - 1) * BW;
+  const int r0 = s + 1 + j * BW;
+  const int r1 = min(s + (j + 1) * BW, n - 1);
+  const int L = r1 - r0 + 1;
+  if (r0 > n - 1 || L < 2) return false;
+  const float x = lane < L ? LB(Lb, r0 + lane, c) : 0.f;
+  const float alpha = __shfl(x, 0, 64);
+  const float sig = wave_sum(lane >= 1 && lane < L ? x * x : 0.f);
+  float tau = 0.f, beta = alpha, scal = 0.f;
+  if (sig != 0.f) {
+    beta = -copysignf(sqrtf(alpha * alpha + sig), alpha);
+    tau = (beta - alpha) / beta;
+    scal = 1.f / (alpha - beta);
+  }
+  const float v = lane == 0 ? 1.f : (lane < L ? x * scal : 0.f);
+  if (lane < L) LB(Lb, r0 + lane, c) = lane == 0 ? beta : 0.f;
+  if (lane < BW) v2row[j * BW + lane] = lane == 0 ? tau : v;
+  if (tau == 0.f) return true;
+  float vl[BW];
+#pragma unroll
+  for (int l = 0; l < BW; ++l) vl[l] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+  // left: bulge block columns c+1 .. r0-1 (BW-1 of them for j >= 1)
+  const int nq = r0 - 1 - c;
+  if (lane < nq) {
+    const int q = c + 1 + lane;
+    float col[BW];
+    float y = 0.f;
+#pragma unroll
+    for (int l = 0; l < BW; ++l) {
+      col[l] = l < L ? LB(Lb, r0 + l, q) : 0.f;
+      y += vl[l] * col[l];
+    }
+    y *= tau;
+#pragma unroll
+    for (int l = 0; l < BW; ++l)
+      if (l < L) LB(Lb, r0 + l, q) = col[l] - y * vl[l];
+  }
+  // both sides: diagonal block D = B[R, R] (symmetric, lower stored)
+  {
+    const int a = lane;
+    float row[BW];
+    float p = 0.f;
+#pragma unroll
+    for (int l = 0; l < BW; ++l) {
+      const bool ok = a < L && l < L;
+      const int hi = a > l ? a : l, lo = a > l ? l : a;
+      row[l] = ok ? LB(Lb, r0 + hi, r0 + lo) : 0.f;
+      p += row[l] * vl[l];
+    }
+    p *= tau;
+    const float va = (a < L) ? v : 0.f;          // this lane's v[a]
+    const float pv = wave_sum(p * va);
+    const float w = a < L ? p - 0.5f * tau * pv * va : 0.f;
+    float wl[BW];
+#pragma unroll
+    for (int l = 0; l < BW; ++l) wl[l] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), l));
+#pragma unroll
+    for (int l = 0; l < BW; ++l)
+      if (a < L && l <= a) LB(Lb, r0 + a, r0 + l) = row[l] - va * wl[l] - w * vl[l];
+  }
+  // right: rows r1+1 .. r1+BW of columns R (creates the next bulge)
+  const int nE = min(BW, n - 1 - r1);
+  if (lane < nE) {
+    const int r = r1 + 1 + lane;
+    float rw[BW];
+    float z = 0.f;
+#pragma unroll
+    for (int l = 0; l < BW; ++l) {
+      rw[l] = l < L ? LB(Lb, r, r0 + l) : 0.f;
+      z += rw[l] * vl[l];
+    }
+    z *= tau;
+#pragma unroll
+    for (int l = 0; l < BW; ++l)
+      if (l < L) LB(Lb, r, r0 + l) = rw[l] - z * vl[l];
+  }
+  return true;
+}
+
+__device__ __forceinline__ int task_min_col(int s, int j) {
+  return j == 0 ? s : s + 1 + (j - 1) * BW;
+}
+
+// wait (thread 0 only) until the previous workgroup of this matrix has
+// published columns < need; false on timeout
+__device__ bool wait_prog(const int* prog, int need) {
+  for (int it = 0; it < SPIN_MAX; ++it) {
+    if (__hip_atomic_load(prog, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= need) return true;
+    __builtin_amdgcn_s_sleep(4);
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(1024) void sb2st_kernel(const SbMat* __restrict__ mats,
+                                                     const SbWg* __restrict__ wgs,
+                                                     int* __restrict__ err) {
+  extern __shared__ float Lb[];                 // WIN x ND
+  __shared__ int s_done[NSW];
+  __shared__ int s_flag;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const SbWg W = wgs[blockIdx.x];
+  const SbMat M = mats[W.mat];
+  const int n = M.n, g = W.g, s0 = g * NSW;
+  AS1 float* const band = gptr(M.band);
+  const int* prev = g > 0 ? M.prog + g - 1 : nullptr;
+  int* const mine = M.prog + g;
+  if (tid < NSW) s_done[tid] = (s0 + tid > n - 2) ? 1 : 0;
+  if (tid == 0) s_flag = 0;
+  // columns [s0, s0 + 3 BW) synchronously, block 3 into register set 1
+  const int cl = tid >> 5, dl = tid & 31;       // thread's (column, diagonal) in a 32-column slab
+  if (tid == 0 && prev && !wait_prog(prev, min(n, s0 + 4 * BW))) {
+    s_flag = 1;
+    atomicOr(err, 1);
+  }
+  __syncthreads();
+  if (s_flag) {
+    if (tid == 0) __hip_atomic_store(mine, n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  for (int c = s0 + cl; c < min(n, s0 + 3 * BW); c += 32) LB(Lb, c + dl, c) = band[(long long)c * ND + dl];
+  float pre[2];
+  {
+    const int c = s0 + 3 * BW + (tid >> 5);
+    pre[1] = (tid < BW * ND && c < n) ? band[(long long)c * ND + dl] : 0.f;
+    pre[0] = 0.f;
+  }
+  int retired = s0;
+  __syncthreads();
+  for (int t = 0;; ++t) {
+    // (1) prefetch block t + LAG into set t & 1 (published by the previous workgroup)
+    const int pc0 = s0 + (t + LAG) * BW;
+    if (pc0 < n) {
+      if (tid == 0 && prev && !wait_prog(prev, min(n, pc0 + BW))) {
+        s_flag = 1;
+        atomicOr(err, 1);
+      }
+      __syncthreads();
+      if (s_flag) break;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const int c = pc0 + (tid >> 5);
+      const float vv = (tid < BW * ND && c < n) ? band[(long long)c * ND + dl] : 0.f;
+      if (t & 1) pre[1] = vv; else pre[0] = vv;
+    }
+    // (2) one step of every active sweep (disjoint regions within the tick)
+    {
+      const int s = s0 + wave, j = t - 3 * wave;
+      if (!s_done[wave] && j >= 0) {
+        const bool more = sb_task(Lb, n, s, j, gptr(M.v2) + (long long)s * M.ldv2, lane);
+        if (!more && lane == 0) s_done[wave] = 1;
+      }
+    }
+    __syncthreads();
+    // (3) commit block t + LAG - 1 (loaded during the previous tick)
+    {
+      const int cc0 = s0 + (t + LAG - 1) * BW;
+      const int c = cc0 + (tid >> 5);
+      if (cc0 < n && tid < BW * ND && c < n) LB(Lb, c + dl, c) = ((t + 1) & 1) ? pre[1] : pre[0];
+    }
+    __syncthreads();
+    // (4) retire: columns below every unfinished sweep's next task
+    int all_done = 1, bound = n;
+#pragma unroll
+    for (int w = 0; w < NSW; ++w) {
+      if (!s_done[w]) {
+        all_done = 0;
+        const int jn = max(t + 1 - 3 * w, 0);
+        bound = min(bound, task_min_col(s0 + w, jn));
+      }
+    }
+    bound = min(bound, min(n, s0 + (t + LAG) * BW));   // never past the committed columns
+    if (all_done) bound = n;
+    if (bound > retired) {
+      for (int c = retired + cl; c < bound; c += 32) band[(long long)c * ND + dl] = LB(Lb, c + dl, c);
+      retired = bound;
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(mine, retired, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (all_done) return;
+    __syncthreads();
+  }
+  // abort path: release the successor (its results are garbage, err is set)
+  if (tid == 0) __hip_atomic_store(mine, n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(256) void sb2st_prep_kernel(const SbMat* __restrict__ mats) {
+  const SbMat M = mats[blockIdx.y];
+  for (int g = blockIdx.x * 256 + threadIdx.x; g < M.nwg; g += gridDim.x * 256) M.prog[g] = 0;
+}
+
+__global__ __launch_bounds__(256) void sb2st_de_kernel(const SbMat* __restrict__ mats) {
+  const SbMat M = mats[blockIdx.y];
+  for (int c = blockIdx.x * 256 + threadIdx.x; c < M.n; c += gridDim.x * 256) {
+    M.d[c] = M.band[(long long)c * ND];
+    M.e[c] = c + 1 < M.n ? M.band[(long long)c * ND + 1] : 0.f;
+  }
+}
+
+struct SbPlan {
+  SbMat* d_mats = nullptr;
+  SbWg* d_wgs = nullptr;
+  int count = 0, nwg = 0, maxn = 0;
+};
+std::mutex g_mu;
+std::map<std::string, SbPlan> g_plans;
+
+}  // namespace
+
+struct KfacSbRecord {
+  float* band; float* v2; float* d; float* e; int* prog; long long n; long long ldv2;
+};
+
+KFAC_API int kfac_sb2st_bw() { return BW; }
+KFAC_API long long kfac_sb2st_ldv2(int n) { return ((long long)n + 2 * BW + 15) / 16 * 16; }
+KFAC_API int kfac_sb2st_nwg(int n) { return (n - 1 + NSW - 1) / NSW; }
+
+// Band (n x 2BW column-major, lower band in diagonals 0..BW, zeros above)
+// -> d, e and the bulge-chasing reflectors, every matrix of the batch in one
+// persistent launch.  err: device int, OR-ed with 1 if a wait timed out.
+KFAC_API int kfac_sb2st_batched(const KfacSbRecord* recs, int count, int* err,
+                                hipStream_t stream) {
+  if (count <= 0) return 0;
+  std::vector<SbMat> mats(count);
+  for (int i = 0; i < count; ++i) {
+    const KfacSbRecord& r = recs[i];
+    if (r.n < 2 || r.ldv2 < kfac_sb2st_ldv2((int)r.n)) return -2;
+    SbMat& M = mats[i];
+    memset(&M, 0, sizeof(M));
+    M.band = r.band; M.v2 = r.v2; M.d = r.d; M.e = r.e; M.prog = r.prog;
+    M.n = (int)r.n; M.ldv2 = (int)r.ldv2; M.nwg = kfac_sb2st_nwg((int)r.n);
+  }
+  const std::string key((const char*)mats.data(), sizeof(SbMat) * mats.size());
+  SbPlan* P;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_plans.find(key);
+    if (it == g_plans.end()) {
+      SbPlan p;
+      p.count = count;
+      std::vector<SbWg> wgs;
+      int gmax = 0;
+      for (auto& M : mats) { gmax = std::max(gmax, M.nwg); p.maxn = std::max(p.maxn, M.n); }
+      for (int g = 0; g < gmax; ++g)          // start-tick order: g major
+        for (int i = 0; i < count; ++i)
+          if (g < mats[i].nwg) wgs.push_back(SbWg{i, g});
+      p.nwg = (int)wgs.size();
+      int e1 = (int)hipMalloc(&p.d_mats, sizeof(SbMat) * count);
+      if (!e1) e1 = (int)hipMemcpy(p.d_mats, mats.data(), sizeof(SbMat) * count, hipMemcpyHostToDevice);
+      if (!e1) e1 = (int)hipMalloc(&p.d_wgs, sizeof(SbWg) * wgs.size());
+      if (!e1) e1 = (int)hipMemcpy(p.d_wgs, wgs.data(), sizeof(SbWg) * wgs.size(), hipMemcpyHostToDevice);
+      if (e1) return e1;
+      static bool attr = false;
+      if (!attr) {
+        e1 = (int)hipFuncSetAttribute((const void*)sb2st_kernel,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      WIN * ND * (int)sizeof(float));
+        if (e1) return e1;
+        attr = true;
+      }
+      it = g_plans.emplace(key, p).first;
+    }
+    P = &it->second;
+  }
+  int gmax = 0;
+  for (auto& M : mats) gmax = std::max(gmax, M.nwg);
+  hipLaunchKernelGGL(sb2st_prep_kernel, dim3((gmax + 255) / 256, count), dim3(256), 0, stream,
+                     P->d_mats);
+  hipLaunchKernelGGL(sb2st_kernel, dim3(P->nwg), dim3(1024), WIN * ND * sizeof(float), stream,
+                     P->d_mats, P->d_wgs, err);
+  hipLaunchKernelGGL(sb2st_de_kernel, dim3((P->maxn + 255) / 256, count), dim3(256), 0, stream,
+                     P->d_mats);
+  return (int)hipGetLastError();
+}

@@ -310,6 +310,9 @@ def _fused_groups(mats):
 
 
 FUSED_STREAMS = int(os.environ.get('KFAC_EIG_FUSED_STREAMS', '2'))
+# two-stage solver (dense -> band -> tridiagonal, ops/eig2s.py) instead of the
+# one-stage fused reduction
+TWO_STAGE = bool(int(os.environ.get('KFAC_EIG_TWO_STAGE', '0')))
 FUSED_SPLIT = bool(int(os.environ.get('KFAC_EIG_FUSED_SPLIT', '1')))
 
 
@@ -347,7 +350,11 @@ def _large_fused(mats, clip, stream, use_graph=True):
 
     def run(slot):
         g, st = groups[slot], streams[slot]
-        for i, r in zip(g, _fused_group([mats[i] for i in g], clip, st, use_graph, slot)):
+        solve = _fused_group
+        if TWO_STAGE:
+            from . import eig2s
+            solve = eig2s.two_stage_group
+        for i, r in zip(g, solve([mats[i] for i in g], clip, st, use_graph, slot)):
             outs[i] = r
 
     key = (str(dev), use_graph, tuple(tuple(mats[i].shape[0] for i in g) for g in groups))

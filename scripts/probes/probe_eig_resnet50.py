@@ -48,13 +48,15 @@ def main():
                 ('w2', {'W': 2}), ('w1', {'W': 1}),
                 ('nothreads', {'TH': False}), ('fs1', {'FS': 1}), ('fs3', {'FS': 3}),
                 ('fs4', {'FS': 4}), ('noprio', {'PR': False}),
-                ('noprio_nothreads', {'PR': False, 'TH': False})]
+                ('noprio_nothreads', {'PR': False, 'TH': False}),
+                ('two_stage', {'TS': True}), ('two_stage_fs1', {'TS': True, 'FS': 1})]
     if len(sys.argv) > 1:
         variants = [v for v in variants if v[0] in sys.argv[1:]]
     res = {}
     base = dict(SPLIT_N=eigen.SPLIT_N, TRIDIAG_MIN_N=eigen.TRIDIAG_MIN_N,
                 SOLVER=eigen.TRIDIAG_SOLVER, LARGE=eigen.LARGE_PATH,
-                FS=eigen.FUSED_STREAMS, TH=eigen.FUSED_THREADS, PR=eigen.FUSED_PRIORITY)
+                FS=eigen.FUSED_STREAMS, TH=eigen.FUSED_THREADS, PR=eigen.FUSED_PRIORITY,
+                TS=eigen.TWO_STAGE)
     for name, cfg in variants:
         eigen.LARGE_PATH = cfg.get('LARGE', base['LARGE'])
         eigen.TRIDIAG_SOLVER = cfg.get('SOLVER', base['SOLVER'])
@@ -63,6 +65,7 @@ def main():
         eigen.FUSED_STREAMS = cfg.get('FS', base['FS'])
         eigen.FUSED_THREADS = cfg.get('TH', base['TH'])
         eigen.FUSED_PRIORITY = cfg.get('PR', base['PR'])
+        eigen.TWO_STAGE = cfg.get('TS', base['TS'])
         if 'W' in cfg:
             os.environ['KFAC_EIGH_WORKERS'] = str(cfg['W'])
         else:
@@ -77,11 +80,13 @@ def main():
             ts.append((time.perf_counter() - t) * 1e3)
         eigen.check_solver_status()
         err = 0.0
-        for A, (Q, d) in zip(mats[-8:], outs[-8:]):
+        orth = 0.0
+        for A, (Q, d) in zip(mats, outs):
             err = max(err, float((A @ Q - Q * d).norm() / A.norm()))
-        res[name] = {'ms': min(ts), 'all_ms': ts, 'resid': err}
-        print('%-14s %8.2f ms  (runs %s)  resid %.1e' % (name, min(ts),
-              ' '.join('%.1f' % t for t in ts), err), flush=True)
+            orth = max(orth, float((Q.t() @ Q - torch.eye(Q.shape[0], device=Q.device)).abs().max()))
+        res[name] = {'ms': min(ts), 'all_ms': ts, 'resid': err, 'orth': orth}
+        print('%-14s %8.2f ms  (runs %s)  resid %.1e  orth %.1e' % (name, min(ts),
+              ' '.join('%.1f' % t for t in ts), err, orth), flush=True)
     print(json.dumps(res))
 
 
