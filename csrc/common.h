@@ -155,3 +155,27 @@ __device__ __forceinline__ float kfac_butterfly64(float (&v)[64]) {
   kfac_butterfly_stage<1>(v, lane);
   return v[0];
 }
+
+// Transposed wave sum of 16 values per lane: lanes with (lane & 15) == x end
+// with the wave sum of value x (15 + 2 shuffles instead of 16 wave sums).
+template <int M>
+__device__ __forceinline__ void kfac_fold16(float (&v)[16], int lane) {
+  const bool up = (lane & M) != 0;
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const float send = up ? v[i] : v[i + M];
+    const float keep = up ? v[i + M] : v[i];
+    v[i] = keep + __shfl_xor(send, M, 64);
+  }
+}
+__device__ __forceinline__ float kfac_butterfly16(float (&v)[16]) {
+  const int lane = threadIdx.x & 63;
+  kfac_fold16<8>(v, lane);
+  kfac_fold16<4>(v, lane);
+  kfac_fold16<2>(v, lane);
+  kfac_fold16<1>(v, lane);
+  float r = v[0];
+  r += __shfl_xor(r, 16, 64);
+  r += __shfl_xor(r, 32, 64);
+  return r;
+}

@@ -133,10 +133,12 @@ __global__ __launch_bounds__(ST) void q2_apply_kernel(const Q2Mat* __restrict__ 
   if (e >= M.n) return;
   const int row0 = BW * g + 1 + BW * j;
   const int w = min(WR, M.n - row0);
-  AS1 float* const zr = gptr(M.Z) + (long long)e * M.ldz + row0;
+  // Z is component-major here (row r = component r of every eigenvector):
+  // a wave's loads of one component are 64 consecutive floats
+  AS1 float* const zr = gptr(M.Z) + (long long)row0 * M.ldz + e;
   float z[WR];
 #pragma unroll
-  for (int r = 0; r < WR; ++r) z[r] = gld_if(zr, r, r < w, 0.f);
+  for (int r = 0; r < WR; ++r) z[r] = gld_if(zr, (long long)r * M.ldz, r < w, 0.f);
   float p[BW];
 #pragma unroll
   for (int i = 0; i < BW; ++i) {
@@ -159,7 +161,7 @@ __global__ __launch_bounds__(ST) void q2_apply_kernel(const Q2Mat* __restrict__ 
 #pragma unroll
     for (int i = 0; i < BW; ++i)
       if (r - i >= 0 && r - i < BW) s -= V[i][r - i] * q[i];
-    if (r < w) zr[r] = s;
+    if (r < w) zr[(long long)r * M.ldz] = s;
   }
 }
 
@@ -203,8 +205,8 @@ KFAC_API long long kfac_q2_t_floats(int n) {
   return (long long)std::max(1, q2_G(n)) * std::max(1, q2_jmax(n)) * BW * BW;
 }
 
-// Z (n rows = eigenvectors of the tridiagonal matrix, ldz) <- Q2 Z for every
-// matrix of the batch.
+// Z (component-major: row r = component r of all n eigenvectors of the
+// tridiagonal matrix, ldz) <- Q2 Z for every matrix of the batch.
 KFAC_API int kfac_q2_batched(const KfacQ2Record* recs, int count, int use_graph,
                              hipStream_t stream) {
   if (count <= 0) return 0;

@@ -148,6 +148,21 @@ __device__ bool sb_task(float* Lb, int n, int s, int j, AS1 float* v2row, int la
   return true;
 }
 
+// Cross-workgroup data (band columns, progress counters) moves through
+// agent-scope RELAXED atomics: on gfx950 these are plain loads / stores with
+// the coherence bit, which write through / read around the per-XCD L2, so no
+// L2 writeback or invalidate (what agent-scope acquire / release fences cost,
+// every tick, for every workgroup) is needed.  Ordering: the writer waits for
+// its band stores to complete (s_waitcnt) before the barrier that precedes
+// the counter store; the reader loads band columns only after the barrier
+// that follows its counter load.
+__device__ __forceinline__ float band_ld(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void band_st(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ int task_min_col(int s, int j) {
   return j == 0 ? s : s + 1 + (j - 1) * BW;
 }
@@ -156,7 +171,7 @@ __device__ __forceinline__ int task_min_col(int s, int j) {
 // published columns < need; false on timeout
 __device__ bool wait_prog(const int* prog, int need) {
   for (int it = 0; it < SPIN_MAX; ++it) {
-    if (__hip_atomic_load(prog, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= need) return true;
+    if (__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) return true;
     __builtin_amdgcn_s_sleep(4);
   }
   return false;
@@ -172,7 +187,6 @@ __global__ __launch_bounds__(1024) void sb2st_kernel(const SbMat* __restrict__ m
   const SbWg W = wgs[blockIdx.x];
   const SbMat M = mats[W.mat];
   const int n = M.n, g = W.g, s0 = g * NSW;
-  AS1 float* const band = gptr(M.band);
   const int* prev = g > 0 ? M.prog + g - 1 : nullptr;
   int* const mine = M.prog + g;
   if (tid < NSW) s_done[tid] = (s0 + tid > n - 2) ? 1 : 0;
@@ -185,15 +199,15 @@ __global__ __launch_bounds__(1024) void sb2st_kernel(const SbMat* __restrict__ m
   }
   __syncthreads();
   if (s_flag) {
-    if (tid == 0) __hip_atomic_store(mine, n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_store(mine, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  for (int c = s0 + cl; c < min(n, s0 + 3 * BW); c += 32) LB(Lb, c + dl, c) = band[(long long)c * ND + dl];
+  for (int c = s0 + cl; c < min(n, s0 + 3 * BW); c += 32)
+    LB(Lb, c + dl, c) = band_ld(M.band + (long long)c * ND + dl);
   float pre[2];
   {
     const int c = s0 + 3 * BW + (tid >> 5);
-    pre[1] = (tid < BW * ND && c < n) ? band[(long long)c * ND + dl] : 0.f;
+    pre[1] = (tid < BW * ND && c < n) ? band_ld(M.band + (long long)c * ND + dl) : 0.f;
     pre[0] = 0.f;
   }
   int retired = s0;
@@ -208,9 +222,8 @@ __global__ __launch_bounds__(1024) void sb2st_kernel(const SbMat* __restrict__ m
       }
       __syncthreads();
       if (s_flag) break;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       const int c = pc0 + (tid >> 5);
-      const float vv = (tid < BW * ND && c < n) ? band[(long long)c * ND + dl] : 0.f;
+      const float vv = (tid < BW * ND && c < n) ? band_ld(M.band + (long long)c * ND + dl) : 0.f;
       if (t & 1) pre[1] = vv; else pre[0] = vv;
     }
     // (2) one step of every active sweep (disjoint regions within the tick)
@@ -242,16 +255,18 @@ __global__ __launch_bounds__(1024) void sb2st_kernel(const SbMat* __restrict__ m
     bound = min(bound, min(n, s0 + (t + LAG) * BW));   // never past the committed columns
     if (all_done) bound = n;
     if (bound > retired) {
-      for (int c = retired + cl; c < bound; c += 32) band[(long long)c * ND + dl] = LB(Lb, c + dl, c);
+      for (int c = retired + cl; c < bound; c += 32)
+        band_st(M.band + (long long)c * ND + dl, LB(Lb, c + dl, c));
       retired = bound;
+      __builtin_amdgcn_s_waitcnt(0);     // this wave's band stores have completed
       __syncthreads();
-      if (tid == 0) __hip_atomic_store(mine, retired, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0) __hip_atomic_store(mine, retired, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (all_done) return;
     __syncthreads();
   }
   // abort path: release the successor (its results are garbage, err is set)
-  if (tid == 0) __hip_atomic_store(mine, n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) __hip_atomic_store(mine, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ __launch_bounds__(256) void sb2st_prep_kernel(const SbMat* __restrict__ mats) {

@@ -83,10 +83,9 @@ struct PanelCol {
 #pragma unroll
       for (int x = 0; x < BW; ++x) rowc[x] = P[0][x];
     }
-#pragma unroll
-    for (int x = c; x < BW; ++x) {
-      const float s = wave_sum(part[x]);
-      if (lane == 0) red16[wave][x] = s;
+    {
+      const float s = kfac_butterfly16(part);       // lane x (< 16): value x
+      if (lane < BW) red16[wave][lane] = s;
     }
     __syncthreads();
     if (tid < BW && tid >= c) {
@@ -201,10 +200,9 @@ __global__ __launch_bounds__(PT) void sy2sb_panel_kernel(const S1Mat* __restrict
 #pragma unroll
       for (int b = a; b < BW; ++b) gp[b] += va * P[q][b];
     }
-#pragma unroll
-    for (int b = a; b < BW; ++b) {
-      const float s = wave_sum(gp[b]);
-      if (lane == 0) gred[wave][a * BW + b] = s;
+    {
+      const float s = kfac_butterfly16(gp);
+      if (lane < BW) gred[wave][a * BW + lane] = s;
     }
   }
   __syncthreads();

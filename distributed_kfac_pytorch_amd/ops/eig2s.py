@@ -77,6 +77,7 @@ def _extra_buffers(dev, n, b, slot):
                  prog=torch.zeros(b, int(L.kfac_sb2st_nwg(n)) + 1, dtype=torch.int32, device=dev),
                  s1ws=torch.zeros(b, int(L.kfac_sy2sb_ws_floats(n)) + 64, **f32),
                  tq2=torch.zeros(b, int(L.kfac_q2_t_floats(n)), **f32),
+                 zc=torch.zeros(b, n, (n + 63) // 64 * 64, **f32),
                  err=torch.zeros(1, dtype=torch.int32, device=dev))
         _BUFS[key] = X
     return X
@@ -125,13 +126,17 @@ def two_stage_group(mats, clip, stream, use_graph=True, slot=0):
                 dc[k] = dcr[i]
                 r = q2[k]
                 r.v2, r.ldv2 = X['v2'][i].data_ptr(), X['ldv2']
-                r.Z, r.ldz, r.T, r.n = B['Z'][i].data_ptr(), lda, X['tq2'][i].data_ptr(), n
+                r.Z, r.ldz, r.T, r.n = X['zc'][i].data_ptr(), lda, X['tq2'][i].data_ptr(), n
                 k += 1
         err.zero_()
         _lib.check(L.kfac_sy2sb_batched(s1, total, int(use_graph), cs), 'kfac_sy2sb_batched')
         _lib.check(L.kfac_sb2st_batched(sb, total, err.data_ptr(), cs), 'kfac_sb2st_batched')
         _lib.check(L.kfac_dc_batched(dc, total, int(use_graph), cs), 'kfac_dc_batched')
+        for n, idx, B, X in bufs:     # eigenvector rows -> component rows (coalesced Q2)
+            X['zc'][:, :, :n].copy_(B['Z'][:, :, :n].transpose(1, 2))
         _lib.check(L.kfac_q2_batched(q2, total, int(use_graph), cs), 'kfac_q2_batched')
+        for n, idx, B, X in bufs:
+            B['Z'][:, :, :n].copy_(X['zc'][:, :, :n].transpose(1, 2))
         for n, idx, B, X in bufs:
             b = len(idx)
             _lib.check(L.kfac_backtransform_shift(*eigen._bt_args(B, n, b), BW, int(use_graph), cs),
