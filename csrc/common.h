@@ -179,3 +179,13 @@ __device__ __forceinline__ float kfac_butterfly16(float (&v)[16]) {
   r += __shfl_xor(r, 32, 64);
   return r;
 }
+
+// Workgroup barrier for LDS traffic only: waits for this wave's LDS
+// operations (lgkmcnt) but NOT for its outstanding global loads / stores, so
+// prefetches stay in flight across it (__syncthreads() is a workgroup-scope
+// release + acquire, which on gfx950 also drains vmcnt).  Callers order any
+// global data themselves (s_waitcnt before publishing, register dependencies
+// for loaded values).
+__device__ __forceinline__ void kfac_lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}

@@ -7,14 +7,14 @@
 // staggered reflectors starting at row 16 g + 1 + 16 j.  Q2 Z applies the
 // blocks g descending and, inside a block, j ascending; group (g, j) at tick
 // (G-1-g) + j keeps that order and the groups of one tick touch disjoint row
-// windows (scripts/models/two_stage_model.py: apply_q2_ticks), so one launch
-// per tick applies every group of the tick to every eigenvector, for every
-// matrix of the batch (~2 n / 16 launches, captured in a hipGraph).
+// windows (scripts/models/two_stage_model.py: apply_q2_ticks).
 //
-//   q2_t      one wave per group: Gram of the window, T (larft, forward)
-//   q2_apply  one workgroup per (group, 256 eigenvectors): a thread holds one
-//             eigenvector's 31-row window in VGPRs; V and T from LDS
-//             (broadcast reads): P = V^T z, P = T P, z -= V P
+//   q2_t     one wave per group: Gram of the window, T (larft, forward)
+//   q2_pass  one workgroup per (matrix, 64 eigenvectors), lane = eigenvector;
+//            8 blocks per pass in the tick order (wave w = block gtop - w),
+//            the touched rows streaming through an LDS window, so Z is read
+//            and written once per pass rather than once per group (a launch
+//            per tick over global memory was 30x slower on ResNet-50)
 #include "common.h"
 
 #include <algorithm>
@@ -28,7 +28,6 @@ namespace {
 
 constexpr int BW = 16;
 constexpr int WR = 2 * BW - 1;     // window rows
-constexpr int ST = 256;            // eigenvectors per apply workgroup
 constexpr int MAXM = 255;
 
 struct Q2Mat {
@@ -60,7 +59,7 @@ __device__ __forceinline__ bool has_step(int n, int s, int j) {
 __device__ __forceinline__ float refl_v(const Q2Mat& M, int g, int j, int i, int l, float* tau) {
   const int s = BW * g + i;
   if (!has_step(M.n, s, j)) { if (tau) *tau = 0.f; return 0.f; }
-  const float* row = M.v2 + (long long)s * M.ldv2 + BW * j;
+  const AS1 float* row = gptr(M.v2) + (long long)s * M.ldv2 + BW * j;
   if (tau) *tau = row[0];
   return l == 0 ? 1.f : row[l];
 }
@@ -108,65 +107,135 @@ __global__ __launch_bounds__(64) void q2_t_kernel(const Q2Mat* __restrict__ mats
   for (int e = lane; e < BW * BW; e += 64) out[e] = T[e / BW][e % BW];
 }
 
-__global__ __launch_bounds__(ST) void q2_apply_kernel(const Q2Mat* __restrict__ mats,
-                                                      const int* __restrict__ offs,
-                                                      const int* __restrict__ jlo, int nact,
-                                                      int tick) {
-  __shared__ int soff[MAXM + 1];
-  __shared__ float V[BW][BW];
-  __shared__ float T[BW][BW];
-  int mi, local;
-  map_block(offs, nact, soff, mi, local);
-  const Q2Mat M = mats[mi];
-  const int task = local / M.nstrips, strip = local % M.nstrips;
-  const int j = jlo[mi] + task;
-  const int g = M.G - 1 - tick + j;
-  const int tid = threadIdx.x;
-  if (g < 0 || g >= M.G || j >= M.jmax || !has_step(M.n, BW * g, j)) return;   // uniform
-  {
-    const int i = tid / BW, l = tid % BW;
-    V[i][l] = refl_v(M, g, j, i, l, nullptr);
-    T[i][l] = M.T[((long long)g * M.jmax + j) * BW * BW + tid];
-  }
-  __syncthreads();
-  const int e = strip * ST + tid;
-  if (e >= M.n) return;
-  const int row0 = BW * g + 1 + BW * j;
-  const int w = min(WR, M.n - row0);
-  // Z is component-major here (row r = component r of every eigenvector):
-  // a wave's loads of one component are 64 consecutive floats
-  AS1 float* const zr = gptr(M.Z) + (long long)row0 * M.ldz + e;
-  float z[WR];
+// One workgroup per (matrix, 64 eigenvectors): lane = eigenvector.  Blocks
+// are processed QW at a time ("passes", g descending); inside a pass wave w
+// owns block gtop - w and runs its step tau - w at tick tau, so the pass is
+// the tick order of the groups it contains.  The rows the pass touches stream
+// through a circular LDS window (ZR rows x 64 eigenvectors): every element of
+// Z is read and written once per pass instead of once per group.
+constexpr int QW = 8;
+constexpr int ZR = 512;
+struct Q2Strip { int mat, e0; };
+
+__device__ __forceinline__ int q2_steps(int n, int g) {      // J_g
+  return (BW * g <= n - 3) ? (n - 3 - BW * g) / BW + 1 : 0;
+}
+
+__global__ __launch_bounds__(QW * 64) void q2_pass_kernel(const Q2Mat* __restrict__ mats,
+                                                          const Q2Strip* __restrict__ strips) {
+  extern __shared__ float Lz[];                 // ZR x 64: row r at (r % ZR) * 64
+  __shared__ float sV[QW][BW][BW];
+  __shared__ float sT[QW][BW][BW];
+  const Q2Strip S = strips[blockIdx.x];
+  const Q2Mat M = mats[S.mat];
+  const int n = M.n, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int e = S.e0 + lane;
+  const bool eok = e < n;
+  AS1 float* const Zg = gptr(M.Z);
+  auto zrow = [&](int r) -> float {   // Z element (row r, this lane's eigenvector)
+    return eok ? Zg[(long long)r * M.ldz + e] : 0.f;
+  };
+  for (int gtop = M.G - 1; gtop >= 0; gtop -= QW) {
+    const int glow = max(0, gtop - QW + 1);
+    const int rlo = BW * glow + 1;
+    int stored = rlo;
+    int nticks = 0;
+    for (int w = 0; w <= gtop - glow; ++w) nticks = max(nticks, w + q2_steps(n, gtop - w));
+    // rows needed by tick tau: < need(tau) = min(n, 16 (gtop + tau) + 32); tick 0's
+    // rows load synchronously, later ticks' 16 new rows (2 per wave) are loaded
+    // one tick ahead into registers; so are each wave's V / T for its next group
+    const int need0 = min(n, BW * gtop + 2 * BW);
+    for (int r = rlo + wave; r < need0; r += QW) Lz[(r & (ZR - 1)) * 64 + lane] = zrow(r);
+    int loaded = need0;
+    float pz0 = 0.f, pz1 = 0.f, pv[4], pt[4];
+    auto load_vt = [&](int tau) {
+      const int g = gtop - wave, j = tau - wave;
+      const bool ok = g >= glow && j >= 0 && j < q2_steps(n, g);
 #pragma unroll
-  for (int r = 0; r < WR; ++r) z[r] = gld_if(zr, (long long)r * M.ldz, r < w, 0.f);
-  float p[BW];
+      for (int k = 0; k < 4; ++k) {
+        const int idx = lane + 64 * k;
+        pv[k] = ok ? refl_v(M, g, j, idx / BW, idx % BW, nullptr) : 0.f;
+        pt[k] = ok ? gptr(M.T)[((long long)g * M.jmax + j) * BW * BW + idx] : 0.f;
+      }
+    };
+    load_vt(0);
+    for (int tau = 0; tau < nticks; ++tau) {
+      // V / T of this tick to the wave's LDS slot, next tick's issued
 #pragma unroll
-  for (int i = 0; i < BW; ++i) {
-    float s = 0.f;
+      for (int k = 0; k < 4; ++k) {
+        const int idx = lane + 64 * k;
+        sV[wave][idx / BW][idx % BW] = pv[k];
+        sT[wave][idx / BW][idx % BW] = pt[k];
+      }
+      load_vt(tau + 1);
+      const int need1 = min(n, BW * (gtop + tau + 1) + 2 * BW);   // rows of tick tau + 1
+      {
+        const int r0 = loaded + wave, r1 = loaded + wave + QW;
+        pz0 = r0 < need1 ? zrow(r0) : 0.f;
+        pz1 = r1 < need1 ? zrow(r1) : 0.f;
+      }
+      kfac_lds_barrier();      // previous tick's commits visible
+      const int g = gtop - wave, j = tau - wave;
+      if (g >= glow && j >= 0 && j < q2_steps(n, g)) {
+        const int row0 = BW * (g + j) + 1;
+        const int wr = min(WR, n - row0);
+        float z[WR];
 #pragma unroll
-    for (int l = 0; l < BW; ++l) s += V[i][l] * z[i + l];
-    p[i] = s;
-  }
-  float q[BW];
+        for (int r = 0; r < WR; ++r) z[r] = r < wr ? Lz[((row0 + r) & (ZR - 1)) * 64 + lane] : 0.f;
+        float p[BW];
 #pragma unroll
-  for (int i = 0; i < BW; ++i) {
-    float s = 0.f;
+        for (int i = 0; i < BW; ++i) {
+          float s_ = 0.f;
 #pragma unroll
-    for (int k = i; k < BW; ++k) s += T[i][k] * p[k];
-    q[i] = s;
-  }
+          for (int l = 0; l < BW; ++l) s_ += sV[wave][i][l] * z[i + l];
+          p[i] = s_;
+        }
+        float q[BW];
 #pragma unroll
-  for (int r = 0; r < WR; ++r) {
-    float s = z[r];
+        for (int i = 0; i < BW; ++i) {
+          float s_ = 0.f;
 #pragma unroll
-    for (int i = 0; i < BW; ++i)
-      if (r - i >= 0 && r - i < BW) s -= V[i][r - i] * q[i];
-    if (r < w) zr[(long long)r * M.ldz] = s;
+          for (int k = i; k < BW; ++k) s_ += sT[wave][i][k] * p[k];
+          q[i] = s_;
+        }
+#pragma unroll
+        for (int r = 0; r < WR; ++r) {
+          float s_ = z[r];
+#pragma unroll
+          for (int i = 0; i < BW; ++i)
+            if (r - i >= 0 && r - i < BW) s_ -= sV[wave][i][r - i] * q[i];
+          if (r < wr) Lz[((row0 + r) & (ZR - 1)) * 64 + lane] = s_;
+        }
+      }
+      // commit the rows of tick tau + 1 (not touched at tick tau: beyond need(tau))
+      {
+        const int r0 = loaded + wave, r1 = loaded + wave + QW;
+        if (r0 < need1) Lz[(r0 & (ZR - 1)) * 64 + lane] = pz0;
+        if (r1 < need1) Lz[(r1 & (ZR - 1)) * 64 + lane] = pz1;
+        loaded = max(loaded, need1);
+      }
+      kfac_lds_barrier();
+      // rows no later step of the pass touches go back to global memory
+      int lo = n;
+      for (int w = 0; w <= gtop - glow; ++w) {
+        const int gw = gtop - w, jn = max(tau + 1 - w, 0);
+        if (jn < q2_steps(n, gw)) lo = min(lo, BW * (gw + jn) + 1);
+      }
+      lo = min(lo, loaded);
+      for (int r = stored + wave; r < lo; r += QW)
+        if (eok) Zg[(long long)r * M.ldz + e] = Lz[(r & (ZR - 1)) * 64 + lane];
+      stored = max(stored, lo);
+    }
+    for (int r = stored + wave; r < loaded; r += QW)
+      if (eok) Zg[(long long)r * M.ldz + e] = Lz[(r & (ZR - 1)) * 64 + lane];
+    __syncthreads();
   }
 }
 
 struct Q2Plan {
   Q2Mat* d_mats = nullptr;
+  Q2Strip* d_strips = nullptr;
+  int nstrip = 0;
   int* d_offs = nullptr;      // [ticks + 1][nm + 1]: [0] = T kernel, [1 + t] = tick t
   int* d_jlo = nullptr;       // [ticks][nm]
   int count = 0, ticks = 0;
@@ -175,16 +244,12 @@ struct Q2Plan {
 };
 
 int enqueue(const Q2Plan& P, hipStream_t stream) {
-  const int nm = P.count;
   if (P.grid[0] > 0)
     hipLaunchKernelGGL(q2_t_kernel, dim3(P.grid[0]), dim3(64), 0, stream, P.d_mats, P.d_offs,
                        P.nact[0]);
-  for (int t = 0; t < P.ticks; ++t) {
-    if (P.grid[1 + t] == 0) continue;
-    hipLaunchKernelGGL(q2_apply_kernel, dim3(P.grid[1 + t]), dim3(ST), 0, stream, P.d_mats,
-                       P.d_offs + (size_t)(1 + t) * (nm + 1), P.d_jlo + (size_t)t * nm,
-                       P.nact[1 + t], t);
-  }
+  if (P.nstrip > 0)
+    hipLaunchKernelGGL(q2_pass_kernel, dim3(P.nstrip), dim3(QW * 64), ZR * 64 * sizeof(float),
+                       stream, P.d_mats, P.d_strips);
   return (int)hipGetLastError();
 }
 
@@ -218,7 +283,7 @@ KFAC_API int kfac_q2_batched(const KfacQ2Record* recs, int count, int use_graph,
     Q2Mat& M = mats[i];
     memset(&M, 0, sizeof(M));
     M.v2 = r.v2; M.ldv2 = r.ldv2; M.Z = r.Z; M.ldz = r.ldz; M.T = r.T; M.n = (int)r.n;
-    M.G = q2_G(M.n); M.jmax = q2_jmax(M.n); M.nstrips = (M.n + ST - 1) / ST;
+    M.G = q2_G(M.n); M.jmax = q2_jmax(M.n); M.nstrips = (M.n + 63) / 64;
   }
   const std::string key((const char*)mats.data(), sizeof(Q2Mat) * mats.size());
   std::lock_guard<std::mutex> lk(g_mu);
@@ -265,6 +330,20 @@ KFAC_API int kfac_q2_batched(const KfacQ2Record* recs, int count, int use_graph,
     if (!e) e = (int)hipMemcpy(P.d_offs, offs.data(), sizeof(int) * offs.size(), hipMemcpyHostToDevice);
     if (!e) e = (int)hipMalloc(&P.d_jlo, sizeof(int) * jl.size());
     if (!e) e = (int)hipMemcpy(P.d_jlo, jl.data(), sizeof(int) * jl.size(), hipMemcpyHostToDevice);
+    std::vector<Q2Strip> strips;
+    for (int i = 0; i < nm; ++i)
+      for (int e0 = 0; e0 < mats[i].n; e0 += 64) strips.push_back(Q2Strip{i, e0});
+    P.nstrip = (int)strips.size();
+    if (!e) e = (int)hipMalloc(&P.d_strips, sizeof(Q2Strip) * strips.size());
+    if (!e) e = (int)hipMemcpy(P.d_strips, strips.data(), sizeof(Q2Strip) * strips.size(),
+                               hipMemcpyHostToDevice);
+    static bool attr = false;
+    if (!e && !attr) {
+      e = (int)hipFuncSetAttribute((const void*)q2_pass_kernel,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   ZR * 64 * (int)sizeof(float));
+      attr = (e == 0);
+    }
     if (e) return e;
     it = g_plans.emplace(key, P).first;
   }

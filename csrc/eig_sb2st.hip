@@ -49,7 +49,9 @@ constexpr int BW = 16;             // half-bandwidth of the stage-1 band
 constexpr int ND = 2 * BW;         // stored diagonals per column (band + bulge room)
 constexpr int NSW = 16;            // sweeps (waves) per workgroup
 constexpr int WIN = 1024;          // LDS window columns (circular)
-constexpr int LAG = 4;             // band block prefetched LAG ticks ahead
+constexpr int PD = 6;              // prefetch register sets: a band block is in flight PD-1 ticks
+constexpr int LAG = PD + 1;        // band block prefetched LAG ticks ahead
+constexpr int RET = 8;             // columns retired / published every RET ticks
 constexpr int SPIN_MAX = 1 << 22;  // bounded waits (~1 s): a lost predecessor cannot hang the GPU
 
 struct SbMat {
@@ -62,12 +64,34 @@ struct SbMat {
 };
 struct SbWg { int mat, g; };
 
+// debug: phase stamps (s_memrealtime, 100 MHz) of one workgroup's first ticks
+__device__ unsigned long long* g_sb_stamps = nullptr;
+__device__ int g_sb_stamp_wg = 0;
+#define SB_STAMP(k)                                                                 \
+  do {                                                                              \
+    if (stamps && tid == 0 && t < 512) stamps[t * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
 __device__ __forceinline__ float& LB(float* Lb, int r, int c) {
   return Lb[((c & (WIN - 1)) * ND) + (r - c)];
 }
 
+// sum over the 16-lane row of the wave (DPP only; every lane of the row ends
+// with the row's sum)
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dpp_f<0xB1>(v);     // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);     // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);    // row_half_mirror
+  v += dpp_f<0x140>(v);    // row_mirror
+  return v;
+}
+
 // one bulge-chasing step of sweep s, by one wave; false when the sweep has
-// run off the end of the matrix
+// run off the end of the matrix.  After the reflector (lanes 0..15), the
+// three independent updates run side by side on the wave's 16-lane rows:
+// lanes 0..15 the diagonal block (both sides), 16..31 the bulge block
+// (left), 32..47 the block below (right) -- one pass of 16 LDS loads and
+// stores instead of three.
 __device__ bool sb_task(float* Lb, int n, int s, int j, AS1 float* v2row, int lane) {
   const int c = j == 0 ? s : s + 1 + (j - 1) * BW;
   const int r0 = s + 1 + j * BW;
@@ -90,60 +114,46 @@ __device__ bool sb_task(float* Lb, int n, int s, int j, AS1 float* v2row, int la
   float vl[BW];
 #pragma unroll
   for (int l = 0; l < BW; ++l) vl[l] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-  // left: bulge block columns c+1 .. r0-1 (BW-1 of them for j >= 1)
-  const int nq = r0 - 1 - c;
-  if (lane < nq) {
-    const int q = c + 1 + lane;
-    float col[BW];
-    float y = 0.f;
+  const int grp = lane >> 4, li = lane & 15;
+  const int nq = r0 - 1 - c;                     // bulge block columns (BW-1 for j >= 1)
+  const int nE = min(BW, n - 1 - r1);            // rows below R in the band
+  // per-lane element (row, col) of entry l, and whether this lane is active
+  bool act;
+  if (grp == 0) act = li < L;
+  else if (grp == 1) act = li < nq;
+  else if (grp == 2) act = li < nE;
+  else act = false;
+  float val[BW];
+  float acc = 0.f;
 #pragma unroll
-    for (int l = 0; l < BW; ++l) {
-      col[l] = l < L ? LB(Lb, r0 + l, q) : 0.f;
-      y += vl[l] * col[l];
-    }
-    y *= tau;
-#pragma unroll
-    for (int l = 0; l < BW; ++l)
-      if (l < L) LB(Lb, r0 + l, q) = col[l] - y * vl[l];
+  for (int l = 0; l < BW; ++l) {
+    int rr, cc;
+    if (grp == 0) { rr = r0 + max(li, l); cc = r0 + min(li, l); }
+    else if (grp == 1) { rr = r0 + l; cc = c + 1 + li; }
+    else { rr = r1 + 1 + li; cc = r0 + l; }
+    const bool ok = act && l < L;
+    val[l] = ok ? LB(Lb, rr, cc) : 0.f;
+    acc += val[l] * vl[l];
   }
-  // both sides: diagonal block D = B[R, R] (symmetric, lower stored)
-  {
-    const int a = lane;
-    float row[BW];
-    float p = 0.f;
+  acc *= tau;                                    // p (diag lanes), y (bulge), z (below)
+  // diagonal block: w = p - tau/2 (p . v) v over the 16-lane row
+  const float va = (grp == 0 && li < L) ? v : 0.f;
+  const float pv = row_sum16(acc * va);
+  const float w = (grp == 0 && li < L) ? acc - 0.5f * tau * pv * va : 0.f;
+  float wl[BW];
 #pragma unroll
-    for (int l = 0; l < BW; ++l) {
-      const bool ok = a < L && l < L;
-      const int hi = a > l ? a : l, lo = a > l ? l : a;
-      row[l] = ok ? LB(Lb, r0 + hi, r0 + lo) : 0.f;
-      p += row[l] * vl[l];
-    }
-    p *= tau;
-    const float va = (a < L) ? v : 0.f;          // this lane's v[a]
-    const float pv = wave_sum(p * va);
-    const float w = a < L ? p - 0.5f * tau * pv * va : 0.f;
-    float wl[BW];
+  for (int l = 0; l < BW; ++l) wl[l] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), l));
+  // new = val - c1 X[l] - c2 v[l]:  diag: c1 = v_a, X = w, c2 = w_a;  others: c1 = 0, c2 = acc
+  const float c1 = grp == 0 ? va : 0.f;
+  const float c2 = grp == 0 ? w : acc;
 #pragma unroll
-    for (int l = 0; l < BW; ++l) wl[l] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), l));
-#pragma unroll
-    for (int l = 0; l < BW; ++l)
-      if (a < L && l <= a) LB(Lb, r0 + a, r0 + l) = row[l] - va * wl[l] - w * vl[l];
-  }
-  // right: rows r1+1 .. r1+BW of columns R (creates the next bulge)
-  const int nE = min(BW, n - 1 - r1);
-  if (lane < nE) {
-    const int r = r1 + 1 + lane;
-    float rw[BW];
-    float z = 0.f;
-#pragma unroll
-    for (int l = 0; l < BW; ++l) {
-      rw[l] = l < L ? LB(Lb, r, r0 + l) : 0.f;
-      z += rw[l] * vl[l];
-    }
-    z *= tau;
-#pragma unroll
-    for (int l = 0; l < BW; ++l)
-      if (l < L) LB(Lb, r, r0 + l) = rw[l] - z * vl[l];
+  for (int l = 0; l < BW; ++l) {
+    int rr, cc;
+    if (grp == 0) { rr = r0 + li; cc = r0 + l; }   // lower entry (li, l), l <= li
+    else if (grp == 1) { rr = r0 + l; cc = c + 1 + li; }
+    else { rr = r1 + 1 + li; cc = r0 + l; }
+    const bool ok = act && l < L && (grp != 0 || l <= li);
+    if (ok) LB(Lb, rr, cc) = val[l] - c1 * wl[l] - c2 * vl[l];
   }
   return true;
 }
@@ -156,11 +166,13 @@ __device__ bool sb_task(float* Lb, int n, int s, int j, AS1 float* v2row, int la
 // its band stores to complete (s_waitcnt) before the barrier that precedes
 // the counter store; the reader loads band columns only after the barrier
 // that follows its counter load.
+// Global (not flat) address space: a flat load also counts in lgkmcnt, so
+// every LDS wait of the tick would wait for the band prefetches too.
 __device__ __forceinline__ float band_ld(const float* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_load(gptr(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void band_st(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(gptr(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ int task_min_col(int s, int j) {
@@ -168,13 +180,14 @@ __device__ __forceinline__ int task_min_col(int s, int j) {
 }
 
 // wait (thread 0 only) until the previous workgroup of this matrix has
-// published columns < need; false on timeout
-__device__ bool wait_prog(const int* prog, int need) {
+// published columns < need; the published value, or -1 on timeout
+__device__ int wait_prog(const int* prog, int need) {
   for (int it = 0; it < SPIN_MAX; ++it) {
-    if (__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) return true;
+    const int v = __hip_atomic_load(gptr(prog), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v >= need) return v;
     __builtin_amdgcn_s_sleep(4);
   }
-  return false;
+  return -1;
 }
 
 __global__ __launch_bounds__(1024) void sb2st_kernel(const SbMat* __restrict__ mats,
@@ -183,90 +196,121 @@ __global__ __launch_bounds__(1024) void sb2st_kernel(const SbMat* __restrict__ m
   extern __shared__ float Lb[];                 // WIN x ND
   __shared__ int s_done[NSW];
   __shared__ int s_flag;
+  __shared__ int s_pc;                          // last seen progress of the previous workgroup
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const SbWg W = wgs[blockIdx.x];
   const SbMat M = mats[W.mat];
+  unsigned long long* const stamps = ((int)blockIdx.x == g_sb_stamp_wg) ? g_sb_stamps : nullptr;
   const int n = M.n, g = W.g, s0 = g * NSW;
   const int* prev = g > 0 ? M.prog + g - 1 : nullptr;
   int* const mine = M.prog + g;
   if (tid < NSW) s_done[tid] = (s0 + tid > n - 2) ? 1 : 0;
-  if (tid == 0) s_flag = 0;
-  // columns [s0, s0 + 3 BW) synchronously, block 3 into register set 1
-  const int cl = tid >> 5, dl = tid & 31;       // thread's (column, diagonal) in a 32-column slab
-  if (tid == 0 && prev && !wait_prog(prev, min(n, s0 + 4 * BW))) {
-    s_flag = 1;
-    atomicOr(err, 1);
-  }
-  __syncthreads();
-  if (s_flag) {
-    if (tid == 0) __hip_atomic_store(mine, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  for (int c = s0 + cl; c < min(n, s0 + 3 * BW); c += 32)
-    LB(Lb, c + dl, c) = band_ld(M.band + (long long)c * ND + dl);
-  float pre[2];
-  {
-    const int c = s0 + 3 * BW + (tid >> 5);
-    pre[1] = (tid < BW * ND && c < n) ? band_ld(M.band + (long long)c * ND + dl) : 0.f;
-    pre[0] = 0.f;
-  }
-  int retired = s0;
-  __syncthreads();
-  for (int t = 0;; ++t) {
-    // (1) prefetch block t + LAG into set t & 1 (published by the previous workgroup)
-    const int pc0 = s0 + (t + LAG) * BW;
-    if (pc0 < n) {
-      if (tid == 0 && prev && !wait_prog(prev, min(n, pc0 + BW))) {
+  if (tid == 0) {
+    s_flag = 0;
+    s_pc = n;
+    if (prev) {
+      s_pc = wait_prog(prev, min(n, s0 + LAG * BW));
+      if (s_pc < 0) {
         s_flag = 1;
         atomicOr(err, 1);
       }
-      __syncthreads();
-      if (s_flag) break;
-      const int c = pc0 + (tid >> 5);
-      const float vv = (tid < BW * ND && c < n) ? band_ld(M.band + (long long)c * ND + dl) : 0.f;
-      if (t & 1) pre[1] = vv; else pre[0] = vv;
     }
-    // (2) one step of every active sweep (disjoint regions within the tick)
-    {
-      const int s = s0 + wave, j = t - 3 * wave;
-      if (!s_done[wave] && j >= 0) {
-        const bool more = sb_task(Lb, n, s, j, gptr(M.v2) + (long long)s * M.ldv2, lane);
-        if (!more && lane == 0) s_done[wave] = 1;
-      }
-    }
-    __syncthreads();
-    // (3) commit block t + LAG - 1 (loaded during the previous tick)
-    {
-      const int cc0 = s0 + (t + LAG - 1) * BW;
-      const int c = cc0 + (tid >> 5);
-      if (cc0 < n && tid < BW * ND && c < n) LB(Lb, c + dl, c) = ((t + 1) & 1) ? pre[1] : pre[0];
-    }
-    __syncthreads();
-    // (4) retire: columns below every unfinished sweep's next task
-    int all_done = 1, bound = n;
-#pragma unroll
-    for (int w = 0; w < NSW; ++w) {
-      if (!s_done[w]) {
-        all_done = 0;
-        const int jn = max(t + 1 - 3 * w, 0);
-        bound = min(bound, task_min_col(s0 + w, jn));
-      }
-    }
-    bound = min(bound, min(n, s0 + (t + LAG) * BW));   // never past the committed columns
-    if (all_done) bound = n;
-    if (bound > retired) {
-      for (int c = retired + cl; c < bound; c += 32)
-        band_st(M.band + (long long)c * ND + dl, LB(Lb, c + dl, c));
-      retired = bound;
-      __builtin_amdgcn_s_waitcnt(0);     // this wave's band stores have completed
-      __syncthreads();
-      if (tid == 0) __hip_atomic_store(mine, retired, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (all_done) return;
-    __syncthreads();
   }
-  // abort path: release the successor (its results are garbage, err is set)
-  if (tid == 0) __hip_atomic_store(mine, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int cl = tid >> 5, dl = tid & 31;       // thread's (column, diagonal) in a 32-column slab
+  __syncthreads();
+  if (s_flag) {
+    if (tid == 0) __hip_atomic_store(gptr(mine), n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  // Band block b (columns s0 + 16 b ..) is loaded at tick b - LAG into
+  // register set (b - LAG) mod PD and committed to LDS at the end of tick
+  // b - LAG + PD - 1; wave 0 needs it at tick b - 1.  Blocks 0 .. LAG-PD load
+  // synchronously, LAG-PD+1 .. LAG-1 are issued before tick 0.
+  const bool pth = tid < BW * ND;               // threads that move band data (16 columns x 32)
+  for (int c = s0 + cl; c < min(n, s0 + (LAG - PD + 1) * BW); c += 32)
+    LB(Lb, c + dl, c) = band_ld(M.band + (long long)c * ND + dl);
+  float pre[PD];
+#pragma unroll
+  for (int u = 0; u < PD; ++u) pre[u] = 0.f;
+#pragma unroll
+  for (int u = 1; u < PD; ++u) {                // set u <- block LAG - PD + u
+    const int c = s0 + (LAG - PD + u) * BW + (tid >> 5);
+    if (pth && c < n) pre[u] = band_ld(M.band + (long long)c * ND + dl);
+  }
+  int retired = s0;
+  __syncthreads();
+  for (int t0 = 0;; t0 += PD) {
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {              // t = t0 + u, register set u is t mod PD
+      const int t = t0 + u;
+      SB_STAMP(0);
+      // (1) issue block t + LAG (published by the previous workgroup)
+      const int pc0 = s0 + (t + LAG) * BW;
+      if (pc0 < n) {
+        const int need = min(n, pc0 + BW);
+        if (need > s_pc) {             // uniform: s_pc changes only here, between barriers
+          if (tid == 0) {
+            const int v = wait_prog(prev, need);
+            if (v < 0) {
+              s_flag = 1;
+              atomicOr(err, 1);
+            } else {
+              s_pc = v;
+            }
+          }
+          __syncthreads();
+          if (s_flag) goto abort;
+        }
+        const int c = pc0 + (tid >> 5);
+        if (pth && c < n) pre[u] = band_ld(M.band + (long long)c * ND + dl);
+      }
+      SB_STAMP(1);
+      // (2) one step of every active sweep (disjoint regions within the tick)
+      {
+        const int s = s0 + wave, j = t - 3 * wave;
+        if (!s_done[wave] && j >= 0) {
+          const bool more = sb_task(Lb, n, s, j, gptr(M.v2) + (long long)s * M.ldv2, lane);
+          if (!more && lane == 0) s_done[wave] = 1;
+        }
+      }
+      kfac_lds_barrier();
+      SB_STAMP(2);
+      // (3) commit block t + LAG - PD + 1 (issued PD - 1 ticks ago, set (u + 1) mod PD)
+      {
+        const int cc0 = s0 + (t + LAG - PD + 1) * BW;
+        const int c = cc0 + (tid >> 5);
+        if (pth && c < n) LB(Lb, c + dl, c) = pre[(u + 1) % PD];
+      }
+      kfac_lds_barrier();
+      SB_STAMP(3);
+      // (4) retire: columns below every unfinished sweep's next task
+      int all_done = 1, bound = n;
+#pragma unroll
+      for (int w = 0; w < NSW; ++w) {
+        if (!s_done[w]) {
+          all_done = 0;
+          const int jn = max(t + 1 - 3 * w, 0);
+          bound = min(bound, task_min_col(s0 + w, jn));
+        }
+      }
+      bound = min(bound, min(n, s0 + (t + LAG - PD + 2) * BW));   // never past the committed columns
+      if (all_done) bound = n;
+      if (bound > retired && ((t % RET) == RET - 1 || all_done)) {
+        for (int c = retired + cl; c < bound; c += 32)
+          band_st(M.band + (long long)c * ND + dl, LB(Lb, c + dl, c));
+        retired = bound;
+        __builtin_amdgcn_s_waitcnt(0);     // this wave's band stores have completed
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(gptr(mine), retired, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      SB_STAMP(4);
+      if (all_done) return;
+      kfac_lds_barrier();
+    }
+  }
+abort:
+  // release the successor (its results are garbage, err is set)
+  if (tid == 0) __hip_atomic_store(gptr(mine), n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ __launch_bounds__(256) void sb2st_prep_kernel(const SbMat* __restrict__ mats) {
@@ -297,6 +341,13 @@ struct KfacSbRecord {
 };
 
 KFAC_API int kfac_sb2st_bw() { return BW; }
+
+// debug: stamps of workgroup `wg` (launch order) into buf (512 ticks x 8), or off
+KFAC_API int kfac_sb2st_stamps(unsigned long long* buf, int wg) {
+  int e = (int)hipMemcpyToSymbol(HIP_SYMBOL(g_sb_stamps), &buf, sizeof(buf));
+  if (!e) e = (int)hipMemcpyToSymbol(HIP_SYMBOL(g_sb_stamp_wg), &wg, sizeof(wg));
+  return e;
+}
 KFAC_API long long kfac_sb2st_ldv2(int n) { return ((long long)n + 2 * BW + 15) / 16 * 16; }
 KFAC_API int kfac_sb2st_nwg(int n) { return (n - 1 + NSW - 1) / NSW; }
 

@@ -3,8 +3,8 @@
 // factor).  Panels of BW = 16 columns; for the panel at columns k .. k+15
 // (m = n - k - 16 rows below the band):
 //
-//   panel  one 1024-thread workgroup per matrix: Householder QR of
-//          A[k+16:, k:k+16] held in registers (<= 5 rows x 16 per thread),
+//   panel  one 512-thread workgroup per matrix: Householder QR of
+//          A[k+16:, k:k+16] held in registers (<= 10 rows x 16 per thread),
 //          one block reduction per column (the column's |x|^2 and its dots
 //          with the later columns together), Gram V^T V, T (larft) and
 //          U^T = (V T)^T; R to the band, v[1:] of reflector k+c to row k+c
@@ -62,74 +62,6 @@ __device__ inline void map_block(const int* __restrict__ offs, int nact, int* so
 }
 
 
-// one column of the panel QR, compile-time column index (P stays in VGPRs)
-template <int C>
-struct PanelCol {
-  static __device__ __forceinline__ void run(float (&P)[RQ][BW], int tid, int lane, int wave,
-                                             int m, float (*red16)[BW], float* red, float* rowc,
-                                             float* taus) {
-    constexpr int c = C;
-    float part[BW];
-#pragma unroll
-    for (int x = 0; x < BW; ++x) part[x] = 0.f;
-#pragma unroll
-    for (int q = 0; q < RQ; ++q) {
-      const int i = tid + PT * q;
-      const float xc = (i > c && i < m) ? P[q][c] : 0.f;
-#pragma unroll
-      for (int x = c; x < BW; ++x) part[x] += xc * P[q][x];
-    }
-    if (tid == c) {
-#pragma unroll
-      for (int x = 0; x < BW; ++x) rowc[x] = P[0][x];
-    }
-    {
-      const float s = kfac_butterfly16(part);       // lane x (< 16): value x
-      if (lane < BW) red16[wave][lane] = s;
-    }
-    __syncthreads();
-    if (tid < BW && tid >= c) {
-      float s = 0.f;
-#pragma unroll
-      for (int w = 0; w < NWV; ++w) s += red16[w][tid];
-      red[tid] = s;
-    }
-    __syncthreads();
-    const float sig = red[c];
-    const float alpha = rowc[c];
-    float tau = 0.f, beta = alpha, scal = 0.f;
-    if (c < m - 1 && sig != 0.f) {
-      beta = -copysignf(sqrtf(alpha * alpha + sig), alpha);
-      tau = (beta - alpha) / beta;
-      scal = 1.f / (alpha - beta);
-    }
-    if (tid == 0) taus[c] = tau;
-    float wc[BW];
-#pragma unroll
-    for (int x = 0; x < BW; ++x) wc[x] = (x > c) ? tau * (rowc[x] + scal * red[x]) : 0.f;
-#pragma unroll
-    for (int q = 0; q < RQ; ++q) {
-      const int i = tid + PT * q;
-      if (i > c && i < m) {
-        const float vi = scal * P[q][c];
-#pragma unroll
-        for (int x = c + 1; x < BW; ++x) P[q][x] -= vi * wc[x];
-        P[q][c] = vi;
-      } else if (i == c) {
-#pragma unroll
-        for (int x = c + 1; x < BW; ++x) P[q][x] -= wc[x];
-        P[q][c] = beta;
-      }
-    }
-    __syncthreads();   // red / rowc reused by the next column
-    PanelCol<C + 1>::run(P, tid, lane, wave, m, red16, red, rowc, taus);
-  }
-};
-template <>
-struct PanelCol<BW> {
-  static __device__ __forceinline__ void run(float (&)[RQ][BW], int, int, int, int, float (*)[BW],
-                                             float*, float*, float*) {}
-};
 
 // -------------------------------------------------------------- panel
 __global__ __launch_bounds__(PT) void sy2sb_panel_kernel(const S1Mat* __restrict__ mats,
@@ -163,7 +95,65 @@ __global__ __launch_bounds__(PT) void sy2sb_panel_kernel(const S1Mat* __restrict
       P[q][4 * x + 2] = ok ? t.z : 0.f; P[q][4 * x + 3] = ok ? t.w : 0.f;
     }
   }
-  PanelCol<0>::run(P, tid, lane, wave, m, red16, red, rowc, taus);
+  // column loop NOT unrolled: P is indexed only with literal x, the runtime
+  // column c enters through compares (selects), so P stays in VGPRs
+#pragma unroll 1
+  for (int c = 0; c < BW; ++c) {
+    float part[BW];
+#pragma unroll
+    for (int x = 0; x < BW; ++x) part[x] = 0.f;
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) {
+      const int i = tid + PT * q;
+      float xc = 0.f;
+#pragma unroll
+      for (int x = 0; x < BW; ++x) xc = (x == c) ? P[q][x] : xc;
+      xc = (i > c && i < m) ? xc : 0.f;
+#pragma unroll
+      for (int x = 0; x < BW; ++x) part[x] += xc * P[q][x];
+    }
+    if (tid == c) {
+#pragma unroll
+      for (int x = 0; x < BW; ++x) rowc[x] = P[0][x];
+    }
+    {
+      const float s_ = kfac_butterfly16(part);       // lane x (< 16): value x
+      if (lane < BW) red16[wave][lane] = s_;
+    }
+    __syncthreads();
+    if (tid < BW) {
+      float s_ = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) s_ += red16[w][tid];
+      red[tid] = s_;
+    }
+    __syncthreads();
+    const float sig = red[c];
+    const float alpha = rowc[c];
+    float tau = 0.f, beta = alpha, scal = 0.f;
+    if (c < m - 1 && sig != 0.f) {
+      beta = -copysignf(sqrtf(alpha * alpha + sig), alpha);
+      tau = (beta - alpha) / beta;
+      scal = 1.f / (alpha - beta);
+    }
+    if (tid == 0) taus[c] = tau;
+    float wc[BW];
+#pragma unroll
+    for (int x = 0; x < BW; ++x) wc[x] = (x > c) ? tau * (rowc[x] + scal * red[x]) : 0.f;
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) {
+      const int i = tid + PT * q;
+      float xc = 0.f;
+#pragma unroll
+      for (int x = 0; x < BW; ++x) xc = (x == c) ? P[q][x] : xc;
+      const bool below = i > c && i < m;
+      const float vi = below ? scal * xc : (i == c ? 1.f : 0.f);
+      const float nc = below ? vi : (i == c ? beta : xc);
+#pragma unroll
+      for (int x = 0; x < BW; ++x) P[q][x] = (x == c) ? nc : P[q][x] - vi * wc[x];
+    }
+    __syncthreads();   // red / rowc reused by the next column
+  }
   // explicit v (1 at row c, zero above) for the Gram and U
 #define vval(q, c) ((tid + PT * (q) < m) ? (tid + PT * (q) == (c) ? 1.f : (tid + PT * (q) > (c) ? P[q][c] : 0.f)) : 0.f)
   // v[1:] of reflector k+c to row k+c (upper triangle, component k+16+i),

@@ -84,6 +84,7 @@ _SIGS = {
                                  c_vp, c_vp, c_vp, c_int, c_int, c_vp],
     'kfac_sb2st_batched': [ctypes.POINTER(SbRecord), c_int, c_vp, c_vp],
     'kfac_sb2st_bw': [],
+    'kfac_sb2st_stamps': [c_vp, c_int],
     'kfac_sb2st_ldv2': [c_int],
     'kfac_sb2st_nwg': [c_int],
     'kfac_syrk_patch': [c_int, c_vp, c_ll, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_int, c_int,
