@@ -89,6 +89,9 @@ def parse():
                     help='world > 1 with graphs: backward in two graph segments, the top '
                          "half's gradient all-reduce overlapped with the bottom half's backward "
                          '(parallel/overlap.py)')
+    ap.add_argument('--fused-sgd', type=int, default=1,
+                    help='torch.optim.SGD(fused=True): one multi-tensor kernel for the whole '
+                         'momentum + weight-decay update (same math as the reference optimizer)')
     ap.add_argument('--ddp', action='store_true',
                     help='eager torch DDP instead of the graphed flat-arena all-reduce')
     return ap.parse_args()
@@ -180,7 +183,10 @@ def main():
         # one flat-arena all-reduce between graph replays (parallel/grad_sync.py)
         grad_sync = grad_sync_mod.GradientAllreduce(model)
     base_lr = 0.0125 * world
-    opt = torch.optim.SGD(model.parameters(), lr=base_lr, momentum=0.9, weight_decay=5e-5)
+    sgd_kw = dict(lr=base_lr, momentum=0.9, weight_decay=5e-5)
+    if args.fused_sgd and device.type == 'cuda':
+        sgd_kw['fused'] = True
+    opt = torch.optim.SGD(model.parameters(), **sgd_kw)
     pre = None
     if not args.no_kfac:
         method = {'comm-opt': kfac.CommMethod.COMM_OPT, 'mem-opt': kfac.CommMethod.MEM_OPT,
@@ -311,6 +317,7 @@ def main():
                            'precond_precision': args.precond_precision,
                            'inverse_lag': args.inverse_lag},
                        'hip_graphs': use_graphs,
+                       'fused_sgd': bool(args.fused_sgd and device.type == 'cuda'),
                        'grad_allreduce': 'ddp' if grad_sync is None and world > 1 else
                                          (('split-backward-overlap' if split else 'flat-arena')
                                           if world > 1 else None),

@@ -52,9 +52,19 @@ def test_graphed_resnet50_step_ignores_stale_memory():
     batch 32, SGD): memory freed and filled with 1e30 between replays must not
     reach the gradients (without the memset rewrite layer2.0.conv1.weight's
     gradient came back ~1e30)."""
+    prev = torch.backends.cudnn.benchmark
+    torch.backends.cudnn.benchmark = True
+    try:
+        _stale_memory_case()
+    finally:
+        # a leaked benchmark=True made every later fp32 model pay MIOpen's
+        # find for each new convolution (the ResNet-50 parity test: 12 -> 164 s)
+        torch.backends.cudnn.benchmark = prev
+
+
+def _stale_memory_case():
     from distributed_kfac_pytorch_amd import graphs
     from distributed_kfac_pytorch_amd.models import resnet
-    torch.backends.cudnn.benchmark = True
     torch.manual_seed(0)
     model = resnet.get_model('resnet50').cuda().to(memory_format=torch.channels_last)
     opt = torch.optim.SGD(model.parameters(), lr=0.0125, momentum=0.9)

@@ -16,6 +16,16 @@ from distributed_kfac_pytorch_amd.models import resnet
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _immediate_mode_convs():
+    # fp32 NCHW convolutions of a model no other test uses: MIOpen's find
+    # (cudnn.benchmark) would time every one of them
+    prev = torch.backends.cudnn.benchmark
+    torch.backends.cudnn.benchmark = False
+    yield
+    torch.backends.cudnn.benchmark = prev
+
+
 def _step(model, x, y, device, **kw):
     pre = kfac.KFAC(model, factor_update_freq=1, inv_update_freq=1, lr=0.1, damping=1e-3,
                     kl_clip=1e-3, **kw)
