@@ -89,6 +89,10 @@ def parse():
                     help='world > 1 with graphs: backward in two graph segments, the top '
                          "half's gradient all-reduce overlapped with the bottom half's backward "
                          '(parallel/overlap.py)')
+    ap.add_argument('--overlap-precond', type=int, default=1,
+                    help='one rank: the last layers\' preconditioning chain starts on a side '
+                         'stream as soon as their gradients exist, under the rest of the '
+                         'backward (KFAC(overlap_precondition=True))')
     ap.add_argument('--fused-sgd', type=int, default=1,
                     help='torch.optim.SGD(fused=True): one multi-tensor kernel for the whole '
                          'momentum + weight-decay update (same math as the reference optimizer)')
@@ -200,6 +204,7 @@ def main():
                         profile=args.profile_phases, precond_precision=args.precond_precision,
                         compute_factor_in_hook=grad_sync is not None,
                         inverse_lag=args.inverse_lag,
+                        overlap_precondition=bool(args.overlap_precond) and world == 1,
                         use_hip_graphs=not os.environ.get('KFAC_NO_TAIL_GRAPH'))
 
     B, S = args.batch_size, args.image_size
@@ -315,7 +320,8 @@ def main():
                            'inv_update_freq': args.kfac_update_freq,
                            'damping': args.damping, 'kl_clip': args.kl_clip,
                            'precond_precision': args.precond_precision,
-                           'inverse_lag': args.inverse_lag},
+                           'inverse_lag': args.inverse_lag,
+                           'overlap_precondition': bool(args.overlap_precond) and world == 1},
                        'hip_graphs': use_graphs,
                        'fused_sgd': bool(args.fused_sgd and device.type == 'cuda'),
                        'grad_allreduce': 'ddp' if grad_sync is None and world > 1 else

@@ -398,3 +398,72 @@ class FusedPreconditioner(object):
         for b in self.bufs:
             b.layer.preconditioned_gradient = b.layer._split_pgrad(b.layer._pgrad_matrix())
         return self.kl if with_kl else None
+
+
+class SplitFused(object):
+    """The fused chain over a forward-order layer split, for single-rank runs
+    (KFAC(overlap_precondition=True)): `top` holds the LAST layers -- the ones
+    whose gradients backward produces first, and most of the chain's flops
+    (ResNet-50's layer4) -- and is launched on a side stream from a gradient
+    hook as soon as its gradients are accumulated, so it runs under the rest
+    of the backward; run() then preconditions `bottom` on the current stream,
+    joins, and adds the two KL partial dots (bottom + top, fixed order).  Same
+    operands, same kernels, same math as one FusedPreconditioner."""
+
+    def __init__(self, layers, precision, split_at):
+        self.layers = list(layers)
+        self.bottom = FusedPreconditioner(self.layers[:split_at], precision)
+        self.top = FusedPreconditioner(self.layers[split_at:], precision)
+        self.inverse = self.top.inverse
+        self.device = self.top.device
+        self.precision = precision
+        self._side = None
+        self._top_kl = None
+        self._launched = False
+        self.early_launches = 0
+        self.kl_sum = torch.zeros((), dtype=torch.float64, device=self.device)
+
+    @property
+    def bufs(self):
+        return self.bottom.bufs + self.top.bufs
+
+    @property
+    def kl(self):
+        return self.kl_sum
+
+    @property
+    def _stage_tables(self):
+        return self.top._stage_tables
+
+    def refresh_eigen(self):
+        self.bottom.refresh_eigen()
+        self.top.refresh_eigen()
+
+    def _side_stream(self):
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
+
+    def launch_top(self, damping=0.0, with_kl=True):
+        """Precondition the top layers on the side stream (called from the
+        hook that sees the last top-layer gradient accumulated)."""
+        cur = torch.cuda.current_stream(self.device)
+        side = self._side_stream()
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            self._top_kl = self.top.run(damping=damping, with_kl=with_kl)
+        self._launched = True
+        self.early_launches += 1
+
+    def run(self, damping=0.0, with_kl=True):
+        cur = torch.cuda.current_stream(self.device)
+        if not self._launched:
+            self._top_kl = self.top.run(damping=damping, with_kl=with_kl)
+        klb = self.bottom.run(damping=damping, with_kl=with_kl)
+        if self._launched:
+            cur.wait_stream(self._side)
+        self._launched = False
+        if not with_kl:
+            return None
+        torch.add(klb, self._top_kl, out=self.kl_sum)
+        return self.kl_sum

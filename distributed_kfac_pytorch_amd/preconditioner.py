@@ -153,7 +153,8 @@ class KFAC(optim.Optimizer):
                  use_eigen_decomp=True, skip_layers=[], verbose=False,
                  bucket_cap_mb=64.0, symmetry_aware_comm=True, eigen_solver='auto',
                  profile=False, use_hip_graphs=True, precond_precision='fp32',
-                 fused_precondition=True, inverse_lag=0, comm_check=False):
+                 fused_precondition=True, inverse_lag=0, comm_check=False,
+                 overlap_precondition=False):
         if not 0.0 <= lr:
             raise ValueError('Invalid learning rate: {}'.format(lr))
         if not 0.0 < factor_decay <= 1:
@@ -235,6 +236,11 @@ class KFAC(optim.Optimizer):
                 sorted(precond_fused.PRECISIONS)))
         self.precond_precision = precond_precision
         self.fused_precondition = fused_precondition
+        # single rank, one backward per step: the last layers' chain starts on a
+        # side stream from a gradient hook, under the rest of the backward
+        self.overlap_precondition = bool(overlap_precondition)
+        self._top_hooks = []
+        self._top_seen = 0
         # all factors of a step in a few grouped launches (GPU)
         self.grouped_factors = True
         self.fused = None
@@ -454,6 +460,36 @@ class KFAC(optim.Optimizer):
         for h in self._hook_handles:
             h.remove()
         self._hook_handles = []
+        for h in self._top_hooks:
+            h.remove()
+        self._top_hooks = []
+
+    # -------------------------------------------- early top-layer precondition
+    def _early_launch_ok(self):
+        p = self.param_groups[0]
+        return (isinstance(self.fused, precond_fused.SplitFused) and self._have_inverses
+                and self._pending_inv is None and p['step'] % p['inv_update_freq'] != 0
+                and not self._graph_eligible() and torch.is_grad_enabled() is False)
+
+    def _top_grad_hook(self, param):
+        self._top_seen += 1
+        if self._top_seen == len(self._top_hooks):
+            self._top_seen = 0
+            if self._early_launch_ok():
+                self.fused.launch_top(damping=self.param_groups[0]['damping'],
+                                      with_kl=self._fused_all)
+
+    def _register_top_hooks(self):
+        for h in self._top_hooks:
+            h.remove()
+        self._top_hooks = []
+        self._top_seen = 0
+        if not isinstance(self.fused, precond_fused.SplitFused):
+            return
+        for layer in self.fused.top.layers:
+            for prm in (layer.module.weight, getattr(layer.module, 'bias', None)):
+                if prm is not None and prm.requires_grad:
+                    self._top_hooks.append(prm.register_post_accumulate_grad_hook(self._top_grad_hook))
 
     # ------------------------------------------------------------------ step
     @torch.no_grad()
@@ -848,8 +884,32 @@ class KFAC(optim.Optimizer):
         rank = comm.backend.rank()
         mine = [l for l in self.layers if rank in l.compute_grad_ranks]
         if mine:
-            self.fused = precond_fused.FusedPreconditioner(mine, self.precond_precision)
+            split = self._overlap_split(mine)
+            if split:
+                self.fused = precond_fused.SplitFused(mine, self.precond_precision, split)
+            else:
+                self.fused = precond_fused.FusedPreconditioner(mine, self.precond_precision)
             self._fused_all = len(mine) == len(self.layers)
+        self._register_top_hooks()
+
+    def _overlap_split(self, mine):
+        """Index splitting `mine` (forward order) so the suffix carries ~60 % of
+        the chain's flops (n_G n_A (n_G + n_A) per layer), or 0 = no split:
+        only on one rank (the hook sees local, final gradients), eigen path,
+        GPU, at least two layers."""
+        if not (self.overlap_precondition and comm.backend.size() == 1 and len(mine) >= 2
+                and self.use_eigen_decomp):
+            return 0
+        cost = []
+        for l in mine:
+            nG, nA = l.grad_shape[0], l.grad_shape[1]
+            cost.append(float(nG) * nA * (nG + nA))
+        total, acc = sum(cost), 0.0
+        for i in range(len(mine) - 1, 0, -1):
+            acc += cost[i]
+            if acc >= 0.6 * total:
+                return i
+        return 0
 
     @torch.no_grad()
     def compute_preconditioned_gradients(self, damping=0.001):
