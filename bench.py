@@ -89,10 +89,12 @@ def parse():
                     help='world > 1 with graphs: backward in two graph segments, the top '
                          "half's gradient all-reduce overlapped with the bottom half's backward "
                          '(parallel/overlap.py)')
-    ap.add_argument('--overlap-precond', type=int, default=1,
+    ap.add_argument('--overlap-precond', type=int, default=0,
                     help='one rank: the last layers\' preconditioning chain starts on a side '
                          'stream as soon as their gradients exist, under the rest of the '
-                         'backward (KFAC(overlap_precondition=True))')
+                         'backward (KFAC(overlap_precondition=True)); off by default: the '
+                         'backward already fills the GPU, 11.05 vs 10.91 ms per plain step '
+                         '(profiles/r2_final_bench20*.log)')
     ap.add_argument('--fused-sgd', type=int, default=1,
                     help='torch.optim.SGD(fused=True): one multi-tensor kernel for the whole '
                          'momentum + weight-decay update (same math as the reference optimizer)')
