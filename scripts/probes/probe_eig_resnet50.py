@@ -49,7 +49,9 @@ def main():
                 ('nothreads', {'TH': False}), ('fs1', {'FS': 1}), ('fs3', {'FS': 3}),
                 ('fs4', {'FS': 4}), ('noprio', {'PR': False}),
                 ('noprio_nothreads', {'PR': False, 'TH': False}),
-                ('two_stage', {'TS': True}), ('two_stage_fs1', {'TS': True, 'FS': 1})]
+                ('two_stage', {'TS': True}), ('two_stage_fs1', {'TS': True, 'FS': 1}),
+                ('only_big', {'SEL': 'big'}), ('only_rest', {'SEL': 'rest'}),
+                ('only_big_fs1', {'SEL': 'big', 'FS': 1}), ('only_rest_fs1', {'SEL': 'rest', 'FS': 1})]
     if len(sys.argv) > 1:
         variants = [v for v in variants if v[0] in sys.argv[1:]]
     res = {}
@@ -70,18 +72,21 @@ def main():
             os.environ['KFAC_EIGH_WORKERS'] = str(cfg['W'])
         else:
             os.environ.pop('KFAC_EIGH_WORKERS', None)
-        eigen.symeig_many(mats)       # warm: buffers, graphs
+        nmax = max(A.shape[0] for A in mats)
+        sel = cfg.get('SEL')
+        run_mats = mats if sel is None else [A for A in mats if (2 * A.shape[0] > nmax) == (sel == 'big')]
+        eigen.symeig_many(run_mats)       # warm: buffers, graphs
         torch.cuda.synchronize()
         ts = []
         for _ in range(3):
             t = time.perf_counter()
-            outs = eigen.symeig_many(mats)
+            outs = eigen.symeig_many(run_mats)
             torch.cuda.synchronize()
             ts.append((time.perf_counter() - t) * 1e3)
         eigen.check_solver_status()
         err = 0.0
         orth = 0.0
-        for A, (Q, d) in zip(mats, outs):
+        for A, (Q, d) in zip(run_mats, outs):
             err = max(err, float((A @ Q - Q * d).norm() / A.norm()))
             orth = max(orth, float((Q.t() @ Q - torch.eye(Q.shape[0], device=Q.device)).abs().max()))
         res[name] = {'ms': min(ts), 'all_ms': ts, 'resid': err, 'orth': orth}
