@@ -34,7 +34,7 @@ struct Q2Mat {
   const float* v2; long long ldv2;
   float* Z; long long ldz;
   float* T;                        // [G][jmax][16][16]
-  int n, G, jmax, nstrips;
+  int n, G, jmax, pad;
 };
 
 __device__ inline void map_block(const int* __restrict__ offs, int nact, int* soff, int& mat,
@@ -236,9 +236,8 @@ struct Q2Plan {
   Q2Mat* d_mats = nullptr;
   Q2Strip* d_strips = nullptr;
   int nstrip = 0;
-  int* d_offs = nullptr;      // [ticks + 1][nm + 1]: [0] = T kernel, [1 + t] = tick t
-  int* d_jlo = nullptr;       // [ticks][nm]
-  int count = 0, ticks = 0;
+  int* d_offs = nullptr;      // [nm + 1]: T-kernel workgroup offsets
+  int count = 0;
   std::vector<int> grid, nact;
   hipGraphExec_t exec = nullptr;
 };
@@ -283,7 +282,7 @@ KFAC_API int kfac_q2_batched(const KfacQ2Record* recs, int count, int use_graph,
     Q2Mat& M = mats[i];
     memset(&M, 0, sizeof(M));
     M.v2 = r.v2; M.ldv2 = r.ldv2; M.Z = r.Z; M.ldz = r.ldz; M.T = r.T; M.n = (int)r.n;
-    M.G = q2_G(M.n); M.jmax = q2_jmax(M.n); M.nstrips = (M.n + 63) / 64;
+    M.G = q2_G(M.n); M.jmax = q2_jmax(M.n);
   }
   const std::string key((const char*)mats.data(), sizeof(Q2Mat) * mats.size());
   std::lock_guard<std::mutex> lk(g_mu);
@@ -292,10 +291,11 @@ KFAC_API int kfac_q2_batched(const KfacQ2Record* recs, int count, int use_graph,
     Q2Plan P;
     P.count = count;
     const int nm = count;
-    for (auto& M : mats) P.ticks = std::max(P.ticks, M.G + M.jmax);
-    std::vector<int> offs((size_t)(P.ticks + 1) * (nm + 1), 0), jl((size_t)std::max(1, P.ticks) * nm, 0);
-    P.grid.assign(P.ticks + 1, 0);
-    P.nact.assign(P.ticks + 1, 0);
+    // T kernel: one workgroup per (matrix, group); the pass kernel: one per
+    // (matrix, 64 eigenvectors)
+    std::vector<int> offs((size_t)nm + 1, 0);
+    P.grid.assign(1, 0);
+    P.nact.assign(1, 0);
     {
       int acc = 0;
       for (int i = 0; i < nm; ++i) {
@@ -307,29 +307,10 @@ KFAC_API int kfac_q2_batched(const KfacQ2Record* recs, int count, int use_graph,
       offs[nm] = acc;
       P.grid[0] = acc;
     }
-    for (int t = 0; t < P.ticks; ++t) {
-      int acc = 0;
-      int* of = offs.data() + (size_t)(1 + t) * (nm + 1);
-      for (int i = 0; i < nm; ++i) {
-        const Q2Mat& M = mats[i];
-        // g = G-1-t+j in [0, G), j in [0, jmax)
-        const int lo = std::max(0, t - (M.G - 1));
-        const int hi = std::min(M.jmax - 1, t);
-        const int cnt = hi >= lo ? hi - lo + 1 : 0;
-        of[i] = acc;
-        jl[(size_t)t * nm + i] = lo;
-        if (cnt > 0) P.nact[1 + t] = i + 1;
-        acc += cnt * M.nstrips;
-      }
-      of[nm] = acc;
-      P.grid[1 + t] = acc;
-    }
     int e = (int)hipMalloc(&P.d_mats, sizeof(Q2Mat) * nm);
     if (!e) e = (int)hipMemcpy(P.d_mats, mats.data(), sizeof(Q2Mat) * nm, hipMemcpyHostToDevice);
     if (!e) e = (int)hipMalloc(&P.d_offs, sizeof(int) * offs.size());
     if (!e) e = (int)hipMemcpy(P.d_offs, offs.data(), sizeof(int) * offs.size(), hipMemcpyHostToDevice);
-    if (!e) e = (int)hipMalloc(&P.d_jlo, sizeof(int) * jl.size());
-    if (!e) e = (int)hipMemcpy(P.d_jlo, jl.data(), sizeof(int) * jl.size(), hipMemcpyHostToDevice);
     std::vector<Q2Strip> strips;
     for (int i = 0; i < nm; ++i)
       for (int e0 = 0; e0 < mats[i].n; e0 += 64) strips.push_back(Q2Strip{i, e0});
