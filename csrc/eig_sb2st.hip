@@ -98,7 +98,8 @@ __device__ bool sb_task(float* Lb, int n, int s, int j, AS1 float* v2row, int la
   const int r1 = min(s + (j + 1) * BW, n - 1);
   const int L = r1 - r0 + 1;
   if (r0 > n - 1 || L < 2) return false;
-  const float x = lane < L ? LB(Lb, r0 + lane, c) : 0.f;
+  const float xl = Lb[lane < L ? ((c & (WIN - 1)) * ND + (r0 + lane - c)) : 0];
+  const float x = lane < L ? xl : 0.f;
   const float alpha = __shfl(x, 0, 64);
   const float sig = wave_sum(lane >= 1 && lane < L ? x * x : 0.f);
   float tau = 0.f, beta = alpha, scal = 0.f;
@@ -127,12 +128,15 @@ __device__ bool sb_task(float* Lb, int n, int s, int j, AS1 float* v2row, int la
   float acc = 0.f;
 #pragma unroll
   for (int l = 0; l < BW; ++l) {
-    int rr, cc;
-    if (grp == 0) { rr = r0 + max(li, l); cc = r0 + min(li, l); }
-    else if (grp == 1) { rr = r0 + l; cc = c + 1 + li; }
-    else { rr = r1 + 1 + li; cc = r0 + l; }
+    // element of entry l for this lane's group, as selects (no divergent branch)
+    const int rr = grp == 0 ? r0 + max(li, l) : (grp == 1 ? r0 + l : r1 + 1 + li);
+    const int cc = grp == 0 ? r0 + min(li, l) : (grp == 1 ? c + 1 + li : r0 + l);
     const bool ok = act && l < L;
-    val[l] = ok ? LB(Lb, rr, cc) : 0.f;
+    // branch-free: inactive lanes read slot 0 (a conditional load becomes a
+    // branch with its own LDS wait, serialising the 16 loads)
+    const int ad = ok ? (((cc & (WIN - 1)) * ND) + (rr - cc)) : 0;
+    const float ld = Lb[ad];
+    val[l] = ok ? ld : 0.f;
     acc += val[l] * vl[l];
   }
   acc *= tau;                                    // p (diag lanes), y (bulge), z (below)
@@ -148,12 +152,12 @@ __device__ bool sb_task(float* Lb, int n, int s, int j, AS1 float* v2row, int la
   const float c2 = grp == 0 ? w : acc;
 #pragma unroll
   for (int l = 0; l < BW; ++l) {
-    int rr, cc;
-    if (grp == 0) { rr = r0 + li; cc = r0 + l; }   // lower entry (li, l), l <= li
-    else if (grp == 1) { rr = r0 + l; cc = c + 1 + li; }
-    else { rr = r1 + 1 + li; cc = r0 + l; }
+    // diagonal group: lower entry (li, l), l <= li
+    const int rr = grp == 0 ? r0 + li : (grp == 1 ? r0 + l : r1 + 1 + li);
+    const int cc = grp == 0 ? r0 + l : (grp == 1 ? c + 1 + li : r0 + l);
     const bool ok = act && l < L && (grp != 0 || l <= li);
-    if (ok) LB(Lb, rr, cc) = val[l] - c1 * wl[l] - c2 * vl[l];
+    const float nv = val[l] - c1 * wl[l] - c2 * vl[l];
+    if (ok) Lb[((cc & (WIN - 1)) * ND) + (rr - cc)] = nv;
   }
   return true;
 }
