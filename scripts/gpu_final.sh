@@ -1,3 +1,5 @@
+#!/bin/bash
+# End-of-session validation: full GPU suite, smoke, driver-command bench, window profile.
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out

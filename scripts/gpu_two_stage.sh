@@ -1,3 +1,6 @@
+#!/bin/bash
+# Two-stage eigensolver session: GPU tests, stage-2 phase stamps, rocprofv3 stats of the
+# ResNet-50 inverse update through the two-stage path (KFAC_EIG_TWO_STAGE variant).
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
