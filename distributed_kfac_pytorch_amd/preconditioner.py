@@ -191,6 +191,10 @@ class KFAC(optim.Optimizer):
             skip_layers = [skip_layers.lower()]
         else:
             skip_layers = [s.lower() for s in skip_layers]
+        # an entry names a module class ('linear', reference semantics) or,
+        # extension, a submodule by attribute or dotted name ('head',
+        # 'blocks.0.fc1'): e.g. a 10k-vocabulary output projection whose
+        # 10k x 10k gradient factor would dominate the inverse update
         for s in skip_layers:
             known.discard(s)
 
@@ -383,7 +387,8 @@ class KFAC(optim.Optimizer):
         for name, module in parent_module.named_children():
             full = prefix + ('.' if prefix else '') + name
             cls = module.__class__.__name__.lower()
-            if cls in self.skip_layers:
+            if cls in self.skip_layers or name.lower() in self.skip_layers or \
+                    full.lower() in self.skip_layers:
                 continue
             if cls not in self.known_modules:
                 self.register_submodules(module, prefix=full)

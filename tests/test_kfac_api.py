@@ -23,6 +23,16 @@ def test_registration_counts():
     assert len(kfac.KFAC(resnet.resnet50()).layers) == 54
 
 
+def test_skip_layers_by_module_name():
+    from distributed_kfac_pytorch_amd.models import TransformerLM
+    lm = TransformerLM(50, d_model=16, n_layers=2, n_heads=2, d_ff=32, max_len=8)
+    n_all = len(kfac.KFAC(lm, skip_layers=['embedding']).layers)
+    assert n_all == 2 * 4 + 1
+    assert len(kfac.KFAC(lm, skip_layers=['embedding', 'head']).layers) == n_all - 1
+    assert len(kfac.KFAC(lm, skip_layers=['embedding', 'blocks.0.fc1']).layers) == n_all - 1
+    assert len(kfac.KFAC(lm, skip_layers=['embedding', 'blocks.1']).layers) == n_all - 4
+
+
 def test_skip_layers():
     m = resnet_cifar.resnet20()
     assert len(kfac.KFAC(m, skip_layers='linear').layers) == 19
