@@ -127,6 +127,8 @@ def main():
     ap.add_argument('--kfac-cov-update-freq', type=int, default=1)
     ap.add_argument('--precond-precision', default='fp32', choices=['fp32', 'bf16x3', 'bf16x6'])
     ap.add_argument('--no-kfac', action='store_true')
+    ap.add_argument('--autocast', default='none', choices=['none', 'bf16'],
+                    help='bf16 autocast of forward + loss (both implementations)')
     ap.add_argument('--skip-head', type=int, default=1,
                     help='transformer: leave the vocabulary projection out of K-FAC')
     ap.add_argument('--graphs', type=int, default=0,
@@ -167,8 +169,9 @@ def main():
         state['i'] = (i + T) % (T * 64)
         data, target = stream[i:i + T], stream[i + 1:i + 1 + T].reshape(-1)
         opt.zero_grad()
-        out, state['hidden'] = fwd(data, state['hidden'])
-        loss = crit(out.reshape(-1, out.size(-1)), target)
+        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=args.autocast == 'bf16'):
+            out, state['hidden'] = fwd(data, state['hidden'])
+            loss = crit(out.reshape(-1, out.size(-1)), target)
         loss.backward()
         torch.nn.utils.clip_grad_norm_(model.parameters(), 0.25)
         if pre is not None:
@@ -186,11 +189,12 @@ def main():
 
         def body():
             opt.zero_grad(set_to_none=True)
-            if h_buf is not None:
-                out, hid = model(x_buf, h_buf)
-            else:
-                out = model(x_buf.t()).transpose(0, 1)
-            loss = crit(out.reshape(-1, out.size(-1)), y_buf)
+            with torch.autocast('cuda', dtype=torch.bfloat16, enabled=args.autocast == 'bf16'):
+                if h_buf is not None:
+                    out, hid = model(x_buf, h_buf)
+                else:
+                    out = model(x_buf.t()).transpose(0, 1)
+                loss = crit(out.reshape(-1, out.size(-1)), y_buf)
             loss.backward()
             torch.nn.utils.clip_grad_norm_(model.parameters(), 0.25)
             if pre is not None:
@@ -247,7 +251,8 @@ def main():
                          if args.model == 'lstm' else
                          {'d_model': 512, 'n_layers': 6, 'n_heads': 8, 'd_ff': 2048,
                           'kfac_skips_head': bool(args.skip_head)}),
-                      'comm_method': args.comm, 'graphs': bool(args.graphs), 'inv_update_freq': f, 'factor_update_freq': args.kfac_cov_update_freq,
+                      'comm_method': args.comm, 'graphs': bool(args.graphs),
+                      'autocast': args.autocast, 'inv_update_freq': f, 'factor_update_freq': args.kfac_cov_update_freq,
                       'precond_precision': args.precond_precision if args.impl == 'ours' else 'fp32'},
            'data': 'synthetic'}
     if dist.get_rank() == 0:
