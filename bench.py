@@ -39,6 +39,8 @@ from distributed_kfac_pytorch_amd.parallel import grad_sync as grad_sync_mod  # 
 from distributed_kfac_pytorch_amd.parallel import overlap  # noqa: E402
 
 METRIC = 'images/sec (whole node) ResNet-50 K-FAC+SGD'
+# the reference K-FAC on one MI355X, same config and timing (not a BASELINE number)
+REFERENCE_MI355X_IMG_S = 296.8
 
 
 def parse():
@@ -352,6 +354,13 @@ def main():
                         'steady_state_mix weights the measured kinds by the reference '
                         'schedule (1 inverse + {} factor steps per {})'.format(
                             inv // ff - 1, inv)}
+        if pre is not None and world == 1 and args.model == 'resnet50' and B == 32:
+            # BASELINE.md publishes no number (vs_baseline stays null); the
+            # reference K-FAC itself, timed the same way on one MI355X
+            # (scripts/bench_reference.py, profiles/r2_reference_kfac_mi355x.log)
+            rec['reference_kfac_same_gpu'] = {
+                'images_per_sec': REFERENCE_MI355X_IMG_S,
+                'speedup': round(value / REFERENCE_MI355X_IMG_S, 2)}
         if phases is not None:
             rec['kfac_phase_ms_total'] = {k: round(v, 2) for k, v in phases.items()}
             rec['kfac_phase_ms_per_step'] = round(sum(phases.values()) / args.steps, 3)
