@@ -104,9 +104,30 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(const uint16_t* __restrict
   float acc[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-  for (long long m = m0 + rr; m < m1; m += g.rpi) {
+  // 4 rows' loads in flight per thread before the (in-order) accumulation:
+  // one 16-byte load at a time left the pass latency bound
+  const long long cs = (long long)C / 8, step = (long long)g.rpi * cs;
+  long long m = m0 + rr;
+  const AS1 u32x4n* Xp = X + (m * C + c0) / 8;
+  for (; m + 3 * g.rpi < m1; m += 4 * g.rpi, Xp += 4 * step) {
+    u32x4n q[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) q[u] = Xp[u * step];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float f[8];
+      unpack8(q[u], f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = f[i] - k[i];
+        acc[i] += d;
+        acc[8 + i] = fmaf(d, d, acc[8 + i]);
+      }
+    }
+  }
+  for (; m < m1; m += g.rpi, Xp += step) {
     float f[8];
-    unpack8(X[(m * C + c0) / 8], f);
+    unpack8(*Xp, f);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float d = f[i] - k[i];
@@ -169,6 +190,32 @@ __global__ __launch_bounds__(NT) void bn_finalize_kernel(
   }
 }
 
+__device__ __forceinline__ void load8(const float* __restrict__ p, int c0, float* o) {
+  const fx4 a = *(const AS1 fx4*)(gptr(p) + c0), b = *(const AS1 fx4*)(gptr(p) + c0 + 4);
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+  o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+
+template <bool RELU, bool ADD>
+__device__ __forceinline__ void apply8(const AS1 u32x4n* X, const AS1 u32x4n* Z, AS1 u32x4n* Y,
+                                       long long v, const float* sc, const float* sh) {
+  float f[8], o[8], zz[8];
+  unpack8(X[v], f);
+  if (ADD) unpack8(Z[v], zz);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    float r = fmaf(f[i], sc[i], sh[i]);
+    if (ADD) r += zz[i];
+    o[i] = RELU ? fmaxf(r, 0.f) : r;
+  }
+  Y[v] = pack8(o);
+}
+
+// Grid-stride elementwise pass.  When C / 8 divides the block size (every
+// power-of-two C <= 2048: all of ResNet-50) the stride is a multiple of C / 8,
+// so each thread keeps ONE channel octet: its per-channel operands are loaded
+// once, and no per-element 64-bit modulo is issued (the pass is VALU-heavy
+// enough at 16 bytes per lane for that to matter).
 template <bool RELU, bool ADD>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(const uint16_t* __restrict__ x,
                                                       const uint16_t* __restrict__ z,
@@ -180,24 +227,21 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const uint16_t* __restrict
   const AS1 u32x4n* Z = (const AS1 u32x4n*)z;
   AS1 u32x4n* Y = (AS1 u32x4n*)y;
   const int cvec = C / 8;
-  for (long long v = blockIdx.x * (long long)NT + threadIdx.x; v < nvec;
-       v += (long long)gridDim.x * NT) {
-    const int c0 = (int)(v % cvec) * 8;
-    float f[8], o[8];
-    unpack8(X[v], f);
-    const fx4 s0 = *(const AS1 fx4*)(gptr(scale) + c0), s1 = *(const AS1 fx4*)(gptr(scale) + c0 + 4);
-    const fx4 h0 = *(const AS1 fx4*)(gptr(shift) + c0), h1 = *(const AS1 fx4*)(gptr(shift) + c0 + 4);
-    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-    float zz[8];
-    if (ADD) unpack8(Z[v], zz);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float r = fmaf(f[i], sc[i], sh[i]);
-      if (ADD) r += zz[i];
-      o[i] = RELU ? fmaxf(r, 0.f) : r;
+  const long long stride = (long long)gridDim.x * NT;
+  const long long v0 = blockIdx.x * (long long)NT + threadIdx.x;
+  float sc[8], sh[8];
+  if (NT % cvec == 0) {
+    const int c0 = (threadIdx.x % cvec) * 8;
+    load8(scale, c0, sc);
+    load8(shift, c0, sh);
+    for (long long v = v0; v < nvec; v += stride) apply8<RELU, ADD>(X, Z, Y, v, sc, sh);
+  } else {
+    for (long long v = v0; v < nvec; v += stride) {
+      const int c0 = (int)(v % cvec) * 8;
+      load8(scale, c0, sc);
+      load8(shift, c0, sh);
+      apply8<RELU, ADD>(X, Z, Y, v, sc, sh);
     }
-    Y[v] = pack8(o);
   }
 }
 
@@ -222,8 +266,32 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(
   float acc[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-  for (long long m = m0 + rr; m < m1; m += g.rpi) {
-    const long long v = (m * C + c0) / 8;
+  // 2 rows (up to 6 loads) in flight per thread, accumulated in row order
+  const long long step = (long long)g.rpi * (C / 8);
+  long long m = m0 + rr, v = (m * C + c0) / 8;
+  for (; m + g.rpi < m1; m += 2 * g.rpi, v += 2 * step) {
+    u32x4n qg[2], qx[2], qy[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      qg[u] = DY[v + u * step];
+      qx[u] = X[v + u * step];
+      if (RELU) qy[u] = Y[v + u * step];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float gv[8], xv[8], yv[8];
+      unpack8(qg[u], gv);
+      unpack8(qx[u], xv);
+      if (RELU) unpack8(qy[u], yv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float gg = (!RELU || yv[i] > 0.f) ? gv[i] : 0.f;
+        acc[i] += gg;
+        acc[8 + i] = fmaf(gg, (xv[i] - mu[i]) * is[i], acc[8 + i]);
+      }
+    }
+  }
+  for (; m < m1; m += g.rpi, v += step) {
     float gv[8], xv[8], yv[8];
     unpack8(DY[v], gv);
     unpack8(X[v], xv);
@@ -246,11 +314,11 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(
   }
 }
 
-// one wave per channel: fp64 chunk sums -> dw, db and (a, k1, k2) of
-// dx = a (g - k1 - x_hat k2)
+// one wave per channel: fp64 chunk sums -> dw, db and the planar (A, B, X)
+// of dx = a (g - k1 - x_hat k2) = A g + B + X x
 __global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(
     const float* __restrict__ part, long long M, int C, Geo g, const float* __restrict__ w,
-    const float* __restrict__ invstd, float* __restrict__ dw, float* __restrict__ db,
+    const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ dw, float* __restrict__ db,
     float* __restrict__ coef) {
   const int lane = threadIdx.x & 63;
   const int c = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
@@ -266,17 +334,41 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(
   if (lane == 0) {
     if (dw) dw[c] = (float)sgx;
     if (db) db[c] = (float)sg;
-    coef[3 * c] = (w ? w[c] : 1.f) * invstd[c];
-    coef[3 * c + 1] = (float)(sg / (double)M);
-    coef[3 * c + 2] = (float)(sgx / (double)M);
+    // dx = a (g - k1 - (x - mean) invstd k2) as an affine map of (g, x):
+    // A g + B + X x, planar per channel (float4 loads in the apply pass)
+    const double a = (double)(w ? w[c] : 1.f) * (double)invstd[c];
+    const double k1 = sg / (double)M, k2 = sgx / (double)M;
+    const double ak = a * k2 * (double)invstd[c];
+    coef[c] = (float)a;
+    coef[C + c] = (float)(ak * (double)mean[c] - a * k1);
+    coef[2 * C + c] = (float)(-ak);
   }
 }
 
 template <bool RELU, bool ADD>
+__device__ __forceinline__ void bwd_apply8(const AS1 u32x4n* DY, const AS1 u32x4n* Y,
+                                           const AS1 u32x4n* X, AS1 u32x4n* DX, AS1 u32x4n* DZ,
+                                           long long v, const float* ca, const float* cb,
+                                           const float* cx) {
+  float gv[8], xv[8], yv[8], o[8], gz[8];
+  unpack8(DY[v], gv);
+  unpack8(X[v], xv);
+  if (RELU) unpack8(Y[v], yv);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float gg = (!RELU || yv[i] > 0.f) ? gv[i] : 0.f;
+    o[i] = fmaf(xv[i], cx[i], fmaf(gg, ca[i], cb[i]));
+    gz[i] = gg;
+  }
+  DX[v] = pack8(o);
+  if (ADD) DZ[v] = pack8(gz);
+}
+
+// same one-octet-per-thread scheme as bn_apply_kernel
+template <bool RELU, bool ADD>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
-    const uint16_t* __restrict__ x, const float* __restrict__ mean,
-    const float* __restrict__ invstd, const float* __restrict__ coef,
+    const uint16_t* __restrict__ x, const float* __restrict__ coef,
     uint16_t* __restrict__ dx, uint16_t* __restrict__ dz, long long nvec, int C) {
   const AS1 u32x4n* DY = (const AS1 u32x4n*)dy;
   const AS1 u32x4n* Y = (const AS1 u32x4n*)y;
@@ -284,23 +376,24 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(
   AS1 u32x4n* DX = (AS1 u32x4n*)dx;
   AS1 u32x4n* DZ = (AS1 u32x4n*)dz;
   const int cvec = C / 8;
-  for (long long v = blockIdx.x * (long long)NT + threadIdx.x; v < nvec;
-       v += (long long)gridDim.x * NT) {
-    const int c0 = (int)(v % cvec) * 8;
-    float gv[8], xv[8], yv[8], o[8], gz[8];
-    unpack8(DY[v], gv);
-    unpack8(X[v], xv);
-    if (RELU) unpack8(Y[v], yv);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int c = c0 + i;
-      const float gg = (!RELU || yv[i] > 0.f) ? gv[i] : 0.f;
-      const float xh = (xv[i] - mean[c]) * invstd[c];
-      o[i] = coef[3 * c] * (gg - coef[3 * c + 1] - xh * coef[3 * c + 2]);
-      gz[i] = gg;
+  const long long stride = (long long)gridDim.x * NT;
+  const long long v0 = blockIdx.x * (long long)NT + threadIdx.x;
+  float ca[8], cb[8], cx[8];
+  if (NT % cvec == 0) {
+    const int c0 = (threadIdx.x % cvec) * 8;
+    load8(coef, c0, ca);
+    load8(coef + C, c0, cb);
+    load8(coef + 2 * C, c0, cx);
+    for (long long v = v0; v < nvec; v += stride)
+      bwd_apply8<RELU, ADD>(DY, Y, X, DX, DZ, v, ca, cb, cx);
+  } else {
+    for (long long v = v0; v < nvec; v += stride) {
+      const int c0 = (int)(v % cvec) * 8;
+      load8(coef, c0, ca);
+      load8(coef + C, c0, cb);
+      load8(coef + 2 * C, c0, cx);
+      bwd_apply8<RELU, ADD>(DY, Y, X, DX, DZ, v, ca, cb, cx);
     }
-    DX[v] = pack8(o);
-    if (ADD) DZ[v] = pack8(gz);
   }
 }
 
@@ -370,18 +463,18 @@ KFAC_API int kfac_bn_backward(const void* dy, const void* y, const void* x, cons
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, dim3(g.ncg, g.nchunks), dim3(NT), 0, stream,
                        DY, Y, X, save_mean, save_invstd, M, C, g, part);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(NT), 0, stream, part, M, C,
-                     g, w, save_invstd, dw, db, coef);
+                     g, w, save_mean, save_invstd, dw, db, coef);
   const long long nvec = M * C / 8;
   const dim3 grid(apply_grid(nvec));
   uint16_t* DX = (uint16_t*)dx;
   uint16_t* DZ = (uint16_t*)dz;
   if (relu && dz)
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<true, true>), grid, dim3(NT), 0, stream, DY, Y, X, save_mean, save_invstd, coef, DX, DZ, nvec, C);
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<true, true>), grid, dim3(NT), 0, stream, DY, Y, X, coef, DX, DZ, nvec, C);
   else if (relu)
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false>), grid, dim3(NT), 0, stream, DY, Y, X, save_mean, save_invstd, coef, DX, DZ, nvec, C);
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false>), grid, dim3(NT), 0, stream, DY, Y, X, coef, DX, DZ, nvec, C);
   else if (dz)
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true>), grid, dim3(NT), 0, stream, DY, Y, X, save_mean, save_invstd, coef, DX, DZ, nvec, C);
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true>), grid, dim3(NT), 0, stream, DY, Y, X, coef, DX, DZ, nvec, C);
   else
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<false, false>), grid, dim3(NT), 0, stream, DY, Y, X, save_mean, save_invstd, coef, DX, DZ, nvec, C);
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<false, false>), grid, dim3(NT), 0, stream, DY, Y, X, coef, DX, DZ, nvec, C);
   return (int)hipGetLastError();
 }
