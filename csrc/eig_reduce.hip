@@ -1,33 +1,41 @@
 // Batched Householder tridiagonalisation for a ragged batch of K-FAC factors
-// (replaces rocSOLVER's sytrd and the round-1 per-class
-// csrc/eig_tridiag.hip path).
+// (reference semantics kfac/layers/utils.py:45-74 -- the
+// reduction stage of a symmetric eigensolver, LAPACK sytrd lower ==
+// row-major upper here).
 //
-// The reduction is a chain of n dependent columns, so what a column costs in
-// launches and per-workgroup latency sets the speed; every matrix of the
-// inverse update (all sizes) advances through ONE launch sequence:
+// The reduction is a chain of n dependent columns, so the latency of one
+// column sets the speed.  Every matrix of the inverse update (any sizes, up to
+// 16384) advances through ONE launch sequence, two launches per column:
 //
-//   fin(j)   one workgroup per 256 rows (each row's work done once):
-//            step 1  Householder scalars of column j-1 from the previous
-//                    launches' partial sums (|xh|^2, W^T xh, V^T xh, xh.a,
-//                    xh^T yh), re-reduced in a fixed order: deterministic
-//            step 2  w_{j-1} = tau (a + s yh - V s1 - W s2) + alpha2 v -> the
-//                    panel columns W/V[:, c-1], reflector row j-1, d/e/tau
-//            step 3  x_j = A row j - V W[j]^T - W V[j]^T, kept UNNORMALISED
-//                    (xh): its Householder scale needs a global norm that
-//                    only the next fin knows; y_j = a_j + s_j A22 xh_j is
-//                    linear in the scale.  Partial sums for fin(j+1).
-//   upd(j)   every NB = 32 columns: A22 -= V W^T + W V^T on the upper 128 x
-//            128 tiles, exact-f32 MFMA (v_mfma_f32_32x32x2_f32)
-//   symv(j)  yh = A22 xh over the upper tiles (an off-diagonal tile feeds its
-//            row and its column block: half the traffic of a full mat-vec),
-//            per-tile partials; lean (tile + 256 floats in, no panel data) so
-//            the bandwidth-bound early columns run at high occupancy
+//   F(j)  row-parallel, one workgroup per 64 rows of every matrix with j < n:
+//         1. the global sums of column j-1 (|xh|^2, xh.a, W^T xh, V^T xh from
+//            the row-block partials of S(j-1), xh^T yh from its tile sums),
+//            reduced once per workgroup: lane = partial kind, wave = quarter
+//            of the blocks, one LDS exchange -- fixed order, deterministic
+//         2. Householder scalars of column j-1; w_{j-1} = tau (a + s yh - V s1
+//            - W s2) + alpha2 v for the workgroup's rows -> panel column c-1
+//         3. x_j = A row j - V W[j]^T - W V[j]^T (UNNORMALISED: its scale needs
+//            a global norm only the next F knows; y_j = a_j + s_j A22 xh_j is
+//            linear in it), a_j = column j+1 of A22 -> XH, AV
+//         No partial sums, no workgroup barrier after a global store.
+//   U(j)  at a panel start (every NB = 32 columns): A22 -= V W^T + W V^T on
+//         the upper 128 x 128 tiles, exact-f32 MFMA
+//   S(j)  tile-parallel: yh = A22 xh over the upper tiles (an off-diagonal
+//         tile feeds its row and its column block), per-row partials + one
+//         xh.yh sum per tile; and, in extra workgroups of the same launch,
+//         the per-128-row-block partial sums F(j+1) needs (|xh|^2, xh.a, the
+//         panel's W^T xh and V^T xh)
+//
+// Round 2 computed those row-block sums at the end of F with a 63-shuffle
+// butterfly and a workgroup barrier that drained F's global stores; F took
+// ~9.5 us per column (profiles/r3_stamps_*.log).  Moving them into S, where
+// they run beside the tiles, leaves F a load -> reduce -> scalar -> row chain.
 //
 // The recurrence (unnormalised xh, scalars one launch late) is modelled
 // exactly in scripts/models/sytrd_fused_model.py (fp64, 1e-15).  Storage:
-// row-major, UPPER triangle maintained (== LAPACK lower, column-major); output
-// d, e, tau and reflector j in row j (beta at j+1, v[2:] after): the layout
-// the compact-WY back-transformation (csrc/eig_library.hip) reads.
+// row-major, UPPER triangle maintained; output d, e, tau and reflector j in
+// row j (beta at j+1, v[2:] after): the layout the compact-WY back-
+// transformation (csrc/eig_library.hip) reads.
 #include "common.h"
 
 #include <algorithm>
@@ -40,27 +48,28 @@
 namespace {
 
 constexpr int TB = 128;        // symv / update tile
-constexpr int FB = 256;        // rows per fin workgroup
+constexpr int FB = 64;         // rows per F workgroup
 constexpr int NB = 32;         // panel width
-constexpr int RSW = 64;       // fin partial kinds per block (see K_W / K_V)
+constexpr int NK = 64;         // partial kinds per row block (one per lane)
+constexpr int K_W = 2, K_V = 2 + (NB - 1);   // kinds: |xh|^2, xh.a, W^T xh, V^T xh
+static_assert(K_V + NB - 1 == NK, "partial kinds must fill one wave");
 constexpr int MAXM = 255;      // matrices per batch
-constexpr int NTMAX = 40;      // 128-row blocks (n <= 5120)
-constexpr int PQ4 = NTMAX / 4; // float4 loads of a row's yh partials
-constexpr int NFMAX = (NTMAX * TB + FB - 1) / FB;   // fin blocks
+constexpr int NMAX = 16384;    // largest factor (F's unrolled loads: RB <= 128 blocks)
 
 struct RMat {
-  float* A; long long lda; int n; int nt; int nf; int pad;
+  float* A; long long lda; int n; int nt; int nf; int ld;   // ld = nt * TB
   float* d; float* e; float* tau;
-  float* V; float* W;                     // n x NB (row r: NB floats)
-  float* P; float* TS; float* RS; float* XH; float* SC;
-  long long sP, sTS, sRS, sXH;            // slot strides (floats); 2 slots each
+  float* V; float* W;                     // NB columns of ld floats (column-major)
+  float* P; float* TS; float* DS; float* XH; float* AV; float* SC;   // P: nt columns of ld
+  long long sP, sTS, sDS, sX;             // slot strides (floats); 2 slots each
 };
 
-// debug: per-launch phase stamps of workgroup 0 of fin (s_memrealtime, 100 MHz)
+// debug: per-column stamps (s_memrealtime, 100 MHz) of the first F and S
+// workgroups into a caller buffer (kfac_reduce_stamps)
 __device__ unsigned long long* g_stamps = nullptr;
 #define STAMP(k)                                                                            \
   do {                                                                                      \
-    if (stamps && tid == 0) stamps[(long long)j * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    if (stamps && threadIdx.x == 0) stamps[(long long)j * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
 __device__ inline void tri_index(int t, int mb, int& I, int& K) {
@@ -80,176 +89,164 @@ __device__ inline void hh_scalars(double alpha, double sig2, double& beta, doubl
   }
 }
 
-// workgroup -> (matrix, local index) from the launch's host-built offsets:
-// one compare per thread (offsets ascending), not a serial scan
-__device__ inline void map_block(const int* __restrict__ offs, int nact, int* soff, int& mat,
-                                 int& local) {
-  __shared__ int sm;
-  const int t = threadIdx.x, b = blockIdx.x;
-  if (t <= nact) soff[t] = offs[t];
-  __syncthreads();
-  if (t < nact && soff[t] <= b && b < soff[t + 1]) sm = t;
-  __syncthreads();
-  mat = sm;
-  local = b - soff[mat];
-}
-
-// in-register transpose-reduce of 64 values per lane over the wave: lane L
-// ends with the wave sum of value L (63 shuffles; pairwise, fixed order)
-template <int M>
-__device__ __forceinline__ void butterfly_stage(float (&v)[64], int lane) {
-  const bool up = (lane & M) != 0;
-#pragma unroll
-  for (int i = 0; i < M; ++i) {
-    const float send = up ? v[i] : v[i + M];
-    const float keep = up ? v[i + M] : v[i];
-    v[i] = keep + __shfl_xor(send, M, 64);
+// workgroup -> (matrix, first workgroup of that matrix) from the launch's
+// ascending offsets: lane i tests offset i (one load + ballot, no LDS)
+__device__ __forceinline__ void find_mat(const int* __restrict__ offs, int nact, int& mi,
+                                         int& base) {
+  const int lane = threadIdx.x & 63, b = blockIdx.x;
+  int cnt = 0;
+  for (int c0 = 0; c0 < nact; c0 += 64) {
+    const int i = c0 + lane;
+    const int o = gld_if(gptr(offs), i, i < nact, 0x7fffffff);
+    cnt += __popcll(__ballot(o <= b));
   }
-}
-__device__ __forceinline__ float butterfly64(float (&v)[64]) {
-  const int lane = threadIdx.x & 63;
-  butterfly_stage<32>(v, lane);
-  butterfly_stage<16>(v, lane);
-  butterfly_stage<8>(v, lane);
-  butterfly_stage<4>(v, lane);
-  butterfly_stage<2>(v, lane);
-  butterfly_stage<1>(v, lane);
-  return v[0];
+  mi = cnt - 1;
+  base = offs[mi];
 }
 
-// ------------------------------------------------------------------- fin
-// partial-sum kinds of a fin block (RSW = 64: one per lane of the butterfly):
-// |xh|^2, xh.a, W^T xh and V^T xh over the panel columns before the current
-// one (at most NB - 1 of them)
-constexpr int K_W = 2, K_V = 2 + (NB - 1);
-static_assert(K_V + NB - 1 == RSW, "fin partial kinds must fill one wave");
-constexpr int TSQ = (NTMAX * (NTMAX + 1) / 2 + 255) / 256;   // float4 tile-sum loads per lane
-constexpr int NFP = (NFMAX + 3) / 4 * 4;                      // RS: blocks per kind (float4 rows)
-// Every wave keeps its loads under the 63 a wave can have in flight
-// (vmcnt is 6 bits): past that, each extra batch costs a full round trip.
-
-struct FinWave {                  // one wave's private slice (no barrier needed)
-  float s12[2 * NB];              // s1, s2
-  float vw[4][NB];                // V[j], W[j], V[j+1], W[j+1] (current panel columns)
-};
-
-// Every wave of every fin workgroup derives column j-1's scalars and rows
-// j / j+1 itself (redundantly, from the same partials, in the same order), so
-// the waves never wait for each other until the block's partial sums at the
-// end; the cross-lane sums are DPP / permlane (common.h wave_sum*).
-__global__ __launch_bounds__(256) void sytrd_fin_kernel(const RMat* __restrict__ mats,
-                                                        const int* __restrict__ offs, int nact,
-                                                        int j) {
-  __shared__ FinWave SW[4];
-  __shared__ float wred[4][RSW];
-  __shared__ int soff[MAXM + 1];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+// ------------------------------------------------------------------- F
+// One workgroup per FB = 64 rows: lane = row, wave q = a quarter of the
+// per-row work (panel columns 8q .. 8q+7, yh partial columns s0p+q+4i), so a
+// workgroup moves ~25 KB instead of ~100 KB (the round-2 kernel's 256 rows x
+// (32+32 panel floats + one partial per tile) came in at ~25 GB/s per
+// workgroup: profiles/r3_r2kernel_stamps_*.log).  RB >= the active 128-row
+// blocks of S(j-1) (nt - j / TB) of every matrix of the launch: fixes the
+// number of partial loads per thread, all issued up front.
+template <int RB>
+__global__ __launch_bounds__(256) void red_fin_kernel(const RMat* __restrict__ mats,
+                                                      const int* __restrict__ offs, int nact,
+                                                      int j) {
+  constexpr int DQ = RB / 4;                            // DS loads per thread
+  constexpr int TQ = (RB * (RB + 1) / 2 + 1023) / 1024; // float4 TS loads per thread
+  constexpr int PK = RB / 4;                            // P partials per thread
+  constexpr int XQ = NB / 4;                            // panel columns per quarter
+  __shared__ double sdk[4][NK];
+  __shared__ double stt[4];
+  __shared__ float sq[4][4][FB];                        // per quarter: yh, c3, c3', c2 of each row
+  const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6;
   unsigned long long* const stamps = blockIdx.x == 0 ? g_stamps : nullptr;
   STAMP(0);
-  if (stamps && tid == 0) stamps[(long long)j * 16 + 8] = __builtin_amdgcn_s_memtime();
-  int mi, local;
-  map_block(offs, nact, soff, mi, local);
+  int mi, base;
+  find_mat(offs, nact, mi, base);
   const RMat M = mats[mi];
   const int n = M.n, nt = M.nt;
-  const long long lda = M.lda;
-  const int bf = j / FB + local;           // this workgroup's 256-row block
-  const int r = bf * FB + tid;
-  const bool lead = (local == 0 && wave == 0);
-  const bool fin = (j == n - 1);
-  const bool has1 = (j + 1 < n);
+  const long long lda = M.lda, ld = M.ld;
+  // first row block: the first row S(j) reads (its tiles start at a 128-row
+  // boundary <= j+1; rows below j+1 get xh = a = 0), or row j's block
+  const int fb0 = min(((j + 1) / TB) * (TB / FB), j / FB);
+  const int r = (fb0 + (blockIdx.x - base)) * FB + lane;   // this thread's row
+  const bool lead = (blockIdx.x == base && q == 0);
+  const bool last = (j == n - 1);
+  const bool j1 = (j >= 1), has1 = (j + 1 < n);
   const int c = j % NB;
-  const int cp = (j >= 1) ? (c == 0 ? NB - 1 : c - 1) : 0;
+  const int cp = j1 ? (c == 0 ? NB - 1 : c - 1) : 0;    // panel column of j-1 (cc = cp + 1)
   const bool pstart = (c == 0 && j > 0);
-  const int cc = pstart ? NB : c;          // panel columns subtracted from A rows j, j+1
   const int cs = j & 1, ps = cs ^ 1;
-  const int s0p = j / TB;                  // first tile block of symv(j-1)
-  const int ntp = (nt + 3) & ~3;
-  const int ntri = (nt - s0p) * (nt - s0p + 1) / 2;   // tiles of symv(j-1)
-  const int f0p = (j - 1) / FB;            // first fin block of fin(j-1)
-  const AS1 float* Pp = gptr(M.P) + ps * M.sP;
-  const AS1 float* XHp = gptr(M.XH) + ps * M.sXH;
-  const AS1 float* RSp = gptr(M.RS) + ps * M.sRS;
+  const int s0p = j / TB;                               // first block of S(j-1)
+  const int ntri = (nt - s0p) * (nt - s0p + 1) / 2;     // tiles of S(j-1)
+  const AS1 float* DSp = gptr(M.DS) + ps * M.sDS;
   const AS1 float* TSp = gptr(M.TS) + ps * M.sTS;
+  const AS1 float* Pp = gptr(M.P) + ps * M.sP;
+  const AS1 float* XHp = gptr(M.XH) + ps * M.sX;
   AS1 float* const gA = gptr(M.A);
   AS1 float* const gV = gptr(M.V);
   AS1 float* const gW = gptr(M.W);
   AS1 float* const gSC = gptr(M.SC);
   STAMP(1);
 
-  // ---- every load up front, branch-free (one memory round trip)
-  const bool j1 = (j >= 1);
-  // fin(j-1) block partials, kind-major [RSW][NFP]: lane = kind, float4s of
-  // 4 blocks (blocks f0p .. nf-1 are valid)
-  fx4 rq[NFP / 4];
+  // ---- every load up front (one memory round trip).  Indices are clamped
+  // into the buffers and out-of-range terms dropped at use: per-load
+  // predicates would cost one SGPR mask each.
+  float dk[DQ];                                         // kind `lane`, blocks s0p + q + 4 i
 #pragma unroll
-  for (int u = 0; u < NFP / 4; ++u) rq[u] = *(const AS1 fx4*)(RSp + lane * NFP + 4 * u);
-  fx4 tq[TSQ];                             // symv(j-1) tile sums, triangle order
+  for (int i = 0; i < DQ; ++i) dk[i] = DSp[(long long)min(s0p + q + 4 * i, nt - 1) * NK + lane];
+  fx4 tq[TQ];
+  const fx4 z4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int u = 0; u < TSQ; ++u) tq[u] = *(const AS1 fx4*)(TSp + 4 * lane + 256 * u);
-  const bool okp = j1 && lane >= s0p && lane < nt;
-  const float pj = gld_if(Pp, j * ntp + lane, okp, 0.f);
-  const float pj1 = gld_if(Pp, (j + 1) * ntp + lane, okp && has1, 0.f);
+  for (int u = 0; u < TQ; ++u)
+    tq[u] = gld_if((const AS1 fx4*)TSp, (long long)tid + 256 * u, j1 && 4 * (tid + 256 * u) < ntri, z4);
+  // rows j, j+1: yh partials (lane = tile column K, two per lane past 64)
+  const bool k0ok = j1 && lane >= s0p && lane < nt, k1ok = j1 && lane + 64 < nt;
+  const float pj = gld_if(Pp, lane * ld + j, k0ok, 0.f) +
+                   gld_if(Pp, (lane + 64) * ld + j, k1ok, 0.f);
+  const float pj1 = gld_if(Pp, lane * ld + j + 1, k0ok && has1, 0.f) +
+                    gld_if(Pp, (lane + 64) * ld + j + 1, k1ok && has1, 0.f);
   const float xhj1 = gld_if(XHp, j + 1, j1 && has1, 0.f);
   const float alpha = gSC[ps * 4];
   const float dprev = gSC[ps * 4 + 1];
-  float vj = gld_if(gV, j * NB + lane, lane < NB, 0.f);
-  float wj = gld_if(gW, j * NB + lane, lane < NB, 0.f);
-  float vj1 = gld_if(gV, (j + 1) * NB + lane, lane < NB && has1, 0.f);
-  float wj1 = gld_if(gW, (j + 1) * NB + lane, lane < NB && has1, 0.f);
+  float vj = gld_if(gV, lane * ld + j, lane < NB, 0.f);           // panel row j (lane = column)
+  float wj = gld_if(gW, lane * ld + j, lane < NB, 0.f);
+  float vj1 = gld_if(gV, lane * ld + j + 1, lane < NB && has1, 0.f);
+  float wj1 = gld_if(gW, lane * ld + j + 1, lane < NB && has1, 0.f);
   const float ajj = gA[(long long)j * lda + j];
   const float ajj1 = gld_if(gA, (long long)j * lda + j + 1, has1, 0.f);
-  // this thread's row (loads from a clamped row; unused lanes masked later)
-  const bool rok = r < n && r >= j;
+  const bool rok = r < n && r >= j + 1;                 // rows that get w_{j-1} and x_j
   const int rc = min(r, n - 1);
-  float vr[NB], wr[NB];
-  {
-    const AS1 fx4* v4 = (const AS1 fx4*)(gV + rc * NB);
-    const AS1 fx4* w4 = (const AS1 fx4*)(gW + rc * NB);
+  float vr[XQ], wr[XQ];                                 // this quarter's panel columns of row r
 #pragma unroll
-    for (int x = 0; x < NB / 4; ++x) {
-      const fx4 a4 = v4[x], b4 = w4[x];
-      vr[4 * x] = a4.x; vr[4 * x + 1] = a4.y; vr[4 * x + 2] = a4.z; vr[4 * x + 3] = a4.w;
-      wr[4 * x] = b4.x; wr[4 * x + 1] = b4.y; wr[4 * x + 2] = b4.z; wr[4 * x + 3] = b4.w;
-    }
+  for (int i = 0; i < XQ; ++i) {
+    vr[i] = gV[(q * XQ + i) * ld + rc];
+    wr[i] = gW[(q * XQ + i) * ld + rc];
   }
-  const float arow = gA[(long long)j * lda + rc];                              // base row j
-  const float brow = gld_if(gA, (long long)(j + 1) * lda + rc, has1 && r >= j + 1, 0.f);
+  const float arow = gA[(long long)j * lda + rc];                     // base row j
+  const float brow = gld_if(gA, (long long)(j + 1) * lda + rc, has1 && rok, 0.f);
   const float xhp = XHp[rc];
-  fx4 pq[PQ4];
-  {
-    const AS1 fx4* pp = (const AS1 fx4*)(Pp + rc * ntp);
-    const fx4 z4 = {0.f, 0.f, 0.f, 0.f};
+  float pk[PK];                                          // yh partials, tile columns s0p + q + 4 i
 #pragma unroll
-    for (int u = 0; u < PQ4; ++u) pq[u] = gld_if(pp, u, j1 && 4 * u + 3 >= s0p && 4 * u < nt, z4);
-  }
-  double pK = 0.0, pT = 0.0;               // this lane's kind over the blocks; tile sums
-#pragma unroll
-  for (int u = 0; u < NFP / 4; ++u) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int bb = 4 * u + e;
-      pK += (j1 && bb >= f0p && bb < M.nf) ? (double)rq[u][e] : 0.0;
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < TSQ; ++u) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int f = 4 * lane + 256 * u + e;
-      pT += (j1 && f < ntri) ? (double)tq[u][e] : 0.0;
-    }
-  }
-  // kinds to their consumers: |xh|^2 and xh.a broadcast, W_x / V_x to lane x
-  const double pW = __shfl(pK, (K_W + lane) & 63, 64);
-  const double pV = __shfl(pK, (K_V + lane) & 63, 64);
-  const double sig2_b = __shfl(pK, 0, 64), xa_b = __shfl(pK, 1, 64);
-  STAMP(2);
+  for (int i = 0; i < PK; ++i) pk[i] = Pp[(long long)min(s0p + q + 4 * i, nt - 1) * ld + rc];
 
-  // ---- step 1 (per wave): scalars of column j-1; step 2 for rows j, j+1
-  double beta_p = 0.0, tau_p = 0.0, s_p = 0.0, alpha2 = 0.0;
+  // ---- global sums of column j-1 (wave = quarter of the blocks, lane = kind)
+  //      and this quarter's share of each row's yh and old-panel corrections
+  {
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < DQ; ++i) acc += (j1 && s0p + q + 4 * i < nt) ? (double)dk[i] : 0.0;
+    sdk[q][lane] = acc;
+    double t = 0.0;
+#pragma unroll
+    for (int u = 0; u < TQ; ++u) {
+      const int f = 4 * (tid + 256 * u);
+      t += (f < ntri) ? (double)tq[u].x : 0.0;
+      t += (f + 1 < ntri) ? (double)tq[u].y : 0.0;
+      t += (f + 2 < ntri) ? (double)tq[u].z : 0.0;
+      t += (f + 3 < ntri) ? (double)tq[u].w : 0.0;
+    }
+    t = wave_sum_d(t);
+    if (lane == 0) stt[q] = t;
+    float yq = 0.f;
+#pragma unroll
+    for (int i = 0; i < PK; ++i) yq += (j1 && s0p + q + 4 * i < nt) ? pk[i] : 0.f;
+    float c3 = 0.f, c3p = 0.f;                           // old columns x < cp
+#pragma unroll
+    for (int i = 0; i < XQ; ++i) {
+      const int x = q * XQ + i;
+      const float Wj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wj), x));
+      const float Vj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(vj), x));
+      const float Wj1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wj1), x));
+      const float Vj1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(vj1), x));
+      if (x < cp) {
+        c3 += vr[i] * Wj + wr[i] * Vj;
+        c3p += vr[i] * Wj1 + wr[i] * Vj1;
+      }
+    }
+    sq[q][0][lane] = yq;
+    sq[q][1][lane] = c3;
+    sq[q][2][lane] = c3p;
+  }
+  kfac_lds_barrier();
+  STAMP(2);
+  const double sig2 = ((sdk[0][0] + sdk[1][0]) + (sdk[2][0] + sdk[3][0]));
+  const double xa = ((sdk[0][1] + sdk[1][1]) + (sdk[2][1] + sdk[3][1]));
+  const int kw = K_W + min(lane, NB - 2), kv = K_V + min(lane, NB - 2);
+  const double pW = ((sdk[0][kw] + sdk[1][kw]) + (sdk[2][kw] + sdk[3][kw]));
+  const double pV = ((sdk[0][kv] + sdk[1][kv]) + (sdk[2][kv] + sdk[3][kv]));
+  const double xy = ((stt[0] + stt[1]) + (stt[2] + stt[3]));
+
+  // ---- step 1 (every wave, identically): scalars of column j-1; rows j, j+1
+  double tau_p = 0.0, s_p = 0.0, alpha2 = 0.0;
   float s1f = 0.f, s2f = 0.f;
-  if (j >= 1) {
-    const double sig2 = sig2_b, xa = xa_b, xy = wave_sum_d(pT);
+  if (j1) {
+    double beta_p;
     hh_scalars((double)alpha, sig2, beta_p, tau_p, s_p);
     // s1 = W^T v, s2 = V^T v over rows >= j (v[j] = 1): row j of the panel
     double s1 = 0.0, s2 = 0.0;
@@ -275,8 +272,8 @@ __global__ __launch_bounds__(256) void sytrd_fin_kernel(const RMat* __restrict__
     }
     if (lead) {
       if (lane == cp) {
-        gV[j * NB + cp] = 1.f;
-        gW[j * NB + cp] = ww;
+        gV[cp * ld + j] = 1.f;
+        gW[cp * ld + j] = ww;
       }
       if (lane == 0) {
         M.d[j - 1] = dprev;
@@ -286,11 +283,11 @@ __global__ __launch_bounds__(256) void sytrd_fin_kernel(const RMat* __restrict__
       }
     }
   }
-  {   // d_j = A(j, j) - 2 V[j] . W[j] over the panel columns
-    const double dd = wave_sum_d(lane < cc ? (double)vj * (double)wj : 0.0);
+  {   // d_j = A(j, j) - 2 V[j] . W[j] over the panel columns 0 .. cp
+    const double dd = wave_sum_d(j1 && lane <= cp ? (double)vj * (double)wj : 0.0);
     if (lead && lane == 0) {
       const float dj = (float)((double)ajj - 2.0 * dd);
-      if (fin) {
+      if (last) {
         M.d[j] = dj;
         M.e[j] = 0.f;
         M.tau[j] = 0.f;
@@ -299,114 +296,85 @@ __global__ __launch_bounds__(256) void sytrd_fin_kernel(const RMat* __restrict__
       }
     }
   }
-  FinWave& F = SW[wave];
-  if (lane < NB) {
-    F.s12[lane] = s1f;
-    F.s12[NB + lane] = s2f;
-    F.vw[0][lane] = vj; F.vw[1][lane] = wj;
-    F.vw[2][lane] = vj1; F.vw[3][lane] = wj1;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  STAMP(3);
-
-  // ---- step 2, this thread's row (r >= j+1)
-  if (j >= 1 && rok && r >= j + 1) {
-    float yh = 0.f;
+  // this quarter's share of the step-2 correction V s1 + W s2 (columns < cp)
+  {
+    float c2 = 0.f;
 #pragma unroll
-    for (int u = 0; u < PQ4; ++u) {
-      if (4 * u >= s0p) yh += pq[u].x;
-      if (4 * u + 1 >= s0p) yh += pq[u].y;
-      if (4 * u + 2 >= s0p) yh += pq[u].z;
-      if (4 * u + 3 >= s0p) yh += pq[u].w;
+    for (int i = 0; i < XQ; ++i) {
+      const int x = q * XQ + i;
+      const float a1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s1f), x));
+      const float a2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s2f), x));
+      if (x < cp) c2 += vr[i] * a1 + wr[i] * a2;
     }
-    float corr = 0.f;
-#pragma unroll
-    for (int x = 0; x < NB; ++x)
-      if (x < cp) corr += vr[x] * F.s12[x] + wr[x] * F.s12[NB + x];
-    const float vmy = (float)(s_p * (double)xhp);
-    const float wmy =
-        (float)(tau_p * ((double)arow + s_p * (double)yh - (double)corr) + alpha2 * (double)vmy);
-#pragma unroll
-    for (int x = 0; x < NB; ++x)
-      if (x == cp) { vr[x] = vmy; wr[x] = wmy; }
-    gV[r * NB + cp] = vmy;
-    gW[r * NB + cp] = wmy;
+    sq[q][3][lane] = c2;
+  }
+  kfac_lds_barrier();
+  STAMP(3);
+  if (q != 0) return;
+
+  // ---- wave 0, this thread's row: step 2 (w_{j-1}, v_{j-1}), step 3 (x_j, a_j)
+  const float yh = (sq[0][0][lane] + sq[1][0][lane]) + (sq[2][0][lane] + sq[3][0][lane]);
+  const float c2 = (sq[0][3][lane] + sq[1][3][lane]) + (sq[2][3][lane] + sq[3][3][lane]);
+  const float c3 = (sq[0][1][lane] + sq[1][1][lane]) + (sq[2][1][lane] + sq[3][1][lane]);
+  const float c3p = (sq[0][2][lane] + sq[1][2][lane]) + (sq[2][2][lane] + sq[3][2][lane]);
+  float vmy = 0.f, wmy = 0.f;
+  if (j1 && rok) {
+    vmy = (float)(s_p * (double)xhp);
+    wmy = (float)(tau_p * ((double)arow + s_p * (double)yh - (double)c2) + alpha2 * (double)vmy);
+    gV[cp * ld + r] = vmy;
+    gW[cp * ld + r] = wmy;
     gA[(long long)(j - 1) * lda + r] = vmy;      // reflector j-1: v[2:] (r >= j+1)
   }
-  if (fin) return;      // uniform: d/e/tau of the last two columns are written
-  STAMP(4);
-
-  // ---- step 3: x_j (rows >= j+1), a_j; alpha_j
+  if (last) return;     // uniform: d/e/tau of the last two columns are written
   float xmy = 0.f, amy = 0.f;
-  if (rok && r >= j + 1) {
-    float corr = 0.f, corr1 = 0.f;
-#pragma unroll
-    for (int x = 0; x < NB; ++x) {
-      if (x < cc) {
-        corr += vr[x] * F.vw[1][x] + wr[x] * F.vw[0][x];
-        corr1 += vr[x] * F.vw[3][x] + wr[x] * F.vw[2][x];
-      }
-    }
-    xmy = arow - corr;
-    amy = pstart ? brow - corr1 : brow;    // a_j = row j+1 of the NEW panel's base
+  if (rok) {
+    // column cp (new): V[j][cp] = 1, W[j][cp] = ww; row j+1: vv1, ww1
+    const float Wj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wj), cp));
+    const float Vj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(vj), cp));
+    const float Wj1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wj1), cp));
+    const float Vj1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(vj1), cp));
+    const float t3 = j1 ? vmy * Wj + wmy * Vj : 0.f;
+    const float t3p = j1 ? vmy * Wj1 + wmy * Vj1 : 0.f;
+    xmy = arow - (c3 + t3);
+    amy = pstart ? brow - (c3p + t3p) : brow;   // a_j = row j+1 of the NEW panel's base
   }
-  const float xh = (rok && r >= j + 2) ? xmy : 0.f;
   if (r == j + 1 && r < n) gSC[cs * 4] = xmy;      // alpha_j
-  if (r < n) gptr(M.XH)[cs * M.sXH + r] = xh;
-  // ---- partial sums for fin(j+1): wave butterfly, then 4 waves in order
-  {
-    const int cn = pstart ? 0 : c;                // the current panel's columns (< NB)
-    float pv[64];
-    pv[0] = xh * xh;
-    pv[1] = xh * amy;
-#pragma unroll
-    for (int x = 0; x < NB - 1; ++x) {
-      pv[K_W + x] = (x < cn) ? wr[x] * xh : 0.f;
-      pv[K_V + x] = (x < cn) ? vr[x] * xh : 0.f;
-    }
-    wred[wave][lane] = butterfly64(pv);
+  if (r < n) {
+    gptr(M.XH)[cs * M.sX + r] = (rok && r >= j + 2) ? xmy : 0.f;
+    gptr(M.AV)[cs * M.sX + r] = amy;
   }
-  __syncthreads();
-  STAMP(5);
-  if (tid < RSW)
-    gptr(M.RS)[cs * M.sRS + tid * NFP + bf] =
-        (float)(((double)wred[0][tid] + (double)wred[1][tid]) +
-                ((double)wred[2][tid] + (double)wred[3][tid]));
-  STAMP(6);
-  if (stamps && tid == 0) stamps[(long long)j * 16 + 9] = __builtin_amdgcn_s_memtime();
+  STAMP(4);
 }
 
-// ------------------------------------------------------------------- upd
+// ------------------------------------------------------------------- U
 // A[I][K] -= L_I R_K^T with L = [V | W], R = [W | V] (rows >= q+1, upper):
 // the panel's rank-2NB update, exact-f32 MFMA, 4 waves of 64 x 64.
-__global__ __launch_bounds__(256) void sytrd_upd_kernel(const RMat* __restrict__ mats,
-                                                        const int* __restrict__ offs, int nact,
-                                                        int q) {
+__global__ __launch_bounds__(256) void red_upd_kernel(const RMat* __restrict__ mats,
+                                                      const int* __restrict__ offs, int nact,
+                                                      int q) {
   __shared__ float sL[TB][2 * NB + 1];
   __shared__ float sR[TB][2 * NB + 1];
-  __shared__ int soff[MAXM + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  int mi, local;
-  map_block(offs, nact, soff, mi, local);
+  int mi, base;
+  find_mat(offs, nact, mi, base);
   const RMat M = mats[mi];
   const int n = M.n, nt = M.nt;
   const int s0 = (q + 1) / TB;
   int I, K;
-  tri_index(local, nt - s0, I, K);
+  tri_index(blockIdx.x - base, nt - s0, I, K);
   I += s0; K += s0;
   const AS1 float* gV = gptr(M.V);
   const AS1 float* gW = gptr(M.W);
 #pragma unroll
   for (int e0 = 0; e0 < TB * NB; e0 += 256) {
     const int e = e0 + tid;
-    const int rr = e / NB, x = e - rr * NB;
+    const int x = e / TB, rr = e - x * TB;            // rows fastest: coalesced columns
     const int ri = I * TB + rr, rk = K * TB + rr;
-    const float vi = gld_if(gV, ri * NB + x, ri < n, 0.f);
-    const float wi = gld_if(gW, ri * NB + x, ri < n, 0.f);
-    const float vk = gld_if(gV, rk * NB + x, rk < n, 0.f);
-    const float wk = gld_if(gW, rk * NB + x, rk < n, 0.f);
+    const long long ld = M.ld;
+    const float vi = gld_if(gV, x * ld + ri, ri < n, 0.f);
+    const float wi = gld_if(gW, x * ld + ri, ri < n, 0.f);
+    const float vk = gld_if(gV, x * ld + rk, rk < n, 0.f);
+    const float wk = gld_if(gW, x * ld + rk, rk < n, 0.f);
     sL[rr][x] = vi; sL[rr][NB + x] = wi;
     sR[rr][x] = wk; sR[rr][NB + x] = vk;
   }
@@ -459,33 +427,86 @@ __global__ __launch_bounds__(256) void sytrd_upd_kernel(const RMat* __restrict__
     }
 }
 
-// ------------------------------------------------------------------- symv
-__global__ __launch_bounds__(256) void sytrd_symv2_kernel(const RMat* __restrict__ mats,
-                                                          const int* __restrict__ offs, int nact,
-                                                          int j) {
+// ------------------------------------------------------------------- S
+// Workgroups 0 .. ntri-1 of a matrix: tile (I, K) of the upper triangle of
+// A22, yh partials per row into P (row sums of block I at column K, column
+// sums of block K at column I) and the tile's xh.yh into TS.  Workgroups
+// ntri .. ntri + nb - 1: row block b = s0 + (local - ntri), the NK partial
+// kinds of its 128 rows into DS (lane = kind, wave = 32 rows, fixed order).
+__global__ __launch_bounds__(256) void red_symv_kernel(const RMat* __restrict__ mats,
+                                                       const int* __restrict__ offs, int nact,
+                                                       int j) {
   __shared__ float sv[2][TB];
   __shared__ float rowred[TB][33];
   __shared__ float colred[4][TB];
   __shared__ double tred[2];
-  __shared__ int soff[MAXM + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  int mi, local;
-  map_block(offs, nact, soff, mi, local);
+  unsigned long long* const stamps = g_stamps;
+  int mi, base;
+  find_mat(offs, nact, mi, base);
   const RMat M = mats[mi];
   const int n = M.n, nt = M.nt;
-  const long long lda = M.lda;
+  const long long lda = M.lda, ld = M.ld;
   const int s0 = (j + 1) / TB;
+  const int ntri = (nt - s0) * (nt - s0 + 1) / 2;
+  const int local = blockIdx.x - base;
+  const int cs = j & 1;
+  if (local >= ntri) {
+    // ---- row-block partial kinds: 0 |xh|^2, 1 xh.a, K_W+x W[:,x].xh, K_V+x V[:,x].xh
+    if (stamps && blockIdx.x == base + ntri && tid == 0)
+      stamps[(long long)j * 16 + 12] = __builtin_amdgcn_s_memrealtime();
+    const int b = s0 + (local - ntri);
+    const int cn = j % NB;                      // finished columns of the current panel
+    const AS1 float* XH = gptr(M.XH) + cs * M.sX;
+    const AS1 float* AV = gptr(M.AV) + cs * M.sX;
+    // wave w: kinds 16 w .. 16 w + 15; lane = row, two passes of 64 rows
+    float x2[2], a2[2], m[2][16];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int rr = b * TB + 64 * h + lane;
+      const bool ok = rr < n;
+      x2[h] = gld_if(XH, rr, ok, 0.f);
+      a2[h] = gld_if(AV, rr, ok, 0.f);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int k = 16 * wave + i;
+        const bool isw = k >= K_W && k < K_W + cn, isv = k >= K_V && k < K_V + cn;
+        const AS1 float* src = isw ? gptr(M.W) : gptr(M.V);
+        const int col = isw ? k - K_W : (isv ? k - K_V : 0);
+        m[h][i] = gld_if(src, col * ld + rr, ok && (isw || isv), 0.f);
+      }
+    }
+    float val[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int k = 16 * wave + i;
+      float acc = 0.f;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float v = k == 0 ? x2[h] : (k == 1 ? a2[h] : m[h][i]);
+        acc += v * x2[h];
+      }
+      val[i] = acc;
+    }
+    const float tot = kfac_butterfly16(val);      // lanes (lane & 15) == i: kind 16 wave + i
+    if (lane < 16) gptr(M.DS)[cs * M.sDS + (long long)b * NK + 16 * wave + lane] = tot;
+    if (stamps && blockIdx.x == base + ntri && tid == 0)
+      stamps[(long long)j * 16 + 13] = __builtin_amdgcn_s_memrealtime();
+    return;
+  }
+  if (stamps && blockIdx.x == 0 && tid == 0)
+    stamps[(long long)j * 16 + 10] = __builtin_amdgcn_s_memrealtime();
   int I, K;
   tri_index(local, nt - s0, I, K);
   I += s0; K += s0;
   const bool diag = (I == K);
-  const int cs = j & 1;
-  const int ntp = (nt + 3) & ~3;
-  // xh of the rows of blocks I and K (written by fin(j))
+  if (stamps && blockIdx.x == 0 && tid == 0)
+    stamps[(long long)j * 16 + 14] = __builtin_amdgcn_s_memrealtime();
+  // xh of the rows of blocks I and K (written by F(j))
   {
     const int h = tid >> 7, lr = tid & (TB - 1);
     const int rr = (h ? K : I) * TB + lr;
-    sv[h][lr] = gld_if(gptr(M.XH) + cs * M.sXH, rr, rr < n, 0.f);
+    sv[h][lr] = gld_if(gptr(M.XH) + cs * M.sX, rr, rr < n, 0.f);
   }
   const int hw = lane >> 5, cl = lane & 31;
   const int kk0 = cl * 4, k0 = K * TB + kk0;
@@ -503,6 +524,8 @@ __global__ __launch_bounds__(256) void sytrd_symv2_kernel(const RMat* __restrict
                         (ok && k0 + 2 < n) ? t.z : 0.f, (ok && k0 + 3 < n) ? t.w : 0.f);
   }
   __syncthreads();
+  if (stamps && blockIdx.x == 0 && tid == 0)
+    stamps[(long long)j * 16 + 15] = __builtin_amdgcn_s_memrealtime();
   float ca[4] = {0.f, 0.f, 0.f, 0.f};
   const float vk0 = sv[1][kk0], vk1 = sv[1][kk0 + 1], vk2 = sv[1][kk0 + 2], vk3 = sv[1][kk0 + 3];
 #pragma unroll
@@ -530,7 +553,7 @@ __global__ __launch_bounds__(256) void sytrd_symv2_kernel(const RMat* __restrict
 #pragma unroll
     for (int x = 0; x < 4; ++x) colred[wave][kk0 + x] = ca[x];
   }
-  __syncthreads();
+  kfac_lds_barrier();
   AS1 float* const Pc = gptr(M.P) + cs * M.sP;
   double tp = 0.0;
   if (tid < TB) {
@@ -539,39 +562,56 @@ __global__ __launch_bounds__(256) void sytrd_symv2_kernel(const RMat* __restrict
     for (int l = 0; l < 32; ++l) rs += rowred[tid][l];
     const float csum = colred[0][tid] + colred[1][tid] + colred[2][tid] + colred[3][tid];
     if (diag) {
-      Pc[((long long)I * TB + tid) * ntp + K] = rs + csum;
+      Pc[K * ld + I * TB + tid] = rs + csum;
       tp = (double)sv[0][tid] * (double)(rs + csum);
     } else {
-      Pc[((long long)I * TB + tid) * ntp + K] = rs;
-      Pc[((long long)K * TB + tid) * ntp + I] = csum;
+      Pc[K * ld + I * TB + tid] = rs;
+      Pc[I * ld + K * TB + tid] = csum;
       tp = (double)sv[0][tid] * (double)rs + (double)sv[1][tid] * (double)csum;
     }
   }
   tp = wave_sum_d(tp);
   if (lane == 0 && wave < 2) tred[wave] = tp;
-  __syncthreads();
+  kfac_lds_barrier();
   if (tid == 0) gptr(M.TS)[cs * M.sTS + local] = (float)(tred[0] + tred[1]);   // triangle order
+  if (stamps && blockIdx.x == 0 && tid == 0)
+    stamps[(long long)j * 16 + 11] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ------------------------------------------------------------------ host
 struct RPlan {
   RMat* d_mats = nullptr;
-  int* d_offs = nullptr;        // [3][nmax][nm + 1]: fin, upd, symv workgroup offsets
+  int* d_offs = nullptr;        // [3][nmax][nm + 1]: F, U, S workgroup offsets
   std::vector<int> n_sorted;    // descending
   std::vector<int> grid[3];     // [nmax] total workgroups per launch kind
   std::vector<int> nact[3];
+  std::vector<int> rb;          // [nmax] F unroll class
   int nmax = 0;
   hipGraphExec_t exec = nullptr;
 };
 
 inline int h_tri(int m) { return m * (m + 1) / 2; }
 
-// workgroups of matrix n at column j: fin, upd (panel start only), symv
+// workgroups of matrix n at column j: F, U (panel start only), S
 void counts(int n, int j, int out[3]) {
   const int nt = (n + TB - 1) / TB, nf = (n + FB - 1) / FB;
-  out[0] = (j <= n - 1) ? nf - j / FB : 0;
-  out[1] = (j % NB == 0 && j > 0 && j <= n - 2) ? h_tri(nt - (j + 1) / TB) : 0;
-  out[2] = (j <= n - 2) ? h_tri(nt - (j + 1) / TB) : 0;
+  const int ntr = nt - (j + 1) / TB;
+  out[0] = (j <= n - 1) ? nf - std::min(((j + 1) / TB) * (TB / FB), j / FB) : 0;
+  out[1] = (j % NB == 0 && j > 0 && j <= n - 2) ? h_tri(ntr) : 0;
+  out[2] = (j <= n - 2) ? h_tri(ntr) + ntr : 0;
+}
+
+int rb_class(int blocks) {
+  static const int cls[] = {8, 16, 24, 40, 64, 96, 128};
+  for (int c : cls)
+    if (blocks <= c) return c;
+  return -1;
+}
+
+template <int RB>
+void launch_fin(const RPlan& P, const int* of, int j, hipStream_t s) {
+  hipLaunchKernelGGL(red_fin_kernel<RB>, dim3(P.grid[0][j]), dim3(256), 0, s, P.d_mats, of,
+                     P.nact[0][j], j);
 }
 
 int enqueue(const RPlan& P, hipStream_t stream) {
@@ -579,14 +619,21 @@ int enqueue(const RPlan& P, hipStream_t stream) {
   const size_t kstride = (size_t)P.nmax * (nm + 1);
   for (int j = 0; j < P.nmax; ++j) {
     const int* of = P.d_offs + (size_t)j * (nm + 1);
-    hipLaunchKernelGGL(sytrd_fin_kernel, dim3(P.grid[0][j]), dim3(256), 0, stream,
-                       P.d_mats, of, P.nact[0][j], j);
+    switch (P.rb[j]) {
+      case 8: launch_fin<8>(P, of, j, stream); break;
+      case 16: launch_fin<16>(P, of, j, stream); break;
+      case 24: launch_fin<24>(P, of, j, stream); break;
+      case 40: launch_fin<40>(P, of, j, stream); break;
+      case 64: launch_fin<64>(P, of, j, stream); break;
+      case 96: launch_fin<96>(P, of, j, stream); break;
+      default: launch_fin<128>(P, of, j, stream); break;
+    }
     if (P.grid[1][j] > 0)
-      hipLaunchKernelGGL(sytrd_upd_kernel, dim3(P.grid[1][j]), dim3(256), 0, stream, P.d_mats,
+      hipLaunchKernelGGL(red_upd_kernel, dim3(P.grid[1][j]), dim3(256), 0, stream, P.d_mats,
                          of + kstride, P.nact[1][j], j);
     if (P.grid[2][j] > 0)
-      hipLaunchKernelGGL(sytrd_symv2_kernel, dim3(P.grid[2][j]), dim3(256), 0, stream,
-                         P.d_mats, of + 2 * kstride, P.nact[2][j], j);
+      hipLaunchKernelGGL(red_symv_kernel, dim3(P.grid[2][j]), dim3(256), 0, stream, P.d_mats,
+                         of + 2 * kstride, P.nact[2][j], j);
   }
   return (int)hipGetLastError();
 }
@@ -594,20 +641,39 @@ int enqueue(const RPlan& P, hipStream_t stream) {
 std::mutex g_mu;
 std::map<std::string, RPlan> g_plans;
 
+struct WsLayout {
+  long long V, W, P, TS, DS, XH, AV, SC, total, sP, sTS, sDS, sX;
+  int nt, ld;
+};
+
+WsLayout ws_layout(long long n) {
+  auto a16 = [](long long x) { return (x + 15) / 16 * 16; };
+  WsLayout L;
+  L.nt = (int)((n + TB - 1) / TB);
+  L.ld = L.nt * TB;
+  const long long nt = L.nt;
+  L.sP = a16(nt * L.ld);
+  L.sTS = a16(std::max<long long>(h_tri((int)nt), 4));
+  L.sDS = a16(nt * NK);
+  L.sX = a16(L.ld);
+  long long o = 0;
+  L.V = o; o += a16((long long)NB * L.ld);
+  L.W = o; o += a16((long long)NB * L.ld);
+  L.P = o; o += 2 * L.sP;
+  L.TS = o; o += 2 * L.sTS + 1024;         // float4 loads past the triangle stay inside
+  L.DS = o; o += 2 * L.sDS;
+  L.XH = o; o += 2 * L.sX;
+  L.AV = o; o += 2 * L.sX;
+  L.SC = o; o += a16(8);
+  L.total = (o + 63) / 64 * 64;
+  return L;
+}
+
 }  // namespace
 
-// workspace floats per matrix (V, W and the 2-slot partial rings)
-KFAC_API long long kfac_reduce_ws_floats(int n) {
-  const long long nt = (n + TB - 1) / TB, nf = (n + FB - 1) / FB;
-  auto a16 = [](long long x) { return (x + 15) / 16 * 16; };
-  long long s = 2 * a16((long long)n * NB);               // V, W
-  s += 2 * a16(nt * TB * ((nt + 3) / 4 * 4));             // P (row-major partials)
-  s += 2 * std::max<long long>(a16(nt * nt), 256LL * TSQ);   // TS
-  s += 2 * a16((long long)RSW * NFP);                     // RS (kind-major)
-  s += 2 * a16(n);                                        // XH
-  s += a16(8);                                            // SC
-  return (s + 63) / 64 * 64;
-}
+// workspace floats per matrix (V, W and the 2-slot partial rings), zeroed by
+// the caller once (rows past n of XH / AV / P must read 0)
+KFAC_API long long kfac_reduce_ws_floats(int n) { return ws_layout(n).total; }
 
 struct KfacReduceRecord {
   float* A; long long lda; float* d; float* e; float* tau; float* ws; long long n;
@@ -624,22 +690,16 @@ RPlan* plan_for(const KfacReduceRecord* recs, int count, bool capture, int* err)
   for (int oi : order) {
     const KfacReduceRecord& r = recs[oi];
     if (r.n < 2 || r.lda < r.n || (r.lda & 3)) { *err = -2; return nullptr; }
-    if (r.n > NTMAX * TB) { *err = -6; return nullptr; }
+    if (r.n > NMAX) { *err = -6; return nullptr; }
+    const WsLayout L = ws_layout(r.n);
     RMat M;
     memset(&M, 0, sizeof(M));
-    M.A = r.A; M.lda = r.lda; M.n = (int)r.n; M.nt = (int)((r.n + TB - 1) / TB);
+    M.A = r.A; M.lda = r.lda; M.n = (int)r.n; M.nt = L.nt; M.ld = L.ld;
     M.nf = (int)((r.n + FB - 1) / FB);
     M.d = r.d; M.e = r.e; M.tau = r.tau;
-    const long long nt = M.nt, n = r.n;
-    float* p = r.ws;
-    auto take = [&](long long fl) { float* o = p; p += (fl + 15) / 16 * 16; return o; };
-    M.V = take(n * NB); M.W = take(n * NB);
-    M.sP = (nt * TB * ((nt + 3) / 4 * 4) + 15) / 16 * 16; M.P = take(2 * M.sP);
-    M.sTS = std::max<long long>((nt * nt + 15) / 16 * 16, 256LL * TSQ);   // float4 reads
-    M.TS = take(2 * M.sTS);
-    M.sRS = RSW * NFP; M.RS = take(2 * M.sRS);
-    M.sXH = (n + 15) / 16 * 16; M.XH = take(2 * M.sXH);
-    M.SC = take(8);
+    M.V = r.ws + L.V; M.W = r.ws + L.W; M.P = r.ws + L.P; M.TS = r.ws + L.TS;
+    M.DS = r.ws + L.DS; M.XH = r.ws + L.XH; M.AV = r.ws + L.AV; M.SC = r.ws + L.SC;
+    M.sP = L.sP; M.sTS = L.sTS; M.sDS = L.sDS; M.sX = L.sX;
     mats.push_back(M);
   }
   const std::string key((const char*)mats.data(), sizeof(RMat) * mats.size());
@@ -659,6 +719,7 @@ RPlan* plan_for(const KfacReduceRecord* recs, int count, bool capture, int* err)
       P.grid[k].assign(P.nmax, 0);
       P.nact[k].assign(P.nmax, 0);
     }
+    P.rb.assign(P.nmax, 0);
     for (int j = 0; j < P.nmax; ++j) {
       int acc[3] = {0, 0, 0};
       for (int i = 0; i < nm; ++i) {
@@ -674,6 +735,10 @@ RPlan* plan_for(const KfacReduceRecord* recs, int count, bool capture, int* err)
         offs[((size_t)k * P.nmax + j) * (nm + 1) + nm] = acc[k];
         P.grid[k][j] = acc[k];
       }
+      // F reads the partials of S(j-1): nt - j / TB blocks of the largest matrix
+      const int nt0 = (P.n_sorted[0] + TB - 1) / TB;
+      P.rb[j] = rb_class(std::max(1, nt0 - j / TB));
+      if (P.rb[j] < 0) { *err = -6; return nullptr; }
     }
     if ((*err = (int)hipMalloc(&P.d_offs, sizeof(int) * offs.size())) != 0) return nullptr;
     if ((*err = (int)hipMemcpy(P.d_offs, offs.data(), sizeof(int) * offs.size(),
@@ -701,10 +766,10 @@ RPlan* plan_for(const KfacReduceRecord* recs, int count, bool capture, int* err)
 
 }  // namespace
 
-// Tridiagonalise `count` symmetric matrices (any sizes <= 5120) with one
+// Tridiagonalise `count` symmetric matrices (any sizes 2 .. 16384) with one
 // launch sequence for all of them: A (n x lda, row-major, upper triangle read
 // and overwritten by the reflectors), d, e, tau (n floats each), ws
-// (kfac_reduce_ws_floats(n) floats, 256-byte aligned).
+// (kfac_reduce_ws_floats(n) floats, 256-byte aligned, zeroed once).
 KFAC_API int kfac_reduce_batched(const KfacReduceRecord* recs, int count, int use_graph,
                                  hipStream_t stream) {
   if (count <= 0 || count > MAXM) return count <= 0 ? 0 : -5;
@@ -718,8 +783,9 @@ KFAC_API int kfac_reduce_batched(const KfacReduceRecord* recs, int count, int us
   return enqueue(*plan, stream);
 }
 
-// debug: record phase stamps of the first fin workgroup of every column into
-// `buf` (nmax x 16 uint64), or stop with nullptr
+// debug: record per-column stamps of the first F / S workgroups into `buf`
+// (nmax x 16 uint64: F 0-4, S tile 10-11, S row-block partials 12-13), or
+// stop with nullptr
 KFAC_API int kfac_reduce_stamps(unsigned long long* buf) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &buf, sizeof(buf));
 }
@@ -728,3 +794,5 @@ KFAC_API int kfac_reduce_prepare(const KfacReduceRecord* recs, int count) {
   int err = 0;
   return plan_for(recs, count, true, &err) ? 0 : (err ? err : -4);
 }
+
+KFAC_API int kfac_reduce_max_n() { return NMAX; }

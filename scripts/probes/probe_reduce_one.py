@@ -40,17 +40,20 @@ def main():
             n, b, graph, it, (time.perf_counter() - t) * 1e3,
             (time.perf_counter() - t) * 1e6 / n), flush=True)
     if os.environ.get('STAMPS'):
-        full = stamps.view(n, 16).cpu().double()
-        clk = (full[1:n - 2, 9] - full[1:n - 2, 8]) / ((full[1:n - 2, 6] - full[1:n - 2, 0]) * 10.0)
-        print('fin shader clock GHz: median %.2f  min %.2f  max %.2f' % (
-            clk.median().item(), clk.min().item(), clk.max().item()))
-        st = full[:, :7]
-        d = (st[:, 1:] - st[:, :-1]) * 10.0   # 100 MHz -> ns
+        full = stamps.view(n, 16).cpu().double() * 10.0     # 100 MHz -> ns
+        # F: 0 start, 1 record loaded, 2 sums reduced, 3 scalars, 4 end;
+        # S: 10/11 first tile workgroup start/end, 12/13 first row-block workgroup
         for name, rows in (('first 64 cols', slice(1, 65)), ('middle', slice(n // 2, n // 2 + 64)),
-                           ('last 64', slice(n - 65, n - 1))):
-            print(name, 'phase ns:', ' '.join('%7.0f' % v for v in d[rows].mean(0).tolist()),
-                  ' total %.0f' % ((st[rows, 6] - st[rows, 0]) * 10).mean().item())
-
+                           ('last 64', slice(n - 66, n - 2))):
+            f = full[rows]
+            nxt = full[rows.start + 1:rows.stop + 1]
+            ph = [(f[:, k + 1] - f[:, k]).mean().item() for k in range(4)]
+            print(name, 'F phases ns: ' + ' '.join('%6.0f' % v for v in ph),
+                  '| F total %6.0f | F->S gap %6.0f | S tile %6.0f (rec %5.0f load %5.0f rest %5.0f) | S part %6.0f | S->F %6.0f | col %6.0f' % (
+                      (f[:, 4] - f[:, 0]).mean().item(), (f[:, 10] - f[:, 4]).mean().item(),
+                      (f[:, 11] - f[:, 10]).mean().item(), (f[:, 14] - f[:, 10]).mean().item(),
+                      (f[:, 15] - f[:, 14]).mean().item(), (f[:, 11] - f[:, 15]).mean().item(), (f[:, 13] - f[:, 12]).mean().item(),
+                      (nxt[:, 0] - f[:, 11]).mean().item(), (nxt[:, 0] - f[:, 0]).mean().item()))
 
 if __name__ == '__main__':
     main()
