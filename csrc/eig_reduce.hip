@@ -39,6 +39,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -48,6 +49,7 @@
 namespace {
 
 constexpr int TB = 128;        // symv / update tile
+constexpr int HT = 64;         // rows per symv workgroup (half a tile)
 constexpr int FB = 64;         // rows per F workgroup
 constexpr int NB = 32;         // panel width
 constexpr int NK = 64;         // partial kinds per row block (one per lane)
@@ -117,8 +119,8 @@ __global__ __launch_bounds__(256) void red_fin_kernel(const RMat* __restrict__ m
                                                       const int* __restrict__ offs, int nact,
                                                       int j) {
   constexpr int DQ = RB / 4;                            // DS loads per thread
-  constexpr int TQ = (RB * (RB + 1) / 2 + 1023) / 1024; // float4 TS loads per thread
-  constexpr int PK = RB / 4;                            // P partials per thread
+  constexpr int TQ = (RB * (RB + 1) + 1023) / 1024;     // float4 TS loads per thread
+  constexpr int PK = RB / 4;                            // P partial pairs per thread
   constexpr int XQ = NB / 4;                            // panel columns per quarter
   __shared__ double sdk[4][NK];
   __shared__ double stt[4];
@@ -143,7 +145,7 @@ __global__ __launch_bounds__(256) void red_fin_kernel(const RMat* __restrict__ m
   const bool pstart = (c == 0 && j > 0);
   const int cs = j & 1, ps = cs ^ 1;
   const int s0p = j / TB;                               // first block of S(j-1)
-  const int ntri = (nt - s0p) * (nt - s0p + 1) / 2;     // tiles of S(j-1)
+  const int ntri = (nt - s0p) * (nt - s0p + 1);         // tile halves of S(j-1)
   const AS1 float* DSp = gptr(M.DS) + ps * M.sDS;
   const AS1 float* TSp = gptr(M.TS) + ps * M.sTS;
   const AS1 float* Pp = gptr(M.P) + ps * M.sP;
@@ -165,12 +167,18 @@ __global__ __launch_bounds__(256) void red_fin_kernel(const RMat* __restrict__ m
 #pragma unroll
   for (int u = 0; u < TQ; ++u)
     tq[u] = gld_if((const AS1 fx4*)TSp, (long long)tid + 256 * u, j1 && 4 * (tid + 256 * u) < ntri, z4);
-  // rows j, j+1: yh partials (lane = tile column K, two per lane past 64)
-  const bool k0ok = j1 && lane >= s0p && lane < nt, k1ok = j1 && lane + 64 < nt;
-  const float pj = gld_if(Pp, lane * ld + j, k0ok, 0.f) +
-                   gld_if(Pp, (lane + 64) * ld + j, k1ok, 0.f);
-  const float pj1 = gld_if(Pp, lane * ld + j + 1, k0ok && has1, 0.f) +
-                    gld_if(Pp, (lane + 64) * ld + j + 1, k1ok && has1, 0.f);
+  // rows j, j+1: yh partials, lane = P column 2T + h - 2 s0p (several per lane);
+  // column 2T+1 of a row of block B exists only for T <= B (see S)
+  const int bj = j / TB, bj1 = (j + 1) / TB;
+  auto pcol_ok = [&](int col, int B) { return j1 && col >= 2 * s0p && col < 2 * nt &&
+                                             ((col & 1) == 0 || (col >> 1) <= B); };
+  float pj = 0.f, pj1 = 0.f;
+#pragma unroll
+  for (int h = 0; h < (2 * RB + 63) / 64; ++h) {
+    const int col = 2 * s0p + lane + 64 * h;           // the 2 (nt - s0p) <= 2 RB live columns
+    pj += gld_if(Pp, col * ld + j, pcol_ok(col, bj), 0.f);
+    pj1 += gld_if(Pp, col * ld + j + 1, has1 && pcol_ok(col, bj1), 0.f);
+  }
   const float xhj1 = gld_if(XHp, j + 1, j1 && has1, 0.f);
   const float alpha = gSC[ps * 4];
   const float dprev = gSC[ps * 4 + 1];
@@ -191,9 +199,13 @@ __global__ __launch_bounds__(256) void red_fin_kernel(const RMat* __restrict__ m
   const float arow = gA[(long long)j * lda + rc];                     // base row j
   const float brow = gld_if(gA, (long long)(j + 1) * lda + rc, has1 && rok, 0.f);
   const float xhp = XHp[rc];
-  float pk[PK];                                          // yh partials, tile columns s0p + q + 4 i
+  float pk[2 * PK];                                      // yh partials, P columns 2T, 2T+1, T = s0p + q + 4 i
 #pragma unroll
-  for (int i = 0; i < PK; ++i) pk[i] = Pp[(long long)min(s0p + q + 4 * i, nt - 1) * ld + rc];
+  for (int i = 0; i < PK; ++i) {
+    const long long t2 = 2 * min(s0p + q + 4 * i, nt - 1);
+    pk[2 * i] = Pp[t2 * ld + rc];
+    pk[2 * i + 1] = Pp[(t2 + 1) * ld + rc];
+  }
 
   // ---- global sums of column j-1 (wave = quarter of the blocks, lane = kind)
   //      and this quarter's share of each row's yh and old-panel corrections
@@ -214,8 +226,13 @@ __global__ __launch_bounds__(256) void red_fin_kernel(const RMat* __restrict__ m
     t = wave_sum_d(t);
     if (lane == 0) stt[q] = t;
     float yq = 0.f;
+    const int br = rc / TB;
 #pragma unroll
-    for (int i = 0; i < PK; ++i) yq += (j1 && s0p + q + 4 * i < nt) ? pk[i] : 0.f;
+    for (int i = 0; i < PK; ++i) {
+      const int T = s0p + q + 4 * i;
+      yq += (j1 && T < nt) ? pk[2 * i] : 0.f;
+      yq += (j1 && T < nt && T <= br) ? pk[2 * i + 1] : 0.f;
+    }
     float c3 = 0.f, c3p = 0.f;                           // old columns x < cp
 #pragma unroll
     for (int i = 0; i < XQ; ++i) {
@@ -437,7 +454,7 @@ __global__ __launch_bounds__(256) void red_symv_kernel(const RMat* __restrict__ 
                                                        const int* __restrict__ offs, int nact,
                                                        int j) {
   __shared__ float sv[2][TB];
-  __shared__ float rowred[TB][33];
+  __shared__ float rowred[HT][33];
   __shared__ float colred[4][TB];
   __shared__ double tred[2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -448,7 +465,7 @@ __global__ __launch_bounds__(256) void red_symv_kernel(const RMat* __restrict__ 
   const int n = M.n, nt = M.nt;
   const long long lda = M.lda, ld = M.ld;
   const int s0 = (j + 1) / TB;
-  const int ntri = (nt - s0) * (nt - s0 + 1) / 2;
+  const int ntri = (nt - s0) * (nt - s0 + 1);          // tile halves
   const int local = blockIdx.x - base;
   const int cs = j & 1;
   if (local >= ntri) {
@@ -496,17 +513,21 @@ __global__ __launch_bounds__(256) void red_symv_kernel(const RMat* __restrict__ 
   }
   if (stamps && blockIdx.x == 0 && tid == 0)
     stamps[(long long)j * 16 + 10] = __builtin_amdgcn_s_memrealtime();
+  // tile (I, K), row half hr: 64 rows x 128 columns (32 KB: a workgroup pulls
+  // ~30 GB/s, so half tiles halve the launch's latency)
+  const int hr = local & 1;
   int I, K;
-  tri_index(local, nt - s0, I, K);
+  tri_index(local >> 1, nt - s0, I, K);
   I += s0; K += s0;
   const bool diag = (I == K);
   if (stamps && blockIdx.x == 0 && tid == 0)
     stamps[(long long)j * 16 + 14] = __builtin_amdgcn_s_memrealtime();
-  // xh of the rows of blocks I and K (written by F(j))
+  const int rb = I * TB + hr * HT;                     // first row of the half
+  // xh of the half's rows (sv[0]) and of block K's columns (sv[1]), from F(j)
   {
-    const int h = tid >> 7, lr = tid & (TB - 1);
-    const int rr = (h ? K : I) * TB + lr;
-    sv[h][lr] = gld_if(gptr(M.XH) + cs * M.sX, rr, rr < n, 0.f);
+    const AS1 float* XH = gptr(M.XH) + cs * M.sX;
+    if (tid < HT) sv[0][tid] = gld_if(XH, rb + tid, rb + tid < n, 0.f);
+    if (tid < TB) sv[1][tid] = gld_if(XH, K * TB + tid, K * TB + tid < n, 0.f);
   }
   const int hw = lane >> 5, cl = lane & 31;
   const int kk0 = cl * 4, k0 = K * TB + kk0;
@@ -514,10 +535,10 @@ __global__ __launch_bounds__(256) void red_symv_kernel(const RMat* __restrict__ 
   // the row (lda % 4 == 0, lda >= n); out-of-range entries zeroed after
   const int kc = min(k0, (int)lda - 4);
   const AS1 float* gA = gptr(M.A);
-  float4 q[16];
+  float4 q[HT / 8];
 #pragma unroll
-  for (int it = 0; it < 16; ++it) {
-    const int rr = I * TB + wave * 32 + it * 2 + hw;
+  for (int it = 0; it < HT / 8; ++it) {
+    const int rr = rb + wave * (HT / 4) + it * 2 + hw;
     const fx4 t = *(const AS1 fx4*)(gA + (long long)min(rr, n - 1) * lda + kc);
     const bool ok = rr < n;
     q[it] = make_float4((ok && k0 < n) ? t.x : 0.f, (ok && k0 + 1 < n) ? t.y : 0.f,
@@ -529,23 +550,24 @@ __global__ __launch_bounds__(256) void red_symv_kernel(const RMat* __restrict__ 
   float ca[4] = {0.f, 0.f, 0.f, 0.f};
   const float vk0 = sv[1][kk0], vk1 = sv[1][kk0 + 1], vk2 = sv[1][kk0 + 2], vk3 = sv[1][kk0 + 3];
 #pragma unroll
-  for (int it = 0; it < 16; ++it) {
-    const int rr = wave * 32 + it * 2 + hw;
+  for (int it = 0; it < HT / 8; ++it) {
+    const int rl = wave * (HT / 4) + it * 2 + hw;      // row within the half
+    const int rk = hr * HT + rl;                       // row within block I
     float x0 = q[it].x, x1 = q[it].y, x2 = q[it].z, x3 = q[it].w;
-    const float vrr = sv[0][rr];
+    const float vrr = sv[0][rl];
     if (diag) {   // upper triangle only: row sums take k >= r, column sums k > r
-      x0 = (kk0 >= rr) ? x0 : 0.f;
-      x1 = (kk0 + 1 >= rr) ? x1 : 0.f;
-      x2 = (kk0 + 2 >= rr) ? x2 : 0.f;
-      x3 = (kk0 + 3 >= rr) ? x3 : 0.f;
-      ca[0] += (kk0 > rr) ? x0 * vrr : 0.f;
-      ca[1] += (kk0 + 1 > rr) ? x1 * vrr : 0.f;
-      ca[2] += (kk0 + 2 > rr) ? x2 * vrr : 0.f;
-      ca[3] += (kk0 + 3 > rr) ? x3 * vrr : 0.f;
+      x0 = (kk0 >= rk) ? x0 : 0.f;
+      x1 = (kk0 + 1 >= rk) ? x1 : 0.f;
+      x2 = (kk0 + 2 >= rk) ? x2 : 0.f;
+      x3 = (kk0 + 3 >= rk) ? x3 : 0.f;
+      ca[0] += (kk0 > rk) ? x0 * vrr : 0.f;
+      ca[1] += (kk0 + 1 > rk) ? x1 * vrr : 0.f;
+      ca[2] += (kk0 + 2 > rk) ? x2 * vrr : 0.f;
+      ca[3] += (kk0 + 3 > rk) ? x3 * vrr : 0.f;
     } else {
       ca[0] += x0 * vrr; ca[1] += x1 * vrr; ca[2] += x2 * vrr; ca[3] += x3 * vrr;
     }
-    rowred[rr][cl] = x0 * vk0 + x1 * vk1 + x2 * vk2 + x3 * vk3;
+    rowred[rl][cl] = x0 * vk0 + x1 * vk1 + x2 * vk2 + x3 * vk3;
   }
 #pragma unroll
   for (int x = 0; x < 4; ++x) ca[x] += __shfl_xor(ca[x], 32, 64);
@@ -554,20 +576,32 @@ __global__ __launch_bounds__(256) void red_symv_kernel(const RMat* __restrict__ 
     for (int x = 0; x < 4; ++x) colred[wave][kk0 + x] = ca[x];
   }
   kfac_lds_barrier();
+  // P columns: 2T + h, T = the other tile index (see F).  Off-diagonal: row
+  // sums -> column 2K (h = 0), column sums of half hr -> 2I + hr.  Diagonal:
+  // half hr -> column 2I + hr for all 128 rows of block I (column sums, plus
+  // the row sums of its own 64 rows).
   AS1 float* const Pc = gptr(M.P) + cs * M.sP;
   double tp = 0.0;
   if (tid < TB) {
-    float rs = 0.f;
-#pragma unroll 8
-    for (int l = 0; l < 32; ++l) rs += rowred[tid][l];
     const float csum = colred[0][tid] + colred[1][tid] + colred[2][tid] + colred[3][tid];
+    const int rown = tid - hr * HT;                    // this column as a row of the half
+    float rs = 0.f;
+    if (diag ? (rown >= 0 && rown < HT) : tid < HT) {
+      const int rl = diag ? rown : tid;
+#pragma unroll 8
+      for (int l = 0; l < 32; ++l) rs += rowred[rl][l];
+    }
     if (diag) {
-      Pc[K * ld + I * TB + tid] = rs + csum;
-      tp = (double)sv[0][tid] * (double)(rs + csum);
+      const float v = csum + rs;
+      Pc[(2 * I + hr) * ld + I * TB + tid] = v;
+      tp = (double)sv[1][tid] * (double)v;
     } else {
-      Pc[K * ld + I * TB + tid] = rs;
-      Pc[I * ld + K * TB + tid] = csum;
-      tp = (double)sv[0][tid] * (double)rs + (double)sv[1][tid] * (double)csum;
+      Pc[(2 * I + hr) * ld + K * TB + tid] = csum;
+      tp = (double)sv[1][tid] * (double)csum;
+      if (tid < HT) {
+        Pc[(2 * K) * ld + rb + tid] = rs;
+        tp += (double)sv[0][tid] * (double)rs;
+      }
     }
   }
   tp = wave_sum_d(tp);
@@ -598,7 +632,7 @@ void counts(int n, int j, int out[3]) {
   const int ntr = nt - (j + 1) / TB;
   out[0] = (j <= n - 1) ? nf - std::min(((j + 1) / TB) * (TB / FB), j / FB) : 0;
   out[1] = (j % NB == 0 && j > 0 && j <= n - 2) ? h_tri(ntr) : 0;
-  out[2] = (j <= n - 2) ? h_tri(ntr) + ntr : 0;
+  out[2] = (j <= n - 2) ? 2 * h_tri(ntr) + ntr : 0;
 }
 
 int rb_class(int blocks) {
@@ -652,8 +686,8 @@ WsLayout ws_layout(long long n) {
   L.nt = (int)((n + TB - 1) / TB);
   L.ld = L.nt * TB;
   const long long nt = L.nt;
-  L.sP = a16(nt * L.ld);
-  L.sTS = a16(std::max<long long>(h_tri((int)nt), 4));
+  L.sP = a16(2 * nt * L.ld);
+  L.sTS = a16(std::max<long long>(2 * h_tri((int)nt), 4));
   L.sDS = a16(nt * NK);
   L.sX = a16(L.ld);
   long long o = 0;
@@ -737,7 +771,8 @@ RPlan* plan_for(const KfacReduceRecord* recs, int count, bool capture, int* err)
       }
       // F reads the partials of S(j-1): nt - j / TB blocks of the largest matrix
       const int nt0 = (P.n_sorted[0] + TB - 1) / TB;
-      P.rb[j] = rb_class(std::max(1, nt0 - j / TB));
+      static const int rb_min = getenv("KFAC_REDUCE_RB_MIN") ? atoi(getenv("KFAC_REDUCE_RB_MIN")) : 1;
+      P.rb[j] = rb_class(std::max(rb_min, nt0 - j / TB));
       if (P.rb[j] < 0) { *err = -6; return nullptr; }
     }
     if ((*err = (int)hipMalloc(&P.d_offs, sizeof(int) * offs.size())) != 0) return nullptr;

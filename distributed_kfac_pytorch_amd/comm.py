@@ -12,8 +12,21 @@ Differences by design (SURVEY.md section 7.4 defects #6/#7):
     division is carried by each handle (the reference inspected only
     `handles[0]`).
   * `local_rank()` returns an int.
-  * Sub-communicators are cached by rank tuple; every rank must create them
-    in the same order (the execution plan does so once, at build time).
+  * K-FAC traffic has a communicator of its own (`TorchBackend.kfac_world`),
+    created once when the backend is selected: with RCCL and a process group
+    bound to its GPU it is split off the default communicator
+    (`dist.split_group` -> ncclCommSplit), otherwise a plain `new_group`.
+    Its collectives run on that communicator's own HIP stream, so the
+    factor all-reduce and the eigendata / gradient all-gathers never queue
+    behind the data-parallel gradient all-reduce on the default group, and
+    are ordered against the compute stream by events only (SURVEY.md
+    5.8.1; reference: one torch group per layer collective,
+    kfac/comm.py:53-64,194-275).
+  * Sub-communicators (HYBRID_OPT / MEM_OPT inverse and gradient groups) are
+    created per PARTITION of the world (`CommGroup.partition`): one
+    ncclCommSplit of the K-FAC world for the whole partition on RCCL, one
+    `new_group` per member group otherwise; every rank creates them in the
+    same order (the execution plan does so once, at build time).
 
 The bulk K-FAC traffic does not go through these per-tensor calls on the
 fast path: parallel/collectives.py packs factors, eigendata and gradients
@@ -49,6 +62,29 @@ def reset_comm_backend():
     global backend
     backend = None
     CommGroup._cache.clear()
+    CommGroup._partitions.clear()
+
+
+def _can_split():
+    """ncclCommSplit is available: RCCL/NCCL default group bound to a device
+    (init_process_group(device_id=...), parallel/launch.py) and a torch
+    with dist.split_group.  Identical on every rank."""
+    if not (_dist_ready() and hasattr(dist, 'split_group')):
+        return False
+    if dist.get_backend() != 'nccl':
+        return False
+    pg = dist.distributed_c10d._get_default_group()
+    return getattr(pg, 'bound_device_id', None) is not None
+
+
+def _new_world_group():
+    world = dist.get_world_size()
+    if world <= 1:
+        return None
+    ranks = list(range(world))
+    if _can_split():
+        return dist.split_group(split_ranks=[ranks], group_desc='kfac_world')
+    return dist.new_group(ranks)
 
 
 def _dist_ready():
@@ -58,21 +94,55 @@ def _dist_ready():
 class CommGroup(object):
     """A set of ranks plus its communicator.
 
-    `group` is None when the ranks are the whole world (use the default
-    group) or a single rank (collectives are no-ops).
+    `group` is None when the ranks are the whole world (collectives use the
+    K-FAC world communicator) or a single rank (collectives are no-ops).
     """
     _cache = {}
+    _partitions = {}
 
-    def __init__(self, ranks):
+    def __init__(self, ranks, group=None):
         self.ranks = sorted(int(r) for r in ranks)
         key = tuple(self.ranks)
-        self.group = None
-        if _dist_ready():
+        self.group = group
+        if group is None and _dist_ready():
             world = dist.get_world_size()
             if 1 < len(self.ranks) < world:
                 if key not in CommGroup._cache:
                     CommGroup._cache[key] = dist.new_group(self.ranks)
                 self.group = CommGroup._cache[key]
+
+    @classmethod
+    def partition(cls, rank_lists):
+        """CommGroups for a partition of the world (disjoint rank lists
+        covering every rank), created collectively: on RCCL one
+        ncclCommSplit of the K-FAC world for the whole partition (this
+        rank's group is a real communicator, the others are bookkeeping),
+        else one new_group per list.  Cached by the partition."""
+        lists = [sorted(int(r) for r in g) for g in rank_lists]
+        key = tuple(tuple(g) for g in lists)
+        if key in cls._partitions:
+            return cls._partitions[key]
+        if not _dist_ready():
+            out = [cls(g) for g in lists]
+        else:
+            world = dist.get_world_size()
+            cover = sorted(r for g in lists for r in g)
+            if cover != list(range(world)):
+                raise ValueError('not a partition of the world: {}'.format(lists))
+            multi = [g for g in lists if 1 < len(g) < world]
+            if multi and _can_split() and isinstance(backend, TorchBackend) and \
+                    backend.kfac_world is not None:
+                me = dist.get_rank()
+                # split_ranks are ranks of the parent (the K-FAC world spans
+                # every rank in order: parent rank == global rank)
+                mine = dist.split_group(parent_pg=backend.kfac_world, split_ranks=multi,
+                                        group_desc='kfac_sub')
+                out = [cls(g, group=mine if (me in g and 1 < len(g) < world) else None)
+                       for g in lists]
+            else:
+                out = [cls(g) for g in lists]
+        cls._partitions[key] = out
+        return out
 
     @property
     def size(self):
@@ -153,7 +223,15 @@ class CommBackend(object):
 
 
 class TorchBackend(CommBackend):
-    """torch.distributed backend (RCCL over xGMI on MI355X, gloo on CPU)."""
+    """torch.distributed backend (RCCL over xGMI on MI355X, gloo on CPU).
+
+    `kfac_world`: the dedicated K-FAC communicator over all ranks (None at
+    world size 1), created here -- every rank selects the backend at the
+    same program point (KFAC construction / parallel.launch.init_distributed).
+    """
+
+    def __init__(self):
+        self.kfac_world = _new_world_group()
 
     def size(self):
         return dist.get_world_size()
@@ -168,14 +246,15 @@ class TorchBackend(CommBackend):
                                'when using torch.distributed')
         return int(v)
 
-    @staticmethod
-    def _resolve(group):
-        """-> (skip, kwargs, group_size)."""
+    def _resolve(self, group):
+        """-> (skip, kwargs, group_size).  None / a world-sized group -> the
+        K-FAC world communicator."""
+        world_kw = {'group': self.kfac_world} if self.kfac_world is not None else {}
         if group is None:
-            return False, {}, dist.get_world_size()
+            return False, world_kw, dist.get_world_size()
         if group.size <= 1:
             return True, {}, 1
-        kw = {'group': group.group} if group.group is not None else {}
+        kw = {'group': group.group} if group.group is not None else world_kw
         return False, kw, group.size
 
     def allreduce(self, tensor, op=Ops.Average, group=None, async_op=True):
@@ -225,4 +304,7 @@ class TorchBackend(CommBackend):
         return Handle(work) if async_op else None
 
     def barrier(self):
-        dist.barrier()
+        if self.kfac_world is not None:
+            dist.barrier(group=self.kfac_world)
+        else:
+            dist.barrier()

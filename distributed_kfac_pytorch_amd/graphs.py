@@ -28,8 +28,14 @@ Two modes:
                   communicate[i] issues its (async) collective, which runs
                   while segment i+1 replays; the first segment returns the
                   loss.  `update` (preconditioner.step() + optimizer.step())
-                  is a graph only when it issues no collective for that kind
-                  (one rank, or K-FAC COMM_OPT plain steps).  With
+                  is a graph when it issues no collective for that kind: one
+                  rank, or COMM_OPT plain and factor steps -- at a factor step
+                  the K-FAC factor all-reduce is issued eagerly first
+                  (KFAC.step_factor_comm: pack + async RCCL all-reduce on the
+                  K-FAC communicator) and joined at the next factor step,
+                  before its forward/backward graph replays
+                  (KFAC.prepare_factor_step), so the captured update holds no
+                  collective.  With
                   `phased_update=True` (update == preconditioner.step() +
                   optimizer.step()), a plain step that does communicate
                   (MEM_OPT / HYBRID_OPT gradient all-gather) runs as two
@@ -174,7 +180,7 @@ class GraphedTrainStep(object):
         if comm.backend is None or comm.backend.size() == 1:
             return True
         from .preconditioner import CommMethod
-        return kind == 'plain' and pre.comm_method == CommMethod.COMM_OPT
+        return kind in ('plain', 'factor') and pre.comm_method == CommMethod.COMM_OPT
 
     # ------------------------------------------------------------ execution
     def _inverse_fb_graphed(self):
@@ -195,10 +201,23 @@ class GraphedTrainStep(object):
         return all(self._key('fb' if i == 0 else 'fb%d' % i, 'factor') in self.graphs
                    for i in range(len(self.fbs)))
 
+    def _prepare_factor(self):
+        # a factor step's captured hooks run the EMA on the averaged factors:
+        # join the previous factor step's deferred all-reduce first
+        if self.pre is not None and hasattr(self.pre, 'prepare_factor_step'):
+            self.pre.prepare_factor_step()
+
+    def _issue_factor_comm(self, kind):
+        # multi-rank factor step: issue the factor all-reduce eagerly so the
+        # update segment holds no collective (KFAC.step_factor_comm)
+        if kind == 'factor' and self.pre is not None and hasattr(self.pre, 'step_factor_comm'):
+            self.pre.step_factor_comm()
+
     def __call__(self):
         kind = self._kind()
         if self.enabled and kind == 'eager' and self._inverse_fb_graphed():
             self.eager_steps += 1
+            self._prepare_factor()
             loss = None
             for i, (fb, cm) in enumerate(zip(self.fbs, self.comms)):
                 out = self._run_segment('fb' if i == 0 else 'fb%d' % i, 'factor', fb,
@@ -228,6 +247,8 @@ class GraphedTrainStep(object):
                 else:
                     torch.cuda.synchronize()
             return out
+        if kind == 'factor':
+            self._prepare_factor()
         if not self.segmented:
             return self._run_segment('step', kind, self.step_fn, advances=True)
         loss = None
@@ -237,7 +258,8 @@ class GraphedTrainStep(object):
                 loss = out
             if cm is not None:
                 cm()
-        if self.phased_update and kind == 'plain' and self.pre is not None and \
+        self._issue_factor_comm(kind)
+        if self.phased_update and kind in ('plain', 'factor') and self.pre is not None and \
                 (self.phased_update == 'force' or not self._update_capturable(kind)):
             self._run_segment('upd_pre', kind, self.pre.step_precondition, advances=False)
             self.pre.step_communicate()

@@ -35,7 +35,7 @@ SMALL_N = 192
 # batched divide and conquer and the WY back-transformation (no library
 # solver); 'auto' / 'tridiag' / 'syevd': the per-size-class paths of round 1
 LARGE_PATH = os.environ.get('KFAC_EIG_LARGE', 'fused')
-FUSED_MAX_N = 5120   # csrc/eig_reduce.hip NTMAX * TB (larger factors: per-class path)
+FUSED_MAX_N = 16384   # csrc/eig_reduce.hip NMAX (larger factors: per-class path)
 # 'auto': the hand-written path from this n up (it wins from 2048 on, rocSOLVER
 # syevd's latency per column wins below: profiles/r1_tridiag_vs_syevd.log)
 TRIDIAG_MIN_N = int(os.environ.get('KFAC_TRIDIAG_MIN_N', '2048'))

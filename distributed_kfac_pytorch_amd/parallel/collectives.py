@@ -6,8 +6,15 @@ FactorAllreduce   X1+X2: the upper triangles of every
                   about `bucket_cap_mb`, and unpacked with the 1/world
                   averaging folded into the unpack kernel.  Halves the bytes
                   on the wire and turns 2 x #layers NCCL calls into a handful.
-                  Buckets are issued back to back (async) and each bucket is
-                  unpacked as soon as its own handle completes.
+                  Split in two: `start()` packs and issues every bucket
+                  asynchronously on the K-FAC communicator's stream and
+                  returns; `finish()` joins (a device-side stream wait, no
+                  host sync on RCCL) and unpacks.  KFAC calls finish() only
+                  where the averaged factors are consumed -- the next EMA
+                  update, the next inverse update, a state_dict -- so the
+                  all-reduce of a factor step runs under the rest of that
+                  step and the following plain steps (reference: issued and
+                  waited inside step(), kfac/preconditioner.py:525-533).
 broadcast_eigendata  X3/X4: ONE in-place all-gather of the plan's eigen arena
                   (equal per-owner slots) over this rank's inverse group:
                   every owner's region reaches every member in one RCCL call
@@ -44,6 +51,8 @@ class FactorAllreduce(object):
         self._signature = None
         self.arenas = {}    # dtype -> flat tensor
         self.buckets = []   # (dtype, start, end, [entries])
+        self._pending = None    # in-flight buckets: [(handle, dtype, entries)]
+        self.waits = 0          # finish() calls that joined an in-flight all-reduce (tests)
 
     def _current_signature(self):
         sig = []
@@ -87,11 +96,22 @@ class FactorAllreduce(object):
                 self.buckets.append((dtype, start, off, cur))
         self._signature = self._current_signature()
 
+    @property
+    def pending(self):
+        return self._pending is not None
+
     def __call__(self):
+        self.start()
+        self.finish()
+
+    def start(self):
+        """Pack every factor and issue the bucketed SUM all-reduce; returns
+        without waiting.  A previous all-reduce still in flight is joined
+        first (its arena is about to be overwritten)."""
         backend = comm.backend
-        world = backend.size()
-        if world == 1:
+        if backend.size() == 1:
             return
+        self.finish()
         if self._signature != self._current_signature():
             self._build()
         for dtype, arena in self.arenas.items():
@@ -104,6 +124,17 @@ class FactorAllreduce(object):
         for dtype, s, e, entries in self.buckets:
             h = backend.allreduce(self.arenas[dtype][s:e], op=comm.Ops.Sum)
             pending.append((h, dtype, entries))
+        self._pending = pending
+
+    def finish(self):
+        """Join the in-flight all-reduce and write the averaged factors back
+        (1/world folded into the unpack).  No-op when nothing is in flight."""
+        pending, self._pending = self._pending, None
+        if pending is None:
+            return
+        backend = comm.backend
+        world = backend.size()
+        self.waits += 1
         for h, dtype, entries in pending:
             backend.wait(h)
             arena = self.arenas[dtype]

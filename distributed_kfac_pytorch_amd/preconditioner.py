@@ -154,7 +154,7 @@ class KFAC(optim.Optimizer):
                  bucket_cap_mb=64.0, symmetry_aware_comm=True, eigen_solver='auto',
                  profile=False, use_hip_graphs=True, precond_precision='fp32',
                  fused_precondition=True, inverse_lag=0, comm_check=False,
-                 overlap_precondition=False):
+                 overlap_precondition=False, defer_factor_comm=True):
         if not 0.0 <= lr:
             raise ValueError('Invalid learning rate: {}'.format(lr))
         if not 0.0 < factor_decay <= 1:
@@ -228,6 +228,11 @@ class KFAC(optim.Optimizer):
         # leave identical on every rank (utils/comm_check.py)
         self.comm_check = bool(comm_check) or \
             bool(int(__import__('os').environ.get('KFAC_COMM_CHECK', '0')))
+        # the factor all-reduce of a factor step is issued asynchronously and
+        # joined where the averaged factors are consumed (next EMA / inverse
+        # update / state_dict): parallel/collectives.FactorAllreduce
+        self.defer_factor_comm = bool(defer_factor_comm)
+        self._factor_comm_step = None   # step whose factor comm step_factor_comm() issued
         self.workers_assigned = False
         self.plan = None
         self.plan_generation = 0
@@ -327,6 +332,7 @@ class KFAC(optim.Optimizer):
     # ------------------------------------------------------------ state dict
     def state_dict(self, include_layer_factors=True, include_layer_inverses=False):
         self.wait_inverses()
+        self.join_factor_comm()
         sd = super(KFAC, self).state_dict()
         layers = None
         if include_layer_factors:
@@ -339,6 +345,7 @@ class KFAC(optim.Optimizer):
         return sd
 
     def load_state_dict(self, state_dict, compute_inverses=True):
+        self.join_factor_comm()    # an in-flight all-reduce would overwrite the loaded factors
         if state_dict.get('layers') is not None:
             if len(state_dict['layers']) != len(self.layers):
                 raise ValueError('loaded state dict contains a different number of layers')
@@ -444,6 +451,7 @@ class KFAC(optim.Optimizer):
         else:
             layer.save_inputs(input)
             if self.compute_factor_in_hook:
+                self.join_factor_comm()     # the EMA reads the averaged factors
                 with self._no_autocast(input[0]):
                     layer.update_A_factor(alpha=alpha)
         if isinstance(output, torch.Tensor) and output.requires_grad:
@@ -458,6 +466,7 @@ class KFAC(optim.Optimizer):
             return
         layer.save_grad_outputs((grad,))
         if self.compute_factor_in_hook:
+            self.join_factor_comm()
             with self._no_autocast(grad):
                 layer.update_G_factor(alpha=self.param_groups[0]['factor_decay'])
 
@@ -506,14 +515,15 @@ class KFAC(optim.Optimizer):
                 loss = closure()
         p = self.param_groups[0]
         t = self.timer
-        if p['step'] % p['factor_update_freq'] == 0:
+        if p['step'] % p['factor_update_freq'] == 0 and self._factor_comm_step != p['step']:
             if not self.compute_factor_in_hook:
                 with t('factors'):
                     self.compute_factors(alpha=p['factor_decay'])
             with t('factor_comm'):
                 self.allreduce_factors()
-            if self.comm_check:
-                self._check_comm('factor all-reduce', ('A', 'G'))
+        if self.comm_check and p['step'] % p['factor_update_freq'] == 0:
+            self.join_factor_comm()
+            self._check_comm('factor all-reduce', ('A', 'G'))
         if not self.workers_assigned:
             self._assign_workers()
             self.workers_assigned = True
@@ -558,10 +568,40 @@ class KFAC(optim.Optimizer):
     # all-gather eagerly between them, so those steps are no longer eager.
     # step() == step_precondition(); step_communicate(); step_finish().
     def is_plain_step(self):
+        """No inverse update this step, and no factor collective left to
+        issue (a plain step, or a factor step whose all-reduce
+        step_factor_comm() has issued): the rest of step() is capturable."""
         p = self.param_groups[0]
         return (self.workers_assigned and self._pending_inv is None
-                and p['step'] % p['factor_update_freq'] != 0
+                and (p['step'] % p['factor_update_freq'] != 0 or
+                     self._factor_comm_step == p['step'])
                 and p['step'] % p['inv_update_freq'] != 0)
+
+    @torch.no_grad()
+    def step_factor_comm(self):
+        """Factor step (not an inverse step), graphed training loops: compute
+        the factors unless the hooks did, and issue their all-reduce now,
+        eagerly; the rest of this step's step() then issues no collective and
+        is captured / replayed (graphs.GraphedTrainStep).  Joined at the
+        next consumer like any deferred factor all-reduce."""
+        p = self.param_groups[0]
+        if p['step'] % p['factor_update_freq'] != 0 or p['step'] % p['inv_update_freq'] == 0:
+            return
+        if not self.compute_factor_in_hook:
+            self.compute_factors(alpha=p['factor_decay'])
+        self.allreduce_factors()
+        self._factor_comm_step = p['step']
+
+    def join_factor_comm(self):
+        """Join a deferred factor all-reduce (device-side wait + unpack of
+        the averaged factors); no-op when none is in flight."""
+        if self._factor_allreduce.pending:
+            self._factor_allreduce.finish()
+
+    def prepare_factor_step(self):
+        """Before a factor step's forward/backward replays (its captured
+        hooks run the EMA on the factors): join the previous all-reduce."""
+        self.join_factor_comm()
 
     @torch.no_grad()
     def step_precondition(self):
@@ -676,9 +716,13 @@ class KFAC(optim.Optimizer):
         comm_check.assert_consistent(named, phase)
 
     def allreduce_factors(self):
+        """Issue the bucketed factor all-reduce; with defer_factor_comm it is
+        joined at the averaged factors' next consumer (join_factor_comm)."""
         if comm.backend.size() == 1:
             return
-        self._factor_allreduce()
+        self._factor_allreduce.start()
+        if not self.defer_factor_comm:
+            self._factor_allreduce.finish()
 
     def broadcast_inverses(self):
         if comm.backend.size() == 1:
@@ -736,6 +780,7 @@ class KFAC(optim.Optimizer):
     def compute_inverses(self, damping=0.001):
         """Eigendecompose / invert every factor this rank owns, in one batch."""
         self._drop_lagged_inverses()
+        self.join_factor_comm()
         jobs = self._inverse_jobs()
         self._have_inverses = True
         if not jobs:
@@ -770,6 +815,7 @@ class KFAC(optim.Optimizer):
         return self._pending_inv is not None
 
     def _launch_lagged_inverses(self, damping):
+        self.join_factor_comm()
         jobs = self._inverse_jobs()
         pend = dict(jobs=jobs, damping=damping, results=None, future=None, event=None,
                     apply_at=self.param_groups[0]['step'] + self.inverse_lag)
@@ -856,6 +902,7 @@ class KFAC(optim.Optimizer):
         """Update every layer's A and G.  On the GPU all factors of the step go
         through a handful of grouped SYRK + EMA launches (ops/factors.py
         update_factors_grouped) instead of ~3 launches per factor."""
+        self.join_factor_comm()     # the EMA reads the averaged factors
         if self.layers and self.layers[0].module.weight.is_cuda and self.grouped_factors:
             items, refs = [], []
             for layer in self.layers:

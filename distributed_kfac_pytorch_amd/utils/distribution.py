@@ -73,13 +73,17 @@ class WorkerAllocator(object):
         self.grad_workers = grad_workers
         self.bcast_grad_ranks = partition_grad_ranks(size, grad_workers)
         self.bcast_inv_ranks = partition_inv_ranks(size, grad_workers)
+        # creation order is identical on every rank: inverse groups, then
+        # gradient groups (each sub-communicator is a collective call); the
+        # default factory builds each partition at once (one ncclCommSplit
+        # on RCCL, comm.CommGroup.partition)
         if group_factory is None:
             from .. import comm
-            group_factory = comm.CommGroup
-        # creation order is identical on every rank: inverse groups, then
-        # gradient groups (each sub-communicator is a collective call)
-        self.bcast_inv_groups = [group_factory(r) for r in self.bcast_inv_ranks]
-        self.bcast_grad_groups = [group_factory(r) for r in self.bcast_grad_ranks]
+            self.bcast_inv_groups = comm.CommGroup.partition(self.bcast_inv_ranks)
+            self.bcast_grad_groups = comm.CommGroup.partition(self.bcast_grad_ranks)
+        else:
+            self.bcast_inv_groups = [group_factory(r) for r in self.bcast_inv_ranks]
+            self.bcast_grad_groups = [group_factory(r) for r in self.bcast_grad_ranks]
         self._inv_index = {r: i for i, g in enumerate(self.bcast_inv_ranks) for r in g}
         self._grad_index = {r: i for i, g in enumerate(self.bcast_grad_ranks) for r in g}
 

@@ -75,6 +75,41 @@ def kfac_strategy(rank, world, port, out_dir, cfg):
     dist.destroy_process_group()
 
 
+def deferred_factor_comm(rank, world, port, out_dir, cfg):
+    """Different data per rank.  The factor all-reduce of a factor-only step
+    must stay in flight after step() returns (no wait inside step()), be
+    joined by the next consumer, and leave factors bit-identical to the
+    joined-inside-step() schedule."""
+    _init(rank, world, port)
+    import distributed_kfac_pytorch_amd as kfac
+    from tests._oracle_common import build_case
+    out = {}
+    for defer in (True, False):
+        model, data = build_case({'seed': 0, 'batch': 6, 'steps': 6})
+        pre = kfac.KFAC(model, factor_update_freq=2, inv_update_freq=4, lr=0.05,
+                        damping=0.003, defer_factor_comm=defer)
+        fa = pre._factor_allreduce
+        opt = torch.optim.SGD(model.parameters(), lr=0.05)
+        g = torch.Generator().manual_seed(100 + rank)
+        record = []
+        for i in range(6):
+            x, y = data[i]
+            x = x + 0.1 * torch.randn(x.shape, generator=g)     # rank-specific data
+            opt.zero_grad()
+            torch.nn.functional.cross_entropy(model(x), y).backward()
+            w0 = fa.waits
+            pre.step()
+            record.append((i, fa.pending, fa.waits - w0))
+            opt.step()
+        sd = pre.state_dict()
+        out[defer] = {'record': record,
+                      'factors': [(l['A'].clone(), l['G'].clone()) for l in sd['layers']],
+                      'params': [p.detach().clone() for p in model.parameters()]}
+    torch.save(out, os.path.join(out_dir, 'rank{}.pt'.format(rank)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def grad_allreduce(rank, world, port, out_dir, cfg):
     """Different data per rank; GradientAllreduce must average gradients and
     start every rank from rank 0's parameters."""

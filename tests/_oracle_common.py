@@ -42,5 +42,7 @@ def run_steps(model, pre, data, steps, lr=0.05):
         pre.step()
         grads.append([p.grad.detach().clone() for p in model.parameters()])
         opt.step()
+    if hasattr(pre, 'join_factor_comm'):
+        pre.join_factor_comm()    # a deferred factor all-reduce may still be in flight
     factors = [(l.state['A'].clone(), l.state['G'].clone()) for l in pre.layers]
     return grads, factors

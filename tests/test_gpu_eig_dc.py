@@ -94,6 +94,24 @@ def test_large_factor_eigensolver_resnet50_sizes(n, b):
         assert res <= 2e-5 and orth <= 1e-4 and lam <= 1e-5, (n, res, orth, lam)
 
 
+@pytest.mark.parametrize('n', [8192, 10000])
+def test_fused_path_beyond_5120(n):
+    """The hand-written reduction takes any factor up to 16384 (round 2's
+    stopped at 5120 and handed larger ones to rocSOLVER): a Transformer LM's
+    10k-vocabulary head factor."""
+    A64 = _kfac_factor(n, 90)
+    (Q, d), = eigen.symeig_many([A64.float()])
+    torch.cuda.synchronize()
+    eigen.check_solver_status()
+    Q64, d64 = Q.double(), d.double()
+    ref = torch.linalg.eigvalsh(A64)
+    an = ref.abs().max().item()
+    res = ((A64 @ Q64 - Q64 * d64).norm() / (an * n ** 0.5)).item()
+    orth = (Q64.t() @ Q64 - torch.eye(n, device=DEV, dtype=torch.float64)).abs().max().item()
+    lam = ((d64 - ref.clamp(min=0)).abs().max() / an).item()
+    assert res <= 2e-5 and orth <= 1e-4 and lam <= 1e-5, (n, res, orth, lam)
+
+
 def test_fused_ragged_large_path():
     """The default large-factor path: every size in ONE fused reduction (one
     launch per column for the ragged batch), one batched D&C, WY back-transform."""
