@@ -145,13 +145,16 @@ __device__ __forceinline__ void store_tile(const PatchArgs& p, const f32x16_t (&
 
 // ws[row][col] (upper triangle, row <= col < ncols) = sum over the job's
 // contributions c (in order) and their splits s (in order) of
-// part_c[s][tile][local]: one workgroup per (job, tile pair).
+// part_c[s][tile][local]: one workgroup per (job, tile pair).  accum = 1 adds
+// the sum to ws instead (a factor with more than MAX_CONTRIB sources, e.g. an
+// LSTM's per-time-step Linears, is reduced in fixed-order chained launches of
+// MAX_CONTRIB contributions: still bitwise reproducible).
 constexpr int MAX_CONTRIB = 8;
 struct RedJob {
   float* ws; int ldw, ncols, ntiles, ncontrib;
   const float* part[MAX_CONTRIB];
   int splits[MAX_CONTRIB];
-  int block_begin, pad;
+  int block_begin, accum;
 };
 constexpr int MAX_RED_JOBS = 24;
 struct RedBatch {
@@ -200,9 +203,10 @@ __global__ __launch_bounds__(256) void tile_reduce_kernel(const RedBatch* __rest
   }
   const int row = ti * BT + e / BT, col0 = tj * BT + (e & (BT - 1));
   AS1 float* w = gptr(J.ws) + (long long)row * J.ldw + col0;
+  const bool add = J.accum != 0;
 #pragma unroll
   for (int u = 0; u < 4; ++u)
-    if (row <= col0 + u && col0 + u < J.ncols) w[u] = acc[u];
+    if (row <= col0 + u && col0 + u < J.ncols) w[u] = add ? w[u] + acc[u] : acc[u];
 }
 
 // LANE_COLS = true when channels are the unit-stride dim (NHWC / Linear):

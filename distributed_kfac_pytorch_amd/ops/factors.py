@@ -88,18 +88,25 @@ class RedJob(ctypes.Structure):
     _fields_ = [('ws', ctypes.c_void_p), ('ldw', ctypes.c_int), ('ncols', ctypes.c_int),
                 ('ntiles', ctypes.c_int), ('ncontrib', ctypes.c_int),
                 ('part', ctypes.c_void_p * 8), ('splits', ctypes.c_int * 8),
-                ('block_begin', ctypes.c_int), ('pad', ctypes.c_int)]
+                ('block_begin', ctypes.c_int), ('accum', ctypes.c_int)]
 
 
-def _red_job(ws_ptr, ldw, n, contribs):
-    """contribs: [(part pointer, splits)] in the fixed summation order."""
-    J = RedJob()
-    J.ws, J.ldw, J.ncols, J.ntiles = ws_ptr, ldw, n, (n + TILE - 1) // TILE
-    J.ncontrib = len(contribs)
-    for c, (ptr, sp) in enumerate(contribs):
-        J.part[c] = ptr
-        J.splits[c] = sp
-    return J
+def _red_jobs(ws_ptr, ldw, n, contribs):
+    """contribs: [(part pointer, splits)] in the fixed summation order ->
+    one RedJob per chunk of MAX_CONTRIB contributions: chunk 0 stores, the
+    later chunks add (launched in order by _tile_reduce: deterministic)."""
+    jobs = []
+    for c0 in range(0, max(len(contribs), 1), MAX_CONTRIB):
+        J = RedJob()
+        J.ws, J.ldw, J.ncols, J.ntiles = ws_ptr, ldw, n, (n + TILE - 1) // TILE
+        chunk = contribs[c0:c0 + MAX_CONTRIB]
+        J.ncontrib = len(chunk)
+        J.accum = int(c0 > 0)
+        for c, (ptr, sp) in enumerate(chunk):
+            J.part[c] = ptr
+            J.splits[c] = sp
+        jobs.append(J)
+    return jobs
 
 
 def _check_red_layout():
@@ -114,20 +121,17 @@ def accumulate_sources(sources, ws, allow_vec=True):
     """ws (n x n f32) = sum_s scale_s * P_s^T P_s  (upper triangle only).
 
     Deterministic: every (source, row split, tile pair) of the SYRK stores its
-    partial tile and ONE tile_reduce launch adds them in a fixed order
-    (source, split) -- bitwise-reproducible factors, no f32 atomics (the
-    atomic form, into a zeroed ws, is the fallback past MAX_CONTRIB sources).
+    partial tile and tile_reduce adds them in a fixed order (source, split)
+    -- one launch per MAX_CONTRIB sources, chained -- bitwise-reproducible
+    factors for any number of sources, no f32 atomics.
     Returns None when ws is in the reference column order (c, kh, kw), or
     (kcols, C, kh*kw) when the channels-contiguous fast path filled it in the
     internal order (kh, kw, c) -- `kfac_factor_ema_perm` maps it back."""
     L = _lib.lib()
     stream = _lib.stream(ws.device)
     n = ws.shape[0]
-    det = len(sources) <= MAX_CONTRIB
-    if det:
-        _check_red_layout()
-    else:
-        ws.zero_()
+    det = True
+    _check_red_layout()
     vec = allow_vec and all(_vec_eligible(s) for s in sources)
     parts, contribs = [], []
     if det:
@@ -165,8 +169,7 @@ def accumulate_sources(sources, ws, allow_vec=True):
             if order is not None and order != o:
                 raise ValueError('factor sources disagree on the patch geometry')
             order = o
-        if det:
-            _tile_reduce([_red_job(ws.data_ptr(), ws.stride(0), n, contribs)], stream)
+        _tile_reduce([_red_jobs(ws.data_ptr(), ws.stride(0), n, contribs)], stream)
         return None if order[2] == 1 else order
     for s, part in zip(sources, parts):
         x = s.x
@@ -183,17 +186,21 @@ def accumulate_sources(sources, ws, allow_vec=True):
             _lib.DTYPE_CODE[x.dtype], _lib.ptr(x), sb, sc, sh, sw, B, C, H, W,
             g.kh, g.kw, g.sh, g.sw, g.ph, g.pw, g.dh, g.dw, int(s.has_bias), s.scale,
             _lib.ptr(ws), ws.stride(0), 0, part, _dptr(s.dscale), stream), 'kfac_syrk_patch')
-    if det:
-        _tile_reduce([_red_job(ws.data_ptr(), ws.stride(0), n, contribs)], stream)
+    _tile_reduce([_red_jobs(ws.data_ptr(), ws.stride(0), n, contribs)], stream)
     return None
 
 
-MAX_CONTRIB = 8    # csrc/factors.hip: sources per deterministic tile reduction
+MAX_CONTRIB = 8    # csrc/factors.hip: sources per tile-reduction job
 
 
-def _tile_reduce(jobs, stream):
-    arr = (RedJob * len(jobs))(*jobs)
-    _lib.check(_lib.lib().kfac_tile_reduce(arr, len(jobs), stream), 'kfac_tile_reduce')
+def _tile_reduce(job_chains, stream):
+    """job_chains: per factor, its chunk jobs (_red_jobs).  Level l launches
+    chunk l of every factor that has one, in order."""
+    depth = max(len(c) for c in job_chains)
+    for lvl in range(depth):
+        jobs = [c[lvl] for c in job_chains if len(c) > lvl]
+        arr = (RedJob * len(jobs))(*jobs)
+        _lib.check(_lib.lib().kfac_tile_reduce(arr, len(jobs), stream), 'kfac_tile_reduce')
 
 
 def _dptr(t):
@@ -281,7 +288,6 @@ def update_factors_grouped(items, alpha):
     items = [tuple(it) + (None,) * (4 - len(it)) for it in items]
     for k, (state, sources, out_dtype, _) in enumerate(items):
         if alpha != 1 and all(_vec_eligible(s) for s in sources) and \
-                len(sources) <= MAX_CONTRIB and \
                 len({(s.x.dtype, s.x.shape[1], s.geom.kh * s.geom.kw) for s in sources}) == 1:
             grouped.append(k)
         else:
@@ -341,8 +347,8 @@ def update_factors_grouped(items, alpha):
             poff += nb * TILE * TILE
         _lib.check(L.kfac_syrk_grouped(raw, len(probs), _lib.DTYPE_CODE[dtype], stream),
                    'kfac_syrk_grouped')
-    _tile_reduce([_red_job(arena.data_ptr() + 4 * ws_of[k][0], ws_of[k][1], ws_of[k][1],
-                           contribs[k]) for k in grouped], stream)
+    _tile_reduce([_red_jobs(arena.data_ptr() + 4 * ws_of[k][0], ws_of[k][1], ws_of[k][1],
+                            contribs[k]) for k in grouped], stream)
     jobs = (EmaJob * len(grouped))()
     a1, a2 = alpha / (1.0 - alpha), 1.0 - alpha
     for j, k in enumerate(grouped):

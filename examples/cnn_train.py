@@ -34,7 +34,8 @@ def run(args, dataset):
     args.verbose = args.verbose and rank == 0
     torch.manual_seed(args.seed)
     if args.cuda:
-        torch.backends.cudnn.benchmark = True
+        torch.backends.cudnn.benchmark = not getattr(args, 'deterministic', False)
+        torch.backends.cudnn.deterministic = bool(getattr(args, 'deterministic', False))
 
     if dataset == 'cifar':
         (train_sampler, train_loader), (_, val_loader) = datasets.get_cifar(args)
@@ -50,7 +51,16 @@ def run(args, dataset):
         model = model.to(memory_format=torch.channels_last)
     if args.verbose:
         print(model)
-    model = launch.wrap_ddp(model, device)
+    # --graphs: the bench's fast path (no eager DDP: a flat-arena all-reduce
+    # between graph replays); otherwise the reference's eager DDP loop
+    args.graphed = bool(getattr(args, 'graphs', 0)) and args.batches_per_allreduce == 1 and \
+        not args.fp16
+    grad_sync = None
+    if args.graphed and args.world_size > 1:
+        from distributed_kfac_pytorch_amd.parallel import grad_sync as grad_sync_mod
+        grad_sync = grad_sync_mod.GradientAllreduce(model)
+    elif not args.graphed:
+        model = launch.wrap_ddp(model, device)
 
     # LR scales with the number of workers and micro-batches (reference)
     args.base_lr = args.base_lr * args.world_size * args.batches_per_allreduce
@@ -69,11 +79,15 @@ def run(args, dataset):
         if args.verbose:
             print('resumed from epoch', resume)
 
+    trainer = engine.GraphedTrainer(model, optimizer, preconditioner, loss_func, args,
+                                    grad_sync) if args.graphed else None
     history = []
     start = time.time()
     for epoch in range(resume, args.epochs):
         tr = engine.train(epoch, model, optimizer, preconditioner, loss_func, train_sampler,
-                          train_loader, args)
+                          train_loader, args, trainer=trainer)
+        if trainer is not None:
+            trainer.sync_buffers()
         va = engine.test(epoch, model, loss_func, val_loader, args)
         for s in lr_schedules:
             s.step()

@@ -52,7 +52,19 @@ def base_parser(desc, d):
     p.add_argument('--kfac-comm-method', default='comm-opt',
                    choices=['comm-opt', 'mem-opt', 'hybrid-opt'])
     p.add_argument('--kfac-grad-worker-fraction', type=float, default=0.25)
-    p.add_argument('--precond-precision', default='fp32', choices=['fp32', 'bf16x3'])
+    p.add_argument('--precond-precision', default='fp32', choices=['fp32', 'bf16x3', 'bf16x6'],
+                   help='fused preconditioning GEMMs: fp32 (exact-f32 MFMA), bf16x6 (three bf16 '
+                        'planes, fp32-level error at the bf16 MFMA rate; the bench default) or '
+                        'bf16x3 (~1e-5 relative error)')
+    p.add_argument('--graphs', type=int, default=0,
+                   help='MI355X fast path (1): the whole training step replayed as hipGraphs '
+                        '(graphs.GraphedTrainStep), the data-parallel gradient all-reduce as one '
+                        'flat-arena RCCL call between graph replays (parallel/grad_sync.py) '
+                        'instead of eager DDP, K-FAC factors computed inside the captured hooks; '
+                        'needs --batches-per-allreduce 1 and no --fp16 (falls back to eager '
+                        'otherwise)')
+    p.add_argument('--deterministic', action='store_true',
+                   help='deterministic MIOpen algorithms (cudnn.deterministic, no autotuning)')
     p.add_argument('--backend', default=None, help='torch.distributed backend (nccl = RCCL)')
     p.add_argument('--local_rank', '--local-rank', type=int, default=None)
     return p

@@ -5,6 +5,15 @@ under `model.no_sync()` (DDP), optional mixed precision (bf16 autocast on the
 GPU; fp16 + GradScaler when `--fp16`), then `preconditioner.step()` between
 the gradient all-reduce and `optimizer.step()`.  Metrics stay on the device
 (examples/utils.Metric) and are reduced once per epoch.
+
+`--graphs 1` (GraphedTrainer): the MI355X fast path of bench.py in the
+examples -- each batch is copied into static input buffers and the step
+replays as hipGraphs (graphs.GraphedTrainStep: forward, backward, K-FAC
+factor SYRKs in the captured hooks, the fused preconditioning chain, SGD);
+at world size > 1 the gradient all-reduce is one flat-arena RCCL call between
+the forward/backward graph and the update graph (parallel/grad_sync.py), the
+K-FAC factor all-reduce is issued eagerly and joined at the next factor step.
+A batch of another shape (the last, ragged one) runs the same step eagerly.
 """
 import contextlib
 import time
@@ -13,7 +22,7 @@ import torch
 
 from examples.utils import Metric, accuracy
 
-__all__ = ['train', 'test']
+__all__ = ['train', 'test', 'GraphedTrainer']
 
 try:
     from tqdm import tqdm
@@ -31,8 +40,82 @@ def _autocast(args):
     return contextlib.nullcontext()
 
 
+class GraphedTrainer(object):
+    """One training step over static input buffers, replayed as hipGraphs."""
+
+    def __init__(self, model, optimizer, preconditioner, loss_func, args, grad_sync=None):
+        from distributed_kfac_pytorch_amd import graphs
+        self.model, self.optimizer, self.pre = model, optimizer, preconditioner
+        self.loss_func, self.args, self.grad_sync = loss_func, args, grad_sync
+        self.x = self.y = None
+        if grad_sync is not None:
+            self.step = graphs.GraphedTrainStep(None, preconditioner, [optimizer],
+                                                enabled=args.cuda,
+                                                forward_backward=self._forward_backward,
+                                                communicate=grad_sync, update=self._update,
+                                                phased_update=True)
+        else:
+            self.step = graphs.GraphedTrainStep(self._train_step, preconditioner, [optimizer],
+                                                enabled=args.cuda)
+
+    def _forward_backward(self):
+        if self.grad_sync is not None:
+            self.grad_sync.zero_grad()
+        else:
+            self.optimizer.zero_grad(set_to_none=False)
+        with _autocast(self.args):
+            out = self.model(self.x)
+            loss = self.loss_func(out, self.y)
+        loss.backward()
+        return loss.detach(), out.detach()
+
+    def _update(self):
+        if self.pre is not None:
+            self.pre.step()
+        self.optimizer.step()
+
+    def _train_step(self):
+        res = self._forward_backward()
+        self._update()
+        return res
+
+    def _eager(self, data, target):
+        x, y = self.x, self.y
+        self.x, self.y = data, target
+        try:
+            loss, out = self._forward_backward()
+            if self.grad_sync is not None:
+                self.grad_sync()
+            self._update()
+        finally:
+            self.x, self.y = x, y
+        return loss, out
+
+    def sync_buffers(self):
+        """Rank 0's BatchNorm running statistics to every rank before an
+        evaluation: what the reference's DDP(broadcast_buffers=True) leaves
+        on every rank at eval time (the graphed loop has no DDP wrapper)."""
+        import torch.distributed as dist
+        if self.grad_sync is None or not dist.is_initialized():
+            return
+        for b in self.model.buffers():
+            if b.is_floating_point() or b.dtype in (torch.int64, torch.int32):
+                dist.broadcast(b.data, src=0)
+
+    def __call__(self, data, target):
+        if self.x is None:
+            self.x, self.y = data.clone(), target.clone()
+        elif data.shape != self.x.shape or data.stride() != self.x.stride() or \
+                target.shape != self.y.shape:
+            return self._eager(data, target)
+        else:
+            self.x.copy_(data)
+            self.y.copy_(target)
+        return self.step()
+
+
 def train(epoch, model, optimizer, preconditioner, loss_func, train_sampler, train_loader, args,
-          log_writer=None):
+          log_writer=None, trainer=None):
     model.train()
     train_sampler.set_epoch(epoch)
     train_loss, train_acc = Metric('train_loss'), Metric('train_accuracy')
@@ -47,6 +130,13 @@ def train(epoch, model, optimizer, preconditioner, loss_func, train_sampler, tra
             data, target = data.cuda(non_blocking=True), target.cuda(non_blocking=True)
             if getattr(args, 'channels_last', False):
                 data = data.contiguous(memory_format=torch.channels_last)
+        if trainer is not None:
+            loss, out = trainer(data, target)
+            train_loss.update(loss)
+            train_acc.update(accuracy(out, target))
+            if bar is not None:
+                bar.update(1)
+            continue
         optimizer.zero_grad(set_to_none=False)
         starts = list(range(0, len(data), args.batch_size))
         for i in starts:

@@ -41,6 +41,10 @@ def get_optimizer(model, args, batch_first=True):
             skip_layers=args.skip_layers,
             use_eigen_decomp=not args.use_inv_kfac,
             precond_precision=getattr(args, 'precond_precision', 'fp32'),
+            # graphed multi-rank loop: a replayed forward/backward runs no Python
+            # hooks, so the factors are computed inside the captured hooks
+            compute_factor_in_hook=bool(getattr(args, 'graphed', False)) and
+            getattr(args, 'world_size', 1) > 1,
             verbose=getattr(args, 'verbose', False))
         kfac_scheduler = kfac.KFACParamScheduler(
             preconditioner,

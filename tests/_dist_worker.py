@@ -219,3 +219,23 @@ def split_backward(rank, world, port, out_dir, cfg):
                os.path.join(out_dir, 'rank{}.pt'.format(rank)))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def example_graphs(rank, world, port, out_dir, cfg):
+    """The ImageNet example at world 2 (gloo), --graphs 1 (flat-arena gradient
+    all-reduce between step segments, factors in hooks, deferred factor
+    all-reduce) vs the reference-style eager DDP loop (--graphs 0)."""
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    os.environ['RANK'] = str(rank)
+    os.environ['WORLD_SIZE'] = str(world)
+    os.environ['LOCAL_RANK'] = str(rank)
+    torch.set_num_threads(1)
+    from examples import torch_imagenet_resnet as ex
+    argv = ['--model', 'resnet_tiny', '--synthetic-size', '16', '--batch-size', '2',
+            '--val-batch-size', '4', '--image-size', '32', '--checkpoint-freq', '0',
+            '--epochs', '1', '--kfac-update-freq', '4', '--kfac-cov-update-freq', '2',
+            '--log-dir', os.path.join(out_dir, 'log{}'.format(rank)),
+            '--graphs', str(cfg['graphs'])]
+    hist = ex.main(argv)
+    torch.save(hist, os.path.join(out_dir, 'rank{}_g{}.pt'.format(rank, cfg['graphs'])))

@@ -206,3 +206,15 @@ def test_deferred_factor_allreduce(tmp_path):
             assert torch.equal(p1, p2)
     for (a0, g0), (a1, g1) in zip(outs[0][True]['factors'], outs[1][True]['factors']):
         assert torch.equal(a0, a1) and torch.equal(g0, g1)
+
+
+def test_example_graphs_path_world2(tmp_path):
+    """Verdict r2 item 7: the examples' fast path (--graphs 1) at world 2 on
+    gloo trains like the eager DDP loop (same losses to fp32 rounding)."""
+    for g in (1, 0):
+        _spawn(_dist_worker.example_graphs, 2, tmp_path, {'graphs': g})
+    h1 = torch.load(os.path.join(str(tmp_path), 'rank0_g1.pt'), weights_only=False)
+    h0 = torch.load(os.path.join(str(tmp_path), 'rank0_g0.pt'), weights_only=False)
+    a, b = h1[0]['train'], h0[0]['train']
+    assert abs(a['loss'] - b['loss']) <= 1e-5 * max(1.0, abs(b['loss'])), (a, b)
+    assert abs(h1[0]['val']['loss'] - h0[0]['val']['loss']) <= 1e-4, (h1, h0)

@@ -21,7 +21,7 @@ def test_cifar_example_train_resume(tmp_path, capsys):
 
 
 @pytest.mark.parametrize('extra', [[], ['--use-inv-kfac', '--batches-per-allreduce', '2'],
-                                   ['--kfac-update-freq', '0']])
+                                   ['--kfac-update-freq', '0'], ['--graphs', '1']])
 def test_imagenet_example_variants(tmp_path, extra):
     from examples import torch_imagenet_resnet as ex
     argv = ['--model', 'resnet_tiny', '--synthetic-size', '8', '--batch-size', '2',

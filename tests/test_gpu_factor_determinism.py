@@ -70,3 +70,69 @@ def test_multi_source_factor_reproducible():
     assert torch.equal(a, b)
     ref = sum(_ref_cov(x, 3, 1, 1, False) for x in xs) / 3
     assert ((a.double() - ref).norm() / ref.norm()).item() < 2e-3
+
+
+def test_many_sources_grouped_bitwise():
+    """More sources than one tile-reduction job holds (an LSTM at bptt 35
+    with accumulate_data: one Linear source per time step): the grouped path
+    chains fixed-order reductions, so the factor is bitwise reproducible and
+    equals the fp64 sum."""
+    g = torch.Generator(device='cuda').manual_seed(8)
+    T, B, D = 35, 20, 256
+    xs = [torch.randn(B, D, device='cuda', generator=g).to(torch.bfloat16) for _ in range(T)]
+    srcs = [factors.linear_source(x, True) for x in xs]
+    for s in srcs:
+        s.scale = 1.0 / (B * T)
+    n = D + 1
+    outs = []
+    for _ in range(3):
+        st = torch.zeros(n, n, device='cuda')
+        st = factors.update_factors_grouped([(st, srcs, torch.float32)], 0.0)[0]
+        outs.append(st.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    P = torch.cat([torch.cat([x.double(), torch.ones(B, 1, dtype=torch.float64, device='cuda')], 1)
+                   for x in xs], 0)
+    ref = P.t() @ P / (B * T)
+    err = ((outs[0].double() - ref).norm() / ref.norm()).item()
+    assert err < 1e-5, err
+
+
+def test_lstm_lm_factors_bitwise():
+    """The LSTM LM (bptt 35, accumulate_data=True, bf16 autocast): two
+    identical K-FAC factor steps give bitwise-equal factors for every layer
+    (round 2 fell back to f32-atomic SYRKs past 8 sources).  The 16-bit
+    sources (the gate Linears' inputs x_t and every grad output) go through
+    the grouped path; the hidden-state inputs h_t stay fp32 under autocast
+    (c_t is fp32, h_t = o_t tanh(c_t)), so the hh Linears' A factors take the
+    per-factor fp32 path -- chained, deterministic too."""
+    import distributed_kfac_pytorch_amd as kfac
+    from distributed_kfac_pytorch_amd.models import lstm_lm
+
+    def run():
+        torch.manual_seed(0)
+        model = lstm_lm.LSTMModel(1000, 128, 128, 2, dropout=0.0).cuda()
+        pre = kfac.KFAC(model, factor_update_freq=1, inv_update_freq=1000, accumulate_data=True,
+                        skip_layers=['embedding', 'linear'])
+        x = torch.randint(0, 1000, (35, 20), device='cuda',
+                          generator=torch.Generator(device='cuda').manual_seed(1))
+        h = model.init_hidden(20)
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            out, _ = model(x, h)
+        out.float().sum().backward()
+        calls = []
+        orig = factors.update_factor
+        factors.update_factor = lambda *a, **k: calls.append(1) or orig(*a, **k)
+        try:
+            pre.compute_factors(alpha=0.95)
+        finally:
+            factors.update_factor = orig
+        # 2 layers x hh Linear: the A factors over the fp32 hidden states
+        assert len(calls) <= 4, 'more LSTM factors than the fp32 ones left the grouped path'
+        torch.cuda.synchronize()
+        return [(l.state['A'].clone(), l.state['G'].clone()) for l in pre.layers]
+
+    a, b = run(), run()
+    assert len(a) > 0
+    for (A1, G1), (A2, G2) in zip(a, b):
+        assert torch.equal(A1, A2) and torch.equal(G1, G2)
