@@ -96,6 +96,12 @@ __device__ inline void hh_scalars(double alpha, double sig2, double& beta, doubl
 __device__ __forceinline__ void find_mat(const int* __restrict__ offs, int nact, int& mi,
                                          int& base) {
   const int lane = threadIdx.x & 63, b = blockIdx.x;
+  if (nact <= 64) {     // one load; the base offset comes from lane mi (no second round trip)
+    const int o = gld_if(gptr(offs), lane, lane < nact, 0x7fffffff);
+    mi = __builtin_amdgcn_readfirstlane(__popcll(__ballot(o <= b)) - 1);
+    base = __builtin_amdgcn_readlane(o, mi);
+    return;
+  }
   int cnt = 0;
   for (int c0 = 0; c0 < nact; c0 += 64) {
     const int i = c0 + lane;
@@ -158,61 +164,73 @@ __global__ __launch_bounds__(256) void red_fin_kernel(const RMat* __restrict__ m
 
   // ---- every load up front (one memory round trip).  Indices are clamped
   // into the buffers and out-of-range terms dropped at use: per-load
-  // predicates would cost one SGPR mask each.
+  // predicates would cost one SGPR mask each.  At j = 0 the partial sums
+  // read stale slot data; they feed only the j >= 1 branch (no j1 test in
+  // the loads: a uniform test there became a branch, and a branch in the
+  // load section makes the compiler wait for every load before it).
+  // 32-bit element offsets from uniform bases (one offset VGPR per load, not
+  // a 64-bit address pair: at ~60 loads that sets the register budget)
+  const unsigned uld = (unsigned)ld, ulda = (unsigned)lda;
   float dk[DQ];                                         // kind `lane`, blocks s0p + q + 4 i
 #pragma unroll
-  for (int i = 0; i < DQ; ++i) dk[i] = DSp[(long long)min(s0p + q + 4 * i, nt - 1) * NK + lane];
+  for (int i = 0; i < DQ; ++i) dk[i] = DSp[(unsigned)min(s0p + q + 4 * i, nt - 1) * NK + lane];
   fx4 tq[TQ];
   const fx4 z4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int u = 0; u < TQ; ++u)
-    tq[u] = gld_if((const AS1 fx4*)TSp, (long long)tid + 256 * u, j1 && 4 * (tid + 256 * u) < ntri, z4);
+    tq[u] = gld_if32((const AS1 fx4*)TSp, (unsigned)(tid + 256 * u), 4 * (tid + 256 * u) < ntri, z4);
   // rows j, j+1: yh partials, lane = P column 2T + h - 2 s0p (several per lane);
   // column 2T+1 of a row of block B exists only for T <= B (see S)
   const int bj = j / TB, bj1 = (j + 1) / TB;
-  auto pcol_ok = [&](int col, int B) { return j1 && col >= 2 * s0p && col < 2 * nt &&
-                                             ((col & 1) == 0 || (col >> 1) <= B); };
+  // (bitwise & / |: a short-circuit && would branch, and a branch in the load
+  // section makes the compiler wait for every load issued before it)
+  auto pcol_ok = [&](int col, int B) -> bool {
+    return (col >= 2 * s0p) & (col < 2 * nt) & (((col & 1) == 0) | ((col >> 1) <= B));
+  };
   float pj = 0.f, pj1 = 0.f;
 #pragma unroll
   for (int h = 0; h < (2 * RB + 63) / 64; ++h) {
     const int col = 2 * s0p + lane + 64 * h;           // the 2 (nt - s0p) <= 2 RB live columns
-    pj += gld_if(Pp, col * ld + j, pcol_ok(col, bj), 0.f);
-    pj1 += gld_if(Pp, col * ld + j + 1, has1 && pcol_ok(col, bj1), 0.f);
+    pj += gld_if32(Pp, (unsigned)col * uld + j, pcol_ok(col, bj), 0.f);
+    pj1 += gld_if32(Pp, (unsigned)col * uld + j + 1, has1 & pcol_ok(col, bj1), 0.f);
   }
-  const float xhj1 = gld_if(XHp, j + 1, j1 && has1, 0.f);
+  const float xhj1 = gld_if32(XHp, j + 1, has1, 0.f);
   const float alpha = gSC[ps * 4];
   const float dprev = gSC[ps * 4 + 1];
-  float vj = gld_if(gV, lane * ld + j, lane < NB, 0.f);           // panel row j (lane = column)
-  float wj = gld_if(gW, lane * ld + j, lane < NB, 0.f);
-  float vj1 = gld_if(gV, lane * ld + j + 1, lane < NB && has1, 0.f);
-  float wj1 = gld_if(gW, lane * ld + j + 1, lane < NB && has1, 0.f);
-  const float ajj = gA[(long long)j * lda + j];
-  const float ajj1 = gld_if(gA, (long long)j * lda + j + 1, has1, 0.f);
-  const bool rok = r < n && r >= j + 1;                 // rows that get w_{j-1} and x_j
+  float vj = gld_if32(gV, (unsigned)lane * uld + j, lane < NB, 0.f);   // panel row j (lane = column)
+  float wj = gld_if32(gW, (unsigned)lane * uld + j, lane < NB, 0.f);
+  float vj1 = gld_if32(gV, (unsigned)lane * uld + j + 1, (lane < NB) & has1, 0.f);
+  float wj1 = gld_if32(gW, (unsigned)lane * uld + j + 1, (lane < NB) & has1, 0.f);
+  const float ajj = gA[(unsigned)j * ulda + j];
+  const float ajj1 = gld_if32(gA, (unsigned)j * ulda + j + 1, has1, 0.f);
+  const bool rok = (r < n) & (r >= j + 1);              // rows that get w_{j-1} and x_j
   const int rc = min(r, n - 1);
   float vr[XQ], wr[XQ];                                 // this quarter's panel columns of row r
 #pragma unroll
   for (int i = 0; i < XQ; ++i) {
-    vr[i] = gV[(q * XQ + i) * ld + rc];
-    wr[i] = gW[(q * XQ + i) * ld + rc];
+    vr[i] = gV[(unsigned)(q * XQ + i) * uld + rc];
+    wr[i] = gW[(unsigned)(q * XQ + i) * uld + rc];
   }
-  const float arow = gA[(long long)j * lda + rc];                     // base row j
-  const float brow = gld_if(gA, (long long)(j + 1) * lda + rc, has1 && rok, 0.f);
-  const float xhp = XHp[rc];
+  const float arow = gA[(unsigned)j * ulda + rc];                     // base row j
+  const float brow = gld_if32(gA, (unsigned)(j + 1) * ulda + rc, has1 & rok, 0.f);
+  const float xhp = XHp[(unsigned)rc];
   float pk[2 * PK];                                      // yh partials, P columns 2T, 2T+1, T = s0p + q + 4 i
 #pragma unroll
   for (int i = 0; i < PK; ++i) {
-    const long long t2 = 2 * min(s0p + q + 4 * i, nt - 1);
-    pk[2 * i] = Pp[t2 * ld + rc];
-    pk[2 * i + 1] = Pp[(t2 + 1) * ld + rc];
+    const unsigned t2 = 2 * min(s0p + q + 4 * i, nt - 1);
+    pk[2 * i] = Pp[t2 * uld + rc];
+    pk[2 * i + 1] = Pp[(t2 + 1) * uld + rc];
   }
+  // every load above is issued before anything consumes one (the scheduler
+  // otherwise interleaves early sums and waits on a half-issued batch)
+  __builtin_amdgcn_sched_barrier(0);
 
   // ---- global sums of column j-1 (wave = quarter of the blocks, lane = kind)
   //      and this quarter's share of each row's yh and old-panel corrections
   {
     double acc = 0.0;
 #pragma unroll
-    for (int i = 0; i < DQ; ++i) acc += (j1 && s0p + q + 4 * i < nt) ? (double)dk[i] : 0.0;
+    for (int i = 0; i < DQ; ++i) acc += (s0p + q + 4 * i < nt) ? (double)dk[i] : 0.0;
     sdk[q][lane] = acc;
     double t = 0.0;
 #pragma unroll
@@ -230,8 +248,8 @@ __global__ __launch_bounds__(256) void red_fin_kernel(const RMat* __restrict__ m
 #pragma unroll
     for (int i = 0; i < PK; ++i) {
       const int T = s0p + q + 4 * i;
-      yq += (j1 && T < nt) ? pk[2 * i] : 0.f;
-      yq += (j1 && T < nt && T <= br) ? pk[2 * i + 1] : 0.f;
+      yq += (T < nt) ? pk[2 * i] : 0.f;
+      yq += ((T < nt) & (T <= br)) ? pk[2 * i + 1] : 0.f;
     }
     float c3 = 0.f, c3p = 0.f;                           // old columns x < cp
 #pragma unroll
@@ -382,22 +400,46 @@ __global__ __launch_bounds__(256) void red_upd_kernel(const RMat* __restrict__ m
   I += s0; K += s0;
   const AS1 float* gV = gptr(M.V);
   const AS1 float* gW = gptr(M.W);
-#pragma unroll
-  for (int e0 = 0; e0 < TB * NB; e0 += 256) {
-    const int e = e0 + tid;
-    const int x = e / TB, rr = e - x * TB;            // rows fastest: coalesced columns
-    const int ri = I * TB + rr, rk = K * TB + rr;
-    const long long ld = M.ld;
-    const float vi = gld_if(gV, x * ld + ri, ri < n, 0.f);
-    const float wi = gld_if(gW, x * ld + ri, ri < n, 0.f);
-    const float vk = gld_if(gV, x * ld + rk, rk < n, 0.f);
-    const float wk = gld_if(gW, x * ld + rk, rk < n, 0.f);
-    sL[rr][x] = vi; sL[rr][NB + x] = wi;
-    sR[rr][x] = wk; sR[rr][NB + x] = vk;
-  }
-  __syncthreads();
+  AS1 float* const A = gptr(M.A);
+  const unsigned uld = (unsigned)M.ld, ulda = (unsigned)M.lda;
   const int wr = wave >> 1, wc = wave & 1;          // 2 x 2 waves of 64 x 64
   const int l31 = lane & 31, lh = lane >> 5;
+  // the panel rows of blocks I and K in one memory round trip (32-bit
+  // offsets, clamped, branch-free), then staged in LDS (loading each chunk
+  // right before its LDS store made the compiler wait 16 times)
+  float pv[4][TB * NB / 256];
+#pragma unroll
+  for (int u = 0; u < TB * NB / 256; ++u) {
+    const int e = u * 256 + tid;
+    const int x = e / TB, rr = e - x * TB;            // rows fastest: coalesced columns
+    const int ri = min(I * TB + rr, n - 1), rk = min(K * TB + rr, n - 1);
+    pv[0][u] = gV[(unsigned)x * uld + ri];
+    pv[1][u] = gW[(unsigned)x * uld + ri];
+    pv[2][u] = gV[(unsigned)x * uld + rk];
+    pv[3][u] = gW[(unsigned)x * uld + rk];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int u = 0; u < TB * NB / 256; ++u) {
+    const int e = u * 256 + tid;
+    const int x = e / TB, rr = e - x * TB;
+    const bool oi = I * TB + rr < n, ok = K * TB + rr < n;
+    sL[rr][x] = oi ? pv[0][u] : 0.f; sL[rr][NB + x] = oi ? pv[1][u] : 0.f;
+    sR[rr][x] = ok ? pv[3][u] : 0.f; sR[rr][NB + x] = ok ? pv[2][u] : 0.f;
+  }
+  __syncthreads();
+  // the old tile values, issued now: they land under the MFMA loop
+  float old[2][2][16];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int x = 0; x < 16; ++x) {
+        const int gr = min(I * TB + wr * 64 + a * 32 + (x & 3) + 8 * (x >> 2) + 4 * lh, n - 1);
+        const int gc = min(K * TB + wc * 64 + b * 32 + l31, n - 1);
+        old[a][b][x] = A[(unsigned)gr * ulda + gc];
+      }
   f32x16_t acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -419,29 +461,18 @@ __global__ __launch_bounds__(256) void red_upd_kernel(const RMat* __restrict__ m
       for (int b = 0; b < 2; ++b)
         acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[b], acc[a][b], 0, 0, 0);
   }
-  // C/D map of 32x32: row = (x&3) + 8 (x>>2) + 4 lh, col = lane & 31.  Per
-  // 32 x 32 block: its 16 old values loaded (clamped, branch-free), then stored
-  AS1 float* const A = gptr(M.A);
+  // C/D map of 32x32: row = (x&3) + 8 (x>>2) + 4 lh, col = lane & 31
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      float old[16];
+    for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int x = 0; x < 16; ++x) {
         const int gr = I * TB + wr * 64 + a * 32 + (x & 3) + 8 * (x >> 2) + 4 * lh;
         const int gc = K * TB + wc * 64 + b * 32 + l31;
-        const bool ok = gr >= q + 1 && gr < n && gc >= gr && gc < n;
-        old[x] = gld_if(A, (long long)gr * M.lda + gc, ok, 0.f);
+        if ((gr >= q + 1) & (gr < n) & (gc >= gr) & (gc < n))
+          A[(unsigned)gr * ulda + gc] = old[a][b][x] - acc[a][b][x];
       }
-#pragma unroll
-      for (int x = 0; x < 16; ++x) {
-        const int gr = I * TB + wr * 64 + a * 32 + (x & 3) + 8 * (x >> 2) + 4 * lh;
-        const int gc = K * TB + wc * 64 + b * 32 + l31;
-        if (gr >= q + 1 && gr < n && gc >= gr && gc < n)
-          A[(long long)gr * M.lda + gc] = old[x] - acc[a][b][x];
-      }
-    }
 }
 
 // ------------------------------------------------------------------- S
@@ -523,12 +554,6 @@ __global__ __launch_bounds__(256) void red_symv_kernel(const RMat* __restrict__ 
   if (stamps && blockIdx.x == 0 && tid == 0)
     stamps[(long long)j * 16 + 14] = __builtin_amdgcn_s_memrealtime();
   const int rb = I * TB + hr * HT;                     // first row of the half
-  // xh of the half's rows (sv[0]) and of block K's columns (sv[1]), from F(j)
-  {
-    const AS1 float* XH = gptr(M.XH) + cs * M.sX;
-    if (tid < HT) sv[0][tid] = gld_if(XH, rb + tid, rb + tid < n, 0.f);
-    if (tid < TB) sv[1][tid] = gld_if(XH, K * TB + tid, K * TB + tid < n, 0.f);
-  }
   const int hw = lane >> 5, cl = lane & 31;
   const int kk0 = cl * 4, k0 = K * TB + kk0;
   // branch-free tile loads: row clamped to n-1, column start clamped inside
@@ -541,8 +566,19 @@ __global__ __launch_bounds__(256) void red_symv_kernel(const RMat* __restrict__ 
     const int rr = rb + wave * (HT / 4) + it * 2 + hw;
     const fx4 t = *(const AS1 fx4*)(gA + (long long)min(rr, n - 1) * lda + kc);
     const bool ok = rr < n;
-    q[it] = make_float4((ok && k0 < n) ? t.x : 0.f, (ok && k0 + 1 < n) ? t.y : 0.f,
-                        (ok && k0 + 2 < n) ? t.z : 0.f, (ok && k0 + 3 < n) ? t.w : 0.f);
+    q[it] = make_float4((ok & (k0 < n)) ? t.x : 0.f, (ok & (k0 + 1 < n)) ? t.y : 0.f,
+                        (ok & (k0 + 2 < n)) ? t.z : 0.f, (ok & (k0 + 3 < n)) ? t.w : 0.f);
+  }
+  // xh of the half's rows (sv[0]) and of block K's columns (sv[1]), from F(j):
+  // loaded by every thread after the tile (clamped, branch-free), so the one
+  // wait before the LDS writes covers the tile too (one memory round trip)
+  {
+    const AS1 float* XH = gptr(M.XH) + cs * M.sX;
+    const int r0 = rb + (tid & (HT - 1)), c0 = K * TB + (tid & (TB - 1));
+    const float x0 = gld_if(XH, r0, r0 < n, 0.f);
+    const float x1 = gld_if(XH, c0, c0 < n, 0.f);
+    if (tid < HT) sv[0][tid] = x0;
+    if (tid < TB) sv[1][tid] = x1;
   }
   __syncthreads();
   if (stamps && blockIdx.x == 0 && tid == 0)
