@@ -476,25 +476,133 @@ __global__ __launch_bounds__(256) void red_upd_kernel(const RMat* __restrict__ m
 }
 
 // ------------------------------------------------------------------- S
-// Workgroups 0 .. ntri-1 of a matrix: tile (I, K) of the upper triangle of
-// A22, yh partials per row into P (row sums of block I at column K, column
-// sums of block K at column I) and the tile's xh.yh into TS.  Workgroups
-// ntri .. ntri + nb - 1: row block b = s0 + (local - ntri), the NK partial
-// kinds of its 128 rows into DS (lane = kind, wave = 32 rows, fixed order).
+// One half tile (I, K, hr): rows rb .. rb+63 (rb = I TB + 64 hr) x columns
+// K TB .. K TB + 127 of A22, times xh.  Thread (wave w, lane = 16 rg + cg)
+// owns rows 4 R .. 4 R + 3 (R = 4 w + rg) x columns 8 cg .. 8 cg + 7: eight
+// 16-byte loads, 32 FMAs for its 4 row partials and 32 for its 8 column
+// partials; rows are summed over the 16 lanes of a DPP row, columns over the
+// 4 row groups of a wave (permlane swaps) and the 4 waves (one LDS pass).
+// A and xh are zero past n up to nt TB (the buffers are padded), so no load
+// is masked.  P columns: 2T + h, T = the other tile index (see F):
+// off-diagonal: row sums -> 2K, column sums of half hr -> 2I + hr; diagonal:
+// half hr -> 2I + hr for all 128 rows of block I (column sums, plus the row
+// sums of its own 64 rows).  The tile's xh.yh -> TS (triangle order).
+struct SymvShared {
+  float cred[4][TB];     // column partials per wave
+  float rsum[HT];        // row sums (diagonal tiles)
+  double tred[4];
+};
+
+__device__ __forceinline__ float row16_sum(float v) {   // over the 16 lanes of a DPP row
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  v += dpp_f<0x140>(v);
+  return v;
+}
+
+template <bool DIAG>
+__device__ __forceinline__ void symv_half(const RMat& M, int I, int K, int hr, int cs, int local,
+                                          SymvShared& sh, int j, unsigned long long* stamps) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int rg = lane >> 4, cg = lane & 15;
+  const int R = wave * 4 + rg;                          // row group of 4 rows
+  const int rb = I * TB + hr * HT;
+  const unsigned ulda = (unsigned)M.lda;
+  const AS1 float* gA = gptr(M.A);
+  const AS1 float* XH = gptr(M.XH) + cs * M.sX;
+  // ---- loads, one round trip
+  fx4 a[4][2];
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      a[rr][h] = *(const AS1 fx4*)(gA + (unsigned)(rb + 4 * R + rr) * ulda + K * TB + 8 * cg + 4 * h);
+  const fx4 xr = *(const AS1 fx4*)(XH + (unsigned)(rb + 4 * R));
+  const fx4 xc0 = *(const AS1 fx4*)(XH + (unsigned)(K * TB + 8 * cg));
+  const fx4 xc1 = *(const AS1 fx4*)(XH + (unsigned)(K * TB + 8 * cg + 4));
+  const float xcol = XH[(unsigned)((DIAG ? I : K) * TB + (tid & (TB - 1)))];   // column `tid`
+  if (stamps && blockIdx.x == 0 && tid == 0)
+    stamps[(long long)j * 16 + 14] = __builtin_amdgcn_s_memrealtime();
+  const float xcv[8] = {xc0.x, xc0.y, xc0.z, xc0.w, xc1.x, xc1.y, xc1.z, xc1.w};
+  const float xrv[4] = {xr.x, xr.y, xr.z, xr.w};
+  float rp[4], cp[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) cp[c] = 0.f;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const float av[8] = {a[rr][0].x, a[rr][0].y, a[rr][0].z, a[rr][0].w,
+                         a[rr][1].x, a[rr][1].y, a[rr][1].z, a[rr][1].w};
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      if (DIAG) {        // upper triangle: row sums take col >= row, column sums col > row
+        const int lr = hr * HT + 4 * R + rr, lc = 8 * cg + c;
+        acc += (lc >= lr) ? av[c] * xcv[c] : 0.f;
+        cp[c] += (lc > lr) ? av[c] * xrv[rr] : 0.f;
+      } else {
+        acc += av[c] * xcv[c];
+        cp[c] += av[c] * xrv[rr];
+      }
+    }
+    rp[rr] = row16_sum(acc);
+  }
+#pragma unroll
+  for (int c = 0; c < 8; ++c) cp[c] = swap_sum32(swap_sum16(cp[c]));
+  if (stamps && blockIdx.x == 0 && tid == 0)
+    stamps[(long long)j * 16 + 15] = __builtin_amdgcn_s_memrealtime();
+  if (rg == 0) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) sh.cred[wave][8 * cg + c] = cp[c];
+  }
+  // this lane's row (cg < 4): row 4 R + cg of the half
+  const float myrow = cg == 0 ? rp[0] : (cg == 1 ? rp[1] : (cg == 2 ? rp[2] : rp[3]));
+  const float myx = cg == 0 ? xrv[0] : (cg == 1 ? xrv[1] : (cg == 2 ? xrv[2] : xrv[3]));
+  AS1 float* const Pc = gptr(M.P) + cs * M.sP;
+  const unsigned uld = (unsigned)M.ld;
+  double tp = 0.0;
+  if (DIAG) {
+    if (cg < 4) sh.rsum[4 * R + cg] = myrow;
+  } else if (cg < 4) {
+    Pc[(unsigned)(2 * K) * uld + rb + 4 * R + cg] = myrow;
+    tp = (double)myx * (double)myrow;
+  }
+  kfac_lds_barrier();
+  if (tid < TB) {
+    float v = (sh.cred[0][tid] + sh.cred[1][tid]) + (sh.cred[2][tid] + sh.cred[3][tid]);
+    if (DIAG) {
+      const int rl = tid - hr * HT;
+      if (rl >= 0 && rl < HT) v += sh.rsum[rl];
+      Pc[(unsigned)(2 * I + hr) * uld + I * TB + tid] = v;
+    } else {
+      Pc[(unsigned)(2 * I + hr) * uld + K * TB + tid] = v;
+    }
+    tp += (double)xcol * (double)v;
+  }
+  tp = wave_sum_d(tp);
+  if (lane == 0) sh.tred[wave] = tp;
+  kfac_lds_barrier();
+  if (tid == 0)
+    gptr(M.TS)[cs * M.sTS + local] = (float)((sh.tred[0] + sh.tred[1]) + (sh.tred[2] + sh.tred[3]));
+  if (stamps && blockIdx.x == 0 && tid == 0)
+    stamps[(long long)j * 16 + 11] = __builtin_amdgcn_s_memrealtime();
+}
+
+// Workgroups 0 .. 2 ntri-1 of a matrix: half tiles (symv_half).  Workgroups
+// 2 ntri .. 2 ntri + nb - 1: row block b = s0 + (local - 2 ntri), the NK
+// partial kinds of its 128 rows into DS (wave = 16 kinds, lane = row, fixed
+// order).
 __global__ __launch_bounds__(256) void red_symv_kernel(const RMat* __restrict__ mats,
                                                        const int* __restrict__ offs, int nact,
                                                        int j) {
-  __shared__ float sv[2][TB];
-  __shared__ float rowred[HT][33];
-  __shared__ float colred[4][TB];
-  __shared__ double tred[2];
+  __shared__ SymvShared sred;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   unsigned long long* const stamps = g_stamps;
   int mi, base;
   find_mat(offs, nact, mi, base);
   const RMat M = mats[mi];
   const int n = M.n, nt = M.nt;
-  const long long lda = M.lda, ld = M.ld;
+  const long long ld = M.ld;
   const int s0 = (j + 1) / TB;
   const int ntri = (nt - s0) * (nt - s0 + 1);          // tile halves
   const int local = blockIdx.x - base;
@@ -544,108 +652,14 @@ __global__ __launch_bounds__(256) void red_symv_kernel(const RMat* __restrict__ 
   }
   if (stamps && blockIdx.x == 0 && tid == 0)
     stamps[(long long)j * 16 + 10] = __builtin_amdgcn_s_memrealtime();
-  // tile (I, K), row half hr: 64 rows x 128 columns (32 KB: a workgroup pulls
-  // ~30 GB/s, so half tiles halve the launch's latency)
   const int hr = local & 1;
   int I, K;
   tri_index(local >> 1, nt - s0, I, K);
   I += s0; K += s0;
-  const bool diag = (I == K);
-  if (stamps && blockIdx.x == 0 && tid == 0)
-    stamps[(long long)j * 16 + 14] = __builtin_amdgcn_s_memrealtime();
-  const int rb = I * TB + hr * HT;                     // first row of the half
-  const int hw = lane >> 5, cl = lane & 31;
-  const int kk0 = cl * 4, k0 = K * TB + kk0;
-  // branch-free tile loads: row clamped to n-1, column start clamped inside
-  // the row (lda % 4 == 0, lda >= n); out-of-range entries zeroed after
-  const int kc = min(k0, (int)lda - 4);
-  const AS1 float* gA = gptr(M.A);
-  float4 q[HT / 8];
-#pragma unroll
-  for (int it = 0; it < HT / 8; ++it) {
-    const int rr = rb + wave * (HT / 4) + it * 2 + hw;
-    const fx4 t = *(const AS1 fx4*)(gA + (long long)min(rr, n - 1) * lda + kc);
-    const bool ok = rr < n;
-    q[it] = make_float4((ok & (k0 < n)) ? t.x : 0.f, (ok & (k0 + 1 < n)) ? t.y : 0.f,
-                        (ok & (k0 + 2 < n)) ? t.z : 0.f, (ok & (k0 + 3 < n)) ? t.w : 0.f);
-  }
-  // xh of the half's rows (sv[0]) and of block K's columns (sv[1]), from F(j):
-  // loaded by every thread after the tile (clamped, branch-free), so the one
-  // wait before the LDS writes covers the tile too (one memory round trip)
-  {
-    const AS1 float* XH = gptr(M.XH) + cs * M.sX;
-    const int r0 = rb + (tid & (HT - 1)), c0 = K * TB + (tid & (TB - 1));
-    const float x0 = gld_if(XH, r0, r0 < n, 0.f);
-    const float x1 = gld_if(XH, c0, c0 < n, 0.f);
-    if (tid < HT) sv[0][tid] = x0;
-    if (tid < TB) sv[1][tid] = x1;
-  }
-  __syncthreads();
-  if (stamps && blockIdx.x == 0 && tid == 0)
-    stamps[(long long)j * 16 + 15] = __builtin_amdgcn_s_memrealtime();
-  float ca[4] = {0.f, 0.f, 0.f, 0.f};
-  const float vk0 = sv[1][kk0], vk1 = sv[1][kk0 + 1], vk2 = sv[1][kk0 + 2], vk3 = sv[1][kk0 + 3];
-#pragma unroll
-  for (int it = 0; it < HT / 8; ++it) {
-    const int rl = wave * (HT / 4) + it * 2 + hw;      // row within the half
-    const int rk = hr * HT + rl;                       // row within block I
-    float x0 = q[it].x, x1 = q[it].y, x2 = q[it].z, x3 = q[it].w;
-    const float vrr = sv[0][rl];
-    if (diag) {   // upper triangle only: row sums take k >= r, column sums k > r
-      x0 = (kk0 >= rk) ? x0 : 0.f;
-      x1 = (kk0 + 1 >= rk) ? x1 : 0.f;
-      x2 = (kk0 + 2 >= rk) ? x2 : 0.f;
-      x3 = (kk0 + 3 >= rk) ? x3 : 0.f;
-      ca[0] += (kk0 > rk) ? x0 * vrr : 0.f;
-      ca[1] += (kk0 + 1 > rk) ? x1 * vrr : 0.f;
-      ca[2] += (kk0 + 2 > rk) ? x2 * vrr : 0.f;
-      ca[3] += (kk0 + 3 > rk) ? x3 * vrr : 0.f;
-    } else {
-      ca[0] += x0 * vrr; ca[1] += x1 * vrr; ca[2] += x2 * vrr; ca[3] += x3 * vrr;
-    }
-    rowred[rl][cl] = x0 * vk0 + x1 * vk1 + x2 * vk2 + x3 * vk3;
-  }
-#pragma unroll
-  for (int x = 0; x < 4; ++x) ca[x] += __shfl_xor(ca[x], 32, 64);
-  if (hw == 0) {
-#pragma unroll
-    for (int x = 0; x < 4; ++x) colred[wave][kk0 + x] = ca[x];
-  }
-  kfac_lds_barrier();
-  // P columns: 2T + h, T = the other tile index (see F).  Off-diagonal: row
-  // sums -> column 2K (h = 0), column sums of half hr -> 2I + hr.  Diagonal:
-  // half hr -> column 2I + hr for all 128 rows of block I (column sums, plus
-  // the row sums of its own 64 rows).
-  AS1 float* const Pc = gptr(M.P) + cs * M.sP;
-  double tp = 0.0;
-  if (tid < TB) {
-    const float csum = colred[0][tid] + colred[1][tid] + colred[2][tid] + colred[3][tid];
-    const int rown = tid - hr * HT;                    // this column as a row of the half
-    float rs = 0.f;
-    if (diag ? (rown >= 0 && rown < HT) : tid < HT) {
-      const int rl = diag ? rown : tid;
-#pragma unroll 8
-      for (int l = 0; l < 32; ++l) rs += rowred[rl][l];
-    }
-    if (diag) {
-      const float v = csum + rs;
-      Pc[(2 * I + hr) * ld + I * TB + tid] = v;
-      tp = (double)sv[1][tid] * (double)v;
-    } else {
-      Pc[(2 * I + hr) * ld + K * TB + tid] = csum;
-      tp = (double)sv[1][tid] * (double)csum;
-      if (tid < HT) {
-        Pc[(2 * K) * ld + rb + tid] = rs;
-        tp += (double)sv[0][tid] * (double)rs;
-      }
-    }
-  }
-  tp = wave_sum_d(tp);
-  if (lane == 0 && wave < 2) tred[wave] = tp;
-  kfac_lds_barrier();
-  if (tid == 0) gptr(M.TS)[cs * M.sTS + local] = (float)(tred[0] + tred[1]);   // triangle order
-  if (stamps && blockIdx.x == 0 && tid == 0)
-    stamps[(long long)j * 16 + 11] = __builtin_amdgcn_s_memrealtime();
+  if (I == K)
+    symv_half<true>(M, I, K, hr, cs, local, sred, j, stamps);
+  else
+    symv_half<false>(M, I, K, hr, cs, local, sred, j, stamps);
 }
 
 // ------------------------------------------------------------------ host
@@ -759,9 +773,10 @@ RPlan* plan_for(const KfacReduceRecord* recs, int count, bool capture, int* err)
   std::vector<RMat> mats;
   for (int oi : order) {
     const KfacReduceRecord& r = recs[oi];
-    if (r.n < 2 || r.lda < r.n || (r.lda & 3)) { *err = -2; return nullptr; }
+    if (r.n < 2) { *err = -2; return nullptr; }
     if (r.n > NMAX) { *err = -6; return nullptr; }
     const WsLayout L = ws_layout(r.n);
+    if (r.lda < (long long)L.nt * TB || (r.lda % TB)) { *err = -2; return nullptr; }
     RMat M;
     memset(&M, 0, sizeof(M));
     M.A = r.A; M.lda = r.lda; M.n = (int)r.n; M.nt = L.nt; M.ld = L.ld;
@@ -838,8 +853,9 @@ RPlan* plan_for(const KfacReduceRecord* recs, int count, bool capture, int* err)
 }  // namespace
 
 // Tridiagonalise `count` symmetric matrices (any sizes 2 .. 16384) with one
-// launch sequence for all of them: A (n x lda, row-major, upper triangle read
-// and overwritten by the reflectors), d, e, tau (n floats each), ws
+// launch sequence for all of them: A (lda x lda, row-major, lda = n rounded up
+// to a multiple of 128, zero outside the leading n x n block; its upper
+// triangle is read and overwritten by the reflectors), d, e, tau (n floats each), ws
 // (kfac_reduce_ws_floats(n) floats, 256-byte aligned, zeroed once).
 KFAC_API int kfac_reduce_batched(const KfacReduceRecord* recs, int count, int use_graph,
                                  hipStream_t stream) {

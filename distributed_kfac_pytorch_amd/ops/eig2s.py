@@ -112,7 +112,7 @@ def two_stage_group(mats, clip, stream, use_graph=True, slot=0):
             bufs.append((n, idx, B, X))
             lda = B['lda']
             for i, m in enumerate(idx):
-                B['A'][i, :, :n].copy_(mats[m])
+                B['A'][i, :n, :n].copy_(mats[m])
             dcr = eigen._dc_records(B, n, b)
             for i in range(b):
                 r = s1[k]

@@ -135,13 +135,16 @@ def _tri_buffers(dev, n, b, slot=0):
     bufs = _TRI_BUFS.get(key)
     if bufs is None:
         L = _lib.lib()
-        lda = (n + 63) // 64 * 64   # zero-padded rows: k-steps of the MFMA GEMMs
+        # A: lda x lda per matrix, lda = n rounded up to the reduction's 128-row
+        # tiles, zero past n (its symv tiles read whole tiles unmasked; the
+        # MFMA GEMMs of the back-transformation step k by 64)
+        lda = (n + 127) // 128 * 128
         wsf = int(L.kfac_sytrd_ws_floats(n))
         f32 = dict(dtype=torch.float32, device=dev)
         nblk = (n + BT - 1) // BT
         wsb = int(L.kfac_dc_ws_bytes(n))
         rwsf = int(L.kfac_reduce_ws_floats(n))
-        bufs = dict(lda=lda, A=torch.zeros(b, n, lda, **f32), Z=torch.zeros(b, n, lda, **f32),
+        bufs = dict(lda=lda, sA=lda * lda, A=torch.zeros(b, lda, lda, **f32), Z=torch.zeros(b, n, lda, **f32),
                     d=torch.zeros(b, n, **f32), e=torch.zeros(b, n, **f32),
                     w=torch.zeros(b, n, **f32), wsb=wsb,
                     dcws=torch.zeros(b * wsb, dtype=torch.uint8, device=dev),
@@ -170,8 +173,8 @@ def _tridiag_class(mats, clip, stream, use_graph=None, slot=0):
         B = _tri_buffers(dev, n, b, slot)
         lda = B['lda']
         for i, A in enumerate(mats):
-            B['A'][i, :, :n].copy_(A)
-        sA = n * lda
+            B['A'][i, :n, :n].copy_(A)
+        sA = B['sA']
         cs = _lib.c_vp(stream.cuda_stream)
         _lib.check(L.kfac_sytrd_batched(_lib.ptr(B['A']), lda, sA, n, b, _lib.ptr(B['d']),
                                         _lib.ptr(B['e']), _lib.ptr(B['tau']), _lib.ptr(B['ws']),
@@ -266,7 +269,7 @@ def tridiag_eigh(ds, es, use_graph=False):
 
 def _bt_args(B, n, b):
     lda = B['lda']
-    return (_lib.ptr(B['A']), lda, n * lda, _lib.ptr(B['tau']), _lib.ptr(B['Z']), lda, n * lda,
+    return (_lib.ptr(B['A']), lda, B['sA'], _lib.ptr(B['tau']), _lib.ptr(B['Z']), lda, n * lda,
             n, b, _lib.ptr(B['T']), _lib.ptr(B['W1']), _lib.ptr(B['W2']), _lib.ptr(B['Vt']))
 
 
@@ -276,7 +279,7 @@ def _tridiag_prepare(n, b, dev, slot=0):
     not overlap other threads' library calls (hipBLASLt inside rocBLAS)."""
     B = _tri_buffers(dev, n, b, slot)
     lda = B['lda']
-    _lib.check(_lib.lib().kfac_sytrd_prepare(_lib.ptr(B['A']), lda, n * lda, n, b,
+    _lib.check(_lib.lib().kfac_sytrd_prepare(_lib.ptr(B['A']), lda, B['sA'], n, b,
                                              _lib.ptr(B['d']), _lib.ptr(B['e']),
                                              _lib.ptr(B['tau']), _lib.ptr(B['ws'])),
                'kfac_sytrd_prepare')
@@ -432,7 +435,7 @@ def _fused_group(mats, clip, stream, use_graph, slot=0):
             B = _tri_buffers(dev, n, b, slot)     # per group: concurrent groups never share
             bufs.append((n, idx, B))
             for i, m in enumerate(idx):
-                B['A'][i, :, :n].copy_(mats[m])
+                B['A'][i, :n, :n].copy_(mats[m])
             dcr = _dc_records(B, n, b)
             for i in range(b):
                 r = rr[k]

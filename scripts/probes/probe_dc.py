@@ -32,9 +32,9 @@ def main():
         A = (X @ X.transpose(1, 2) / X.shape[2] + 1e-3 * torch.eye(n, device=dev))
         B = eigen._tri_buffers(dev, n, b)
         lda = B['lda']
-        B['A'][:, :, :n].copy_(A)
+        B['A'][:, :n, :n].copy_(A)
         L = _lib.lib()
-        _lib.check(L.kfac_sytrd_batched(_lib.ptr(B['A']), lda, n * lda, n, b, _lib.ptr(B['d']),
+        _lib.check(L.kfac_sytrd_batched(_lib.ptr(B['A']), lda, B['sA'], n, b, _lib.ptr(B['d']),
                                         _lib.ptr(B['e']), _lib.ptr(B['tau']), _lib.ptr(B['ws']),
                                         0, _lib.stream()), 'sytrd')
         recs = eigen._dc_records(B, n, b)
@@ -51,7 +51,7 @@ def main():
         t_bt = timeit(lambda: _lib.check(L.kfac_tridiag_backtransform(
             *eigen._bt_args(B, n, b), 1, cs), 'bt'))
         t_red = timeit(lambda: _lib.check(L.kfac_sytrd_batched(
-            _lib.ptr(B['A']), lda, n * lda, n, b, _lib.ptr(B['d']), _lib.ptr(B['e']),
+            _lib.ptr(B['A']), lda, B['sA'], n, b, _lib.ptr(B['d']), _lib.ptr(B['e']),
             _lib.ptr(B['tau']), _lib.ptr(B['ws']), 1, cs), 'sytrd'), reps=1)
         print('n=%5d b=%d  dc %7.2f ms  stedc %7.2f ms  backtransform %7.2f ms  reduction %7.2f ms'
               % (n, b, t_dc, t_st, t_bt, t_red), flush=True)

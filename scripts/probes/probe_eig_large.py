@@ -33,7 +33,7 @@ def main():
           'fp32 rounding shift %.2e' % ((ref32 - ref).abs().max().item() / an))
     L = _lib.lib()
     B = eigen._tri_buffers(dev, n, 1, slot=7)
-    B['A'][0, :, :n].copy_(A32)
+    B['A'][0, :n, :n].copy_(A32)
     rr = (_lib.ReduceRecord * 1)()
     r = rr[0]
     r.A, r.lda, r.d = B['A'][0].data_ptr(), B['lda'], B['d'][0].data_ptr()

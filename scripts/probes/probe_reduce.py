@@ -35,7 +35,7 @@ def records(classes, dev):
         b = len(mats)
         B = eigen._tri_buffers(dev, n, b, slot=7)
         for i, m in enumerate(mats):
-            B['A'][i, :, :n].copy_(m)
+            B['A'][i, :n, :n].copy_(m)
         dcr = eigen._dc_records(B, n, b)
         for i in range(b):
             r = rr[k]

@@ -25,7 +25,7 @@ def main():
     dev = torch.device('cuda')
     L = _lib.lib()
     B = eigen._tri_buffers(dev, n, 1, slot=9)
-    B['A'][0, :, :n].copy_(A32.to(dev))
+    B['A'][0, :n, :n].copy_(A32.to(dev))
     rr = (_lib.ReduceRecord * 1)()
     r = rr[0]
     r.A, r.lda, r.d = B['A'][0].data_ptr(), B['lda'], B['d'][0].data_ptr()

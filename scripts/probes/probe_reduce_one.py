@@ -20,7 +20,7 @@ def main():
     g = torch.Generator(device=dev).manual_seed(n)
     B = eigen._tri_buffers(dev, n, b)
     X = torch.randn(b, n, n // 3, device=dev, generator=g)
-    B['A'][:, :, :n].copy_(X @ X.transpose(1, 2) / X.shape[2])
+    B['A'][:, :n, :n].copy_(X @ X.transpose(1, 2) / X.shape[2])
     rr = (_lib.ReduceRecord * b)()
     for i in range(b):
         r = rr[i]

@@ -43,7 +43,7 @@ def main():
         t_tri = timeit(lambda: eigen._tridiag_class(mats, 0.0, cur))
         B = eigen._tri_buffers(dev, n, b)
         lda = B['lda']
-        red = timeit(lambda: L.kfac_sytrd_batched(_lib.ptr(B['A']), lda, n * lda, n, b,
+        red = timeit(lambda: L.kfac_sytrd_batched(_lib.ptr(B['A']), lda, B['sA'], n, b,
                                                   _lib.ptr(B['d']), _lib.ptr(B['e']),
                                                   _lib.ptr(B['tau']), _lib.ptr(B['ws']), 1,
                                                   _lib.stream()))

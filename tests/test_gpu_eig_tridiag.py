@@ -23,9 +23,9 @@ def _sytrd(mats):
     B = eigen._tri_buffers(torch.device(DEV), n, b)
     lda = B['lda']
     for i, A in enumerate(mats):
-        B['A'][i, :, :n].copy_(A)
+        B['A'][i, :n, :n].copy_(A)
     s = _lib.stream()
-    _lib.check(_lib.lib().kfac_sytrd_batched(_lib.ptr(B['A']), lda, n * lda, n, b,
+    _lib.check(_lib.lib().kfac_sytrd_batched(_lib.ptr(B['A']), lda, B['sA'], n, b,
                                              _lib.ptr(B['d']), _lib.ptr(B['e']),
                                              _lib.ptr(B['tau']), _lib.ptr(B['ws']), 0, s),
                'sytrd')
