@@ -487,10 +487,15 @@ __global__ __launch_bounds__(256) void red_upd_kernel(const RMat* __restrict__ m
 // off-diagonal: row sums -> 2K, column sums of half hr -> 2I + hr; diagonal:
 // half hr -> 2I + hr for all 128 rows of block I (column sums, plus the row
 // sums of its own 64 rows).  The tile's xh.yh -> TS (triangle order).
+// half tiles per S workgroup (1 or 2).  2 (64 KB per workgroup) measured
+// slower: the first workgroup's loads took 1.6 vs 0.74 us at the tail (a
+// workgroup pulls ~40 GB/s), 4608 x 3 75.9 vs 74.7 ms
+// (profiles/r3_symv_snh2_stamps_4608x3.log)
+constexpr int SNH = 1;
 struct SymvShared {
-  float cred[4][TB];     // column partials per wave
-  float rsum[HT];        // row sums (diagonal tiles)
-  double tred[4];
+  float cred[SNH][4][TB];   // column partials per half and wave
+  float rsum[SNH][HT];      // row sums (diagonal tiles)
+  double tred[SNH][4];
 };
 
 __device__ __forceinline__ float row16_sum(float v) {   // over the 16 lanes of a DPP row
@@ -501,95 +506,114 @@ __device__ __forceinline__ float row16_sum(float v) {   // over the 16 lanes of 
   return v;
 }
 
-template <bool DIAG>
-__device__ __forceinline__ void symv_half(const RMat& M, int I, int K, int hr, int cs, int local,
-                                          SymvShared& sh, int j, unsigned long long* stamps) {
+// NH = SNH consecutive half tiles hr0 .. hr0 + NH - 1 of tile (I, K); `half0`
+// = the first one's index in triangle order (its TS slot)
+template <bool DIAG, int NH>
+__device__ __forceinline__ void symv_halves(const RMat& M, int I, int K, int hr0, int cs,
+                                            int half0, SymvShared& sh, int j,
+                                            unsigned long long* stamps) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rg = lane >> 4, cg = lane & 15;
   const int R = wave * 4 + rg;                          // row group of 4 rows
-  const int rb = I * TB + hr * HT;
   const unsigned ulda = (unsigned)M.lda;
   const AS1 float* gA = gptr(M.A);
   const AS1 float* XH = gptr(M.XH) + cs * M.sX;
   // ---- loads, one round trip
-  fx4 a[4][2];
+  fx4 a[NH][4][2], xr[NH];
 #pragma unroll
-  for (int rr = 0; rr < 4; ++rr)
+  for (int u = 0; u < NH; ++u) {
+    const int rb = I * TB + (hr0 + u) * HT;
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-      a[rr][h] = *(const AS1 fx4*)(gA + (unsigned)(rb + 4 * R + rr) * ulda + K * TB + 8 * cg + 4 * h);
-  const fx4 xr = *(const AS1 fx4*)(XH + (unsigned)(rb + 4 * R));
+    for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        a[u][rr][h] =
+            *(const AS1 fx4*)(gA + (unsigned)(rb + 4 * R + rr) * ulda + K * TB + 8 * cg + 4 * h);
+    xr[u] = *(const AS1 fx4*)(XH + (unsigned)(rb + 4 * R));
+  }
   const fx4 xc0 = *(const AS1 fx4*)(XH + (unsigned)(K * TB + 8 * cg));
   const fx4 xc1 = *(const AS1 fx4*)(XH + (unsigned)(K * TB + 8 * cg + 4));
-  const float xcol = XH[(unsigned)((DIAG ? I : K) * TB + (tid & (TB - 1)))];   // column `tid`
+  const float xcol = XH[(unsigned)(K * TB + (tid & (TB - 1)))];   // column `tid`
   if (stamps && blockIdx.x == 0 && tid == 0)
     stamps[(long long)j * 16 + 14] = __builtin_amdgcn_s_memrealtime();
   const float xcv[8] = {xc0.x, xc0.y, xc0.z, xc0.w, xc1.x, xc1.y, xc1.z, xc1.w};
-  const float xrv[4] = {xr.x, xr.y, xr.z, xr.w};
-  float rp[4], cp[8];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) cp[c] = 0.f;
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    const float av[8] = {a[rr][0].x, a[rr][0].y, a[rr][0].z, a[rr][0].w,
-                         a[rr][1].x, a[rr][1].y, a[rr][1].z, a[rr][1].w};
-    float acc = 0.f;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      if (DIAG) {        // upper triangle: row sums take col >= row, column sums col > row
-        const int lr = hr * HT + 4 * R + rr, lc = 8 * cg + c;
-        acc += (lc >= lr) ? av[c] * xcv[c] : 0.f;
-        cp[c] += (lc > lr) ? av[c] * xrv[rr] : 0.f;
-      } else {
-        acc += av[c] * xcv[c];
-        cp[c] += av[c] * xrv[rr];
-      }
-    }
-    rp[rr] = row16_sum(acc);
-  }
-#pragma unroll
-  for (int c = 0; c < 8; ++c) cp[c] = swap_sum32(swap_sum16(cp[c]));
-  if (stamps && blockIdx.x == 0 && tid == 0)
-    stamps[(long long)j * 16 + 15] = __builtin_amdgcn_s_memrealtime();
-  if (rg == 0) {
-#pragma unroll
-    for (int c = 0; c < 8; ++c) sh.cred[wave][8 * cg + c] = cp[c];
-  }
-  // this lane's row (cg < 4): row 4 R + cg of the half
-  const float myrow = cg == 0 ? rp[0] : (cg == 1 ? rp[1] : (cg == 2 ? rp[2] : rp[3]));
-  const float myx = cg == 0 ? xrv[0] : (cg == 1 ? xrv[1] : (cg == 2 ? xrv[2] : xrv[3]));
   AS1 float* const Pc = gptr(M.P) + cs * M.sP;
   const unsigned uld = (unsigned)M.ld;
-  double tp = 0.0;
-  if (DIAG) {
-    if (cg < 4) sh.rsum[4 * R + cg] = myrow;
-  } else if (cg < 4) {
-    Pc[(unsigned)(2 * K) * uld + rb + 4 * R + cg] = myrow;
-    tp = (double)myx * (double)myrow;
+  double tp[NH];
+#pragma unroll
+  for (int u = 0; u < NH; ++u) {
+    const int hr = hr0 + u;
+    const float xrv[4] = {xr[u].x, xr[u].y, xr[u].z, xr[u].w};
+    float rp[4], cp[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) cp[c] = 0.f;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const float av[8] = {a[u][rr][0].x, a[u][rr][0].y, a[u][rr][0].z, a[u][rr][0].w,
+                           a[u][rr][1].x, a[u][rr][1].y, a[u][rr][1].z, a[u][rr][1].w};
+      float acc = 0.f;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        if (DIAG) {      // upper triangle: row sums take col >= row, column sums col > row
+          const int lr = hr * HT + 4 * R + rr, lc = 8 * cg + c;
+          acc += (lc >= lr) ? av[c] * xcv[c] : 0.f;
+          cp[c] += (lc > lr) ? av[c] * xrv[rr] : 0.f;
+        } else {
+          acc += av[c] * xcv[c];
+          cp[c] += av[c] * xrv[rr];
+        }
+      }
+      rp[rr] = row16_sum(acc);
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) cp[c] = swap_sum32(swap_sum16(cp[c]));
+    if (rg == 0) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) sh.cred[u][wave][8 * cg + c] = cp[c];
+    }
+    // this lane's row (cg < 4): row 4 R + cg of the half
+    const float myrow = cg == 0 ? rp[0] : (cg == 1 ? rp[1] : (cg == 2 ? rp[2] : rp[3]));
+    const float myx = cg == 0 ? xrv[0] : (cg == 1 ? xrv[1] : (cg == 2 ? xrv[2] : xrv[3]));
+    tp[u] = 0.0;
+    if (DIAG) {
+      if (cg < 4) sh.rsum[u][4 * R + cg] = myrow;
+    } else if (cg < 4) {
+      Pc[(unsigned)(2 * K) * uld + I * TB + hr * HT + 4 * R + cg] = myrow;
+      tp[u] = (double)myx * (double)myrow;
+    }
   }
+  if (stamps && blockIdx.x == 0 && tid == 0)
+    stamps[(long long)j * 16 + 15] = __builtin_amdgcn_s_memrealtime();
   kfac_lds_barrier();
   if (tid < TB) {
-    float v = (sh.cred[0][tid] + sh.cred[1][tid]) + (sh.cred[2][tid] + sh.cred[3][tid]);
-    if (DIAG) {
-      const int rl = tid - hr * HT;
-      if (rl >= 0 && rl < HT) v += sh.rsum[rl];
-      Pc[(unsigned)(2 * I + hr) * uld + I * TB + tid] = v;
-    } else {
+#pragma unroll
+    for (int u = 0; u < NH; ++u) {
+      const int hr = hr0 + u;
+      float v = (sh.cred[u][0][tid] + sh.cred[u][1][tid]) + (sh.cred[u][2][tid] + sh.cred[u][3][tid]);
+      if (DIAG) {
+        const int rl = tid - hr * HT;
+        if (rl >= 0 && rl < HT) v += sh.rsum[u][rl];
+      }
       Pc[(unsigned)(2 * I + hr) * uld + K * TB + tid] = v;
+      tp[u] += (double)xcol * (double)v;
     }
-    tp += (double)xcol * (double)v;
   }
-  tp = wave_sum_d(tp);
-  if (lane == 0) sh.tred[wave] = tp;
+#pragma unroll
+  for (int u = 0; u < NH; ++u) {
+    const double t = wave_sum_d(tp[u]);
+    if (lane == 0) sh.tred[u][wave] = t;
+  }
   kfac_lds_barrier();
-  if (tid == 0)
-    gptr(M.TS)[cs * M.sTS + local] = (float)((sh.tred[0] + sh.tred[1]) + (sh.tred[2] + sh.tred[3]));
+  if (tid < NH)
+    gptr(M.TS)[cs * M.sTS + half0 + tid] =
+        (float)((sh.tred[tid][0] + sh.tred[tid][1]) + (sh.tred[tid][2] + sh.tred[tid][3]));
   if (stamps && blockIdx.x == 0 && tid == 0)
     stamps[(long long)j * 16 + 11] = __builtin_amdgcn_s_memrealtime();
 }
 
-// Workgroups 0 .. 2 ntri-1 of a matrix: half tiles (symv_half).  Workgroups
-// 2 ntri .. 2 ntri + nb - 1: row block b = s0 + (local - 2 ntri), the NK
+// Workgroups 0 .. nh / SNH - 1 of a matrix (nh half tiles): SNH half tiles
+// each (symv_halves).  Workgroups nh / SNH .. + nb - 1: row block b = s0 +
+// (local - nh / SNH), the NK
 // partial kinds of its 128 rows into DS (wave = 16 kinds, lane = row, fixed
 // order).
 __global__ __launch_bounds__(256) void red_symv_kernel(const RMat* __restrict__ mats,
@@ -604,7 +628,7 @@ __global__ __launch_bounds__(256) void red_symv_kernel(const RMat* __restrict__ 
   const int n = M.n, nt = M.nt;
   const long long ld = M.ld;
   const int s0 = (j + 1) / TB;
-  const int ntri = (nt - s0) * (nt - s0 + 1);          // tile halves
+  const int ntri = (nt - s0) * (nt - s0 + 1) / SNH;    // tile workgroups
   const int local = blockIdx.x - base;
   const int cs = j & 1;
   if (local >= ntri) {
@@ -652,14 +676,14 @@ __global__ __launch_bounds__(256) void red_symv_kernel(const RMat* __restrict__ 
   }
   if (stamps && blockIdx.x == 0 && tid == 0)
     stamps[(long long)j * 16 + 10] = __builtin_amdgcn_s_memrealtime();
-  const int hr = local & 1;
+  const int half0 = local * SNH;
   int I, K;
-  tri_index(local >> 1, nt - s0, I, K);
+  tri_index(half0 >> 1, nt - s0, I, K);
   I += s0; K += s0;
   if (I == K)
-    symv_half<true>(M, I, K, hr, cs, local, sred, j, stamps);
+    symv_halves<true, SNH>(M, I, K, half0 & 1, cs, half0, sred, j, stamps);
   else
-    symv_half<false>(M, I, K, hr, cs, local, sred, j, stamps);
+    symv_halves<false, SNH>(M, I, K, half0 & 1, cs, half0, sred, j, stamps);
 }
 
 // ------------------------------------------------------------------ host
@@ -682,7 +706,7 @@ void counts(int n, int j, int out[3]) {
   const int ntr = nt - (j + 1) / TB;
   out[0] = (j <= n - 1) ? nf - std::min(((j + 1) / TB) * (TB / FB), j / FB) : 0;
   out[1] = (j % NB == 0 && j > 0 && j <= n - 2) ? h_tri(ntr) : 0;
-  out[2] = (j <= n - 2) ? 2 * h_tri(ntr) + ntr : 0;
+  out[2] = (j <= n - 2) ? 2 * h_tri(ntr) / SNH + ntr : 0;
 }
 
 int rb_class(int blocks) {
