@@ -41,11 +41,25 @@ for b in fz.bufs:
     flops[2] += 2.0 * nG * nA * nG
     flops[3] += 2.0 * nG * nA * nA
 from distributed_kfac_pytorch_amd.ops import precond_fused as pf
-for cfg in [int(c) for c in os.environ.get('PGEMM_CFGS', '0,3,5,6,7').split(',')]:
+
+
+def outputs():
+    fz.run(damping=0.001)
+    torch.cuda.synchronize()
+    return [b.layer._pgrad_matrix().clone() for b in fz.bufs]
+
+
+pf.TILE_CFG = None
+fz._build_stage_tables()
+ref = outputs()
+for cfg in [int(c) for c in os.environ.get('PGEMM_CFGS', '0,3,5,6,7').split(',') if c]:
     pf.TILE_CFG = cfg
     fz._build_stage_tables()
     t = timeit(lambda: fz.run(damping=0.001))
-    print('tile cfg %d %s: chain %.3f ms' % (cfg, pf.TILE_SHAPES[cfg], t), flush=True)
+    err = max(((o - r).abs().max() / r.abs().max().clamp_min(1e-30)).item()
+              for o, r in zip(outputs(), ref))
+    print('tile cfg %d %s: chain %.3f ms  max rel diff vs default %.2e' % (
+        cfg, pf.TILE_SHAPES[cfg], t, err), flush=True)
 pf.TILE_CFG = int(os.environ['TILE_CFG']) if 'TILE_CFG' in os.environ else None
 fz._build_stage_tables()
 tot = timeit(lambda: fz.run(damping=0.001))
