@@ -28,9 +28,8 @@ FLAGS = ['-O3', '-std=c++17', '-fPIC', '--offload-arch=' + ARCH, '-munsafe-fp-at
          '-Wno-unused-result', '-mllvm', '-amdgpu-kernarg-preload-count=16']
 
 
-# rocSOLVER/rocBLAS: tridiagonal divide-and-conquer stage of the large-factor
-# eigensolver (csrc/eig_library.hip); everything else is hand-written.
-LIBS = ['-L/opt/rocm/lib', '-lrocsolver', '-lrocblas', '-Wl,-rpath,/opt/rocm/lib']
+# no vendor math library: every kernel is hand-written (the HIP runtime only)
+LIBS = []
 
 
 def sources():

@@ -269,6 +269,8 @@ struct CPlan {
   std::vector<int> grid[5], nact[5];
   int nbmax = 0, nm = 0;
   hipGraphExec_t exec = nullptr;
+  unsigned long long used = 0;      // LRU clock
+  bool pinned = false;              // enqueued into an outer capture: never evicted
 };
 
 int cdiv(int a, int b) { return (a + b - 1) / b; }
@@ -314,7 +316,11 @@ KFAC_API long long kfac_chol_ws_bytes(int n) {
 
 namespace {
 
-CPlan* plan_for(const KfacCholRecord* recs, int count, float damping, bool capture, int* err) {
+constexpr int kMaxPlans = 16;
+unsigned long long g_clock = 0;
+
+CPlan* plan_for(const KfacCholRecord* recs, int count, float damping, bool capture,
+                bool capturing, int* err) {
   std::vector<int> order(count);
   for (int i = 0; i < count; ++i) order[i] = i;
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return recs[a].n > recs[b].n; });
@@ -339,6 +345,25 @@ CPlan* plan_for(const KfacCholRecord* recs, int count, float damping, bool captu
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_plans.find(key);
   if (it == g_plans.end()) {
+    // the key holds the factor / output / workspace pointers and the damping:
+    // fresh snapshot buffers or a damping schedule make new keys, so the cache
+    // is bounded (LRU).  Eviction drains the device first (an evicted graph or
+    // table may still be in flight), never inside a stream capture.
+    if ((int)g_plans.size() >= kMaxPlans && !capturing) {
+      auto victim = g_plans.end();
+      for (auto v = g_plans.begin(); v != g_plans.end(); ++v)
+        if (!v->second.pinned && (victim == g_plans.end() || v->second.used < victim->second.used))
+          victim = v;
+      if (victim != g_plans.end()) {
+        (void)hipDeviceSynchronize();
+        CPlan& V = victim->second;
+        if (V.exec) (void)hipGraphExecDestroy(V.exec);
+        (void)hipFree(V.d_mats);
+        (void)hipFree(V.d_offs);
+        (void)hipFree(V.d_gemm);
+        g_plans.erase(victim);
+      }
+    }
     CPlan P;
     P.nm = (int)mats.size();
     P.nbmax = mats[0].nb;
@@ -399,6 +424,8 @@ CPlan* plan_for(const KfacCholRecord* recs, int count, float damping, bool captu
     it = g_plans.emplace(key, P).first;
   }
   CPlan* plan = &it->second;
+  plan->used = ++g_clock;
+  if (capturing) plan->pinned = true;
   if (capture && !plan->exec) {
     static hipStream_t cap = nullptr;
     if (!cap && hipStreamCreateWithFlags(&cap, hipStreamNonBlocking) != hipSuccess) cap = nullptr;
@@ -430,7 +457,7 @@ KFAC_API int kfac_chol_inverse_batched(const KfacCholRecord* recs, int count, fl
   if (hipStreamIsCapturing(stream, &cst) != hipSuccess) return -3;
   const bool graph = use_graph && stream != nullptr && cst == hipStreamCaptureStatusNone;
   int err = 0;
-  CPlan* plan = plan_for(recs, count, damping, graph, &err);
+  CPlan* plan = plan_for(recs, count, damping, graph, cst != hipStreamCaptureStatusNone, &err);
   if (!plan) return err ? err : -4;
   if (graph && plan->exec) return (int)hipGraphLaunch(plan->exec, stream);
   return enqueue(*plan, stream);

@@ -1,17 +1,12 @@
-// Tridiagonal-path eigensolver plumbing for large K-FAC factors.
+// Batched compact-WY back-transformation of the hand-written tridiagonal
+// eigensolver (reference semantics kfac/layers/utils.py:45-74:
+// the eigenvectors of a symmetric factor, eigenvalues ascending).
 //
-// Large factors (n > the LDS Jacobi limit) are solved by size class: every
-// factor of one n that the rank owns is stacked into ONE strided batch and
-// handed to rocSOLVER's divide-and-conquer driver (sytrd + stedc + ormtr) in
-// a single call, so the per-column panel latency of the tridiagonal reduction
-// (the dominant cost at these sizes: profiles/r1_rocsolver_variants.log) is
-// paid once per class instead of once per factor.  A rocblas handle is cached
-// per HIP stream; callers drive several classes concurrently on different
-// streams (ops/eigen.py).
-//
-// Reference semantics: kfac/layers/utils.py:45-74 (symeig, ascending
-// eigenvalues); the row-major <-> column-major flip is harmless for the
-// symmetric input and handled for the eigenvectors on the Python side.
+// Stage 3 of ops/eigen.py's fused path: after the ragged tridiagonal
+// reduction (csrc/eig_reduce.hip) and the batched divide and conquer
+// (csrc/eig_dc.hip), Z (eigenvectors of the tridiagonal matrices) becomes
+// Q Z.  Every GEMM is the grouped MFMA kernel of csrc/precond_gemm.hip; no
+// vendor library is linked.
 #include "pgemm.h"
 
 #include <cstring>
@@ -19,90 +14,10 @@
 #include <mutex>
 #include <tuple>
 #include <vector>
-#include <rocblas/rocblas.h>
-#include <rocsolver/rocsolver.h>
-
-namespace {
-
-std::mutex g_handle_mu;
-std::map<hipStream_t, rocblas_handle> g_handles;
-
-rocblas_handle handle_for(hipStream_t stream) {
-  std::lock_guard<std::mutex> lk(g_handle_mu);
-  auto it = g_handles.find(stream);
-  if (it != g_handles.end()) return it->second;
-  rocblas_handle h = nullptr;
-  if (rocblas_create_handle(&h) != rocblas_status_success) return nullptr;
-  rocblas_set_stream(h, stream);
-  g_handles[stream] = h;
-  return h;
-}
-
-}  // namespace
-
-// A: batch x n x n (symmetric, overwritten by eigenvectors: column-major
-// eigenvector k = row k of the row-major view), D: batch x n eigenvalues
-// (ascending), E: batch x n scratch, info: batch ints (device).
-KFAC_API int kfac_syevd_batched(float* A, int n, int batch, float* D, float* E, int* info,
-                                hipStream_t stream) {
-  rocblas_handle h = handle_for(stream);
-  if (!h) return -2;
-  const rocblas_stride nn = (rocblas_stride)n * n;
-  rocblas_status st;
-  if (batch == 1)
-    st = rocsolver_ssyevd(h, rocblas_evect_original, rocblas_fill_upper, n, A, n, D, E, info);
-  else
-    st = rocsolver_ssyevd_strided_batched(h, rocblas_evect_original, rocblas_fill_upper, n, A, n,
-                                          nn, D, n, E, n, info, batch);
-  return st == rocblas_status_success ? 0 : 1000 + (int)st;
-}
-
-// Tridiagonal divide and conquer only (for the hand-written reduction path):
-// D (n) diagonal, E (n) off-diagonal, C (n x n, column-major) receives the
-// eigenvectors of the tridiagonal matrix.
-KFAC_API int kfac_stedc(float* D, float* E, float* C, int n, int* info, hipStream_t stream) {
-  rocblas_handle h = handle_for(stream);
-  if (!h) return -2;
-  rocblas_status st = rocsolver_sstedc(h, rocblas_evect_tridiagonal, n, D, E, C, n, info);
-  return st == rocblas_status_success ? 0 : 1000 + (int)st;
-}
-
-// Householder tridiagonalisation only (strided batch, lower/upper per `lower`):
-// d, e (batch x n), tau (batch x n).  Pure kernel launches: capturable.
-KFAC_API int kfac_rocsolver_sytrd_batched(float* A, int n, int batch, float* D, float* E, float* tau,
-                                int lower, hipStream_t stream) {
-  rocblas_handle h = handle_for(stream);
-  if (!h) return -2;
-  const rocblas_stride nn = (rocblas_stride)n * n;
-  rocblas_status st = rocsolver_ssytrd_strided_batched(
-      h, lower ? rocblas_fill_lower : rocblas_fill_upper, n, A, n, nn, D, n, E, n, tau, n, batch);
-  return st == rocblas_status_success ? 0 : 1000 + (int)st;
-}
-
-// Tail of the hand-written reduction path (csrc/eig_tridiag.hip): for every
-// matrix of the batch, the tridiagonal divide and conquer (eigenvalues
-// ascending in d, tridiagonal eigenvectors into Z, column-major) and the
-// back-transformation Z <- Q Z with the reflectors left in A (LAPACK lower,
-// column-major == our row-major upper rows).
-KFAC_API int kfac_stedc_ormtr_batched(float* A, int lda, long long strideA, float* d, float* e,
-                                      float* tau, float* Z, int ldz, long long strideZ, int n,
-                                      int batch, int* info, hipStream_t stream) {
-  rocblas_handle h = handle_for(stream);
-  if (!h) return -2;
-  for (int b = 0; b < batch; ++b) {
-    rocblas_status st = rocsolver_sstedc(h, rocblas_evect_tridiagonal, n, d + (long long)b * n,
-                                         e + (long long)b * n, Z + b * strideZ, ldz, info + b);
-    if (st != rocblas_status_success) return 1000 + (int)st;
-    st = rocsolver_sormtr(h, rocblas_side_left, rocblas_fill_lower, rocblas_operation_none, n, n,
-                          A + b * strideA, lda, tau + (long long)b * n, Z + b * strideZ, ldz);
-    if (st != rocblas_status_success) return 2000 + (int)st;
-  }
-  return 0;
-}
 
 // ---------------------------------------------------------------------------
 // Batched blocked back-transformation Z <- Q Z for the hand-written reduction
-// (replaces one rocSOLVER ormtr call per matrix, 13 ms at n = 4608).
+// (round 1 called rocSOLVER ormtr per matrix: 13 ms at n = 4608).
 // Q = H_0 H_1 ... H_{n-2} is applied as compact-WY blocks of BT reflectors,
 // last block first:  Z[j0:, :] -= V_k (T_k (V_k^T Z[j0:, :])).  Every GEMM is
 // the grouped MFMA kernel of csrc/precond_gemm.hip (exact f32 MFMA) over all
@@ -127,15 +42,15 @@ constexpr int TILE_F32 = 0;   // pgemm 128 x 128 fp32, 4 waves (best since round
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 // Zero fill as a kernel (captured memset nodes misbehaved for multi-matrix
-// batches on ROCm 7.2: tests/test_gpu_eig_tridiag.py).
+// batches on ROCm 7.2).
 __global__ __launch_bounds__(256) void zero_kernel(float4* p, long long n4) {
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256)
     p[i] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 // Row j of the reduced matrix (== reflector j in column-major) made explicit:
-// zeros up to j, the implicit 1 at j+shift, v[1:] after (shift 1: one-stage
-// tridiagonalisation; 16: the band reduction of csrc/eig_sy2sb.hip).
+// zeros up to j, the implicit 1 at j+shift (shift 1: tridiagonalisation),
+// v[1:] after.
 __global__ __launch_bounds__(256) void make_v_kernel(float* A, int lda, long long sA, int n,
                                                      int shift) {
   float* row = A + blockIdx.y * sA + (long long)blockIdx.x * lda;
@@ -371,43 +286,4 @@ KFAC_API int kfac_backtransform_prepare(float* A, int lda, long long strideA, co
   const BtArgs a{A, lda, strideA, tau, Z, ldz, strideZ, n, batch, Tbuf, W1, W2, Vt, 1};
   int err = 0;
   return plan_for(a, &err) ? 0 : (err ? err : -4);
-}
-
-// Same, for reflectors that start `shift` rows below their index (the band
-// reduction's Q1: shift 16).
-KFAC_API int kfac_backtransform_shift(float* A, int lda, long long strideA, const float* tau,
-                                      float* Z, int ldz, long long strideZ, int n, int batch,
-                                      float* Tbuf, float* W1, float* W2, float* Vt, int shift,
-                                      int use_graph, hipStream_t stream) {
-  if (lda % 64 || ldz % 64 || lda != ldz || n < 2 || shift < 1) return -2;
-  const BtArgs a{A, lda, strideA, tau, Z, ldz, strideZ, n, batch, Tbuf, W1, W2, Vt, shift};
-  int err = 0;
-  BtPlan* plan = plan_for(a, &err);
-  if (!plan) return err ? err : -4;
-  if (use_graph && plan->exec) return (int)hipGraphLaunch(plan->exec, stream);
-  return run_plan(a, *plan, stream);
-}
-
-// Tridiagonal divide and conquer only, every matrix of the batch (eigenvalues
-// ascending in d, tridiagonal eigenvectors into Z, column-major).
-KFAC_API int kfac_stedc_batched(float* d, float* e, float* Z, int ldz, long long strideZ, int n,
-                                int batch, int* info, hipStream_t stream) {
-  rocblas_handle h = handle_for(stream);
-  if (!h) return -2;
-  for (int b = 0; b < batch; ++b) {
-    rocblas_status st = rocsolver_sstedc(h, rocblas_evect_tridiagonal, n, d + (long long)b * n,
-                                         e + (long long)b * n, Z + b * strideZ, ldz, info + b);
-    if (st != rocblas_status_success) return 1000 + (int)st;
-  }
-  return 0;
-}
-
-// C <- Q C with Q from kfac_sytrd_batched (single matrix).
-KFAC_API int kfac_ormtr(float* A, float* tau, float* C, int n, int lower, hipStream_t stream) {
-  rocblas_handle h = handle_for(stream);
-  if (!h) return -2;
-  rocblas_status st = rocsolver_sormtr(h, rocblas_side_left,
-                                       lower ? rocblas_fill_lower : rocblas_fill_upper,
-                                       rocblas_operation_none, n, n, A, n, tau, C, n);
-  return st == rocblas_status_success ? 0 : 1000 + (int)st;
 }

@@ -1,6 +1,7 @@
 // Batched symmetric tridiagonal divide-and-conquer eigensolver for gfx950
-// (replaces rocSOLVER's stedc behind the hand-written
-// tridiagonal reduction of csrc/eig_tridiag.hip).
+// (stage 2 of the hand-written eigensolver, between the
+// tridiagonal reduction of csrc/eig_reduce.hip and the back-transformation of
+// csrc/eig_backtransform.hip).
 //
 // Every matrix of an inverse update goes through ONE launch sequence: the
 // recursion trees of all matrices are processed level by level (all merges of

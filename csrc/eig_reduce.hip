@@ -35,7 +35,7 @@
 // exactly in scripts/models/sytrd_fused_model.py (fp64, 1e-15).  Storage:
 // row-major, UPPER triangle maintained; output d, e, tau and reflector j in
 // row j (beta at j+1, v[2:] after): the layout the compact-WY back-
-// transformation (csrc/eig_library.hip) reads.
+// transformation (csrc/eig_backtransform.hip) reads.
 #include "common.h"
 
 #include <algorithm>

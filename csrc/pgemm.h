@@ -1,6 +1,6 @@
 // Grouped "NT" GEMM records shared by the preconditioning chain
 // (csrc/precond_gemm.hip) and the eigensolver back-transformation
-// (csrc/eig_library.hip).  Host mirrors: ops/precond_fused.py (layout sizes
+// (csrc/eig_backtransform.hip).  Host mirrors: ops/precond_fused.py (layout sizes
 // are checked at load through kfac_*_record_size).
 #pragma once
 #include "common.h"

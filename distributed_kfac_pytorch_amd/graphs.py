@@ -133,6 +133,7 @@ class GraphedTrainStep(object):
         self._warm = {}
         self.replays = 0
         self.eager_steps = 0
+        self._plan_gen = None
         # warm-up and capture share one side stream, so the autograd
         # AccumulateGrad nodes created in warm-up live on the capture stream
         # (`stream`: reuse another GraphedTrainStep's, for the same model)
@@ -213,7 +214,20 @@ class GraphedTrainStep(object):
         if kind == 'factor' and self.pre is not None and hasattr(self.pre, 'step_factor_comm'):
             self.pre.step_factor_comm()
 
+    def _purge_stale_plans(self):
+        """A re-plan (KFAC._assign_workers) moved every buffer the captured
+        graphs address: drop graphs of older plan generations (their keys can
+        never match again) so their memory pools are released."""
+        gen = getattr(self.pre, 'plan_generation', 0) if self.pre is not None else 0
+        if gen == self._plan_gen:
+            return
+        self._plan_gen = gen
+        for d in (self.graphs, self.outputs, self._warm):
+            for k in [k for k in d if k[2] and k[2][-1][-1] != gen]:
+                del d[k]
+
     def __call__(self):
+        self._purge_stale_plans()
         kind = self._kind()
         if self.enabled and kind == 'eager' and self._inverse_fb_graphed():
             self.eager_steps += 1

@@ -409,12 +409,29 @@ class KFACLayer(object):
         gs = [g for g, _ in outputs]
         srcs = self._g_sources(gs)
         keep = None
+        fins = []
         for s, (g, sc) in zip(srcs, outputs):
             fin = torch.isfinite(g).all().reshape(1)
             sc = sc if torch.is_tensor(sc) else torch.full((1,), float(sc), device=g.device)
             s.dscale = torch.where(fin, 1.0 / (sc * sc), torch.zeros_like(sc))
             keep = fin if keep is None else (keep | fin)
+            fins.append(fin)
+        rows = [self._g_rows(g) for g in gs]
+        if len(gs) > 1 and rows[0] is not None:
+            # the sources share one 1/total normalisation (all rows); the
+            # reference averages over the KEPT rows only, so rescale by
+            # total / kept on the device (no host read; 0 kept -> keep = 0)
+            total = float(sum(rows))
+            kept = sum(f.float() * float(r) for f, r in zip(fins, rows))
+            renorm = total / torch.clamp(kept, min=1.0)
+            for s in srcs:
+                s.dscale = s.dscale * renorm
         return srcs, self._factor_out_dtype(gs[0]), keep.float()
+
+    def _g_rows(self, g):
+        """Rows source `g` contributes to the shared normalisation of the G
+        factor, or None when every source is normalised on its own."""
+        return None
 
     def _take_g_outputs(self):
         outputs, self.g_outputs = self.g_outputs, []

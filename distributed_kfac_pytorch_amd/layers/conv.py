@@ -95,3 +95,6 @@ class Conv2dLayer(KFACLayer):
             spatial = g.shape[2] * g.shape[3]
             s.scale = 1.0 / (float(spatial) ** 2 * total)
         return srcs
+
+    def _g_rows(self, g):
+        return g.shape[0] * g.shape[2] * g.shape[3]

@@ -48,6 +48,9 @@ class LinearLayer(KFACLayer):
     def _g_sources(self, g_outputs):
         return self._sources(g_outputs, False)
 
+    def _g_rows(self, g):
+        return _rows2d(g).shape[0]
+
 
 class LinearMultiLayer(LinearLayer):
     """Linear module invoked several times per step (e.g. per RNN time step)."""
@@ -74,3 +77,6 @@ class LinearMultiLayer(LinearLayer):
             s.scale = 1.0 / m.shape[0]
             srcs.append(s)
         return srcs
+
+    def _g_rows(self, g):
+        return None     # each time step's covariance is normalised on its own

@@ -57,36 +57,7 @@ class DcRecord(ctypes.Structure):
                 ('ws', c_vp), ('n', c_ll)]
 
 
-class SbRecord(ctypes.Structure):
-    # csrc/eig_sb2st.hip KfacSbRecord
-    _fields_ = [('band', c_vp), ('v2', c_vp), ('d', c_vp), ('e', c_vp), ('prog', c_vp),
-                ('n', c_ll), ('ldv2', c_ll)]
-
-
-class S1Record(ctypes.Structure):
-    # csrc/eig_sy2sb.hip KfacS1Record
-    _fields_ = [('A', c_vp), ('lda', c_ll), ('tau', c_vp), ('ws', c_vp), ('band', c_vp),
-                ('n', c_ll)]
-
-
-class Q2Record(ctypes.Structure):
-    # csrc/eig_q2.hip KfacQ2Record
-    _fields_ = [('v2', c_vp), ('ldv2', c_ll), ('Z', c_vp), ('ldz', c_ll), ('T', c_vp),
-                ('n', c_ll)]
-
-
 _SIGS = {
-    'kfac_sy2sb_batched': [ctypes.POINTER(S1Record), c_int, c_int, c_vp],
-    'kfac_sy2sb_ws_floats': [c_int],
-    'kfac_q2_batched': [ctypes.POINTER(Q2Record), c_int, c_int, c_vp],
-    'kfac_q2_t_floats': [c_int],
-    'kfac_backtransform_shift': [c_vp, c_int, c_ll, c_vp, c_vp, c_int, c_ll, c_int, c_int, c_vp,
-                                 c_vp, c_vp, c_vp, c_int, c_int, c_vp],
-    'kfac_sb2st_batched': [ctypes.POINTER(SbRecord), c_int, c_vp, c_vp],
-    'kfac_sb2st_bw': [],
-    'kfac_sb2st_stamps': [c_vp, c_int],
-    'kfac_sb2st_ldv2': [c_int],
-    'kfac_sb2st_nwg': [c_int],
     'kfac_syrk_patch': [c_int, c_vp, c_ll, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_int, c_int,
                         c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_vp, c_int,
                         c_int, c_vp, c_vp, c_vp],
@@ -120,21 +91,10 @@ _SIGS = {
     'kfac_hadamard': [c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_f, c_int, c_vp],
     'kfac_eig_jacobi_small': [ctypes.POINTER(EigRecord), c_int, c_int, c_f, c_int, c_f, c_vp],
     'kfac_max_small_eig_n': [],
-    'kfac_syevd_batched': [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp],
-    'kfac_stedc': [c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
-    'kfac_rocsolver_sytrd_batched': [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp],
-    'kfac_sytrd_batched': [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp],
-    'kfac_sytrd_forget': [c_vp],
-    'kfac_sytrd_prepare': [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp],
-    'kfac_sytrd_ws_floats': [c_int],
-    'kfac_stedc_batched': [c_vp, c_vp, c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp],
     'kfac_tridiag_backtransform': [c_vp, c_int, c_ll, c_vp, c_vp, c_int, c_ll, c_int, c_int,
                                    c_vp, c_vp, c_vp, c_vp, c_int, c_vp],
     'kfac_backtransform_prepare': [c_vp, c_int, c_ll, c_vp, c_vp, c_int, c_ll, c_int, c_int,
                                    c_vp, c_vp, c_vp, c_vp],
-    'kfac_stedc_ormtr_batched': [c_vp, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_int,
-                                 c_int, c_vp, c_vp],
-    'kfac_ormtr': [c_vp, c_vp, c_vp, c_int, c_int, c_vp],
     'kfac_pgemm': [c_int, c_int, c_vp, c_int, c_int, c_vp, c_vp],
     'kfac_kl_finalize': [c_vp, c_int, c_vp, c_vp],
     'kfac_kl_elems_per_block': [],
@@ -160,12 +120,11 @@ _SIGS = {
 }
 
 
-_RESTYPES = {'kfac_sytrd_ws_floats': c_ll, 'kfac_sytrd_forget': None, 'kfac_dc_ws_bytes': c_ll,
+_RESTYPES = {'kfac_dc_ws_bytes': c_ll,
              'kfac_reduce_ws_floats': c_ll, 'kfac_syrk_splits': c_ll,
              'kfac_chol_ws_bytes': c_ll, 'kfac_chol_info_offset': c_ll,
              'kfac_syrk_problem_set_part': None, 'kfac_syrk_problem_set_dscale': None,
-             'kfac_bn_ws_floats': c_ll, 'kfac_sb2st_ldv2': c_ll,
-             'kfac_sy2sb_ws_floats': c_ll, 'kfac_q2_t_floats': c_ll}
+             'kfac_bn_ws_floats': c_ll}
 
 
 def _load():

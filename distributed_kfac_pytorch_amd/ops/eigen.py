@@ -1,22 +1,14 @@
 """Symmetric eigendecomposition / damped inverse of Kronecker factors (K6, K9).
 
-GPU path (MI355X), LARGE_PATH = 'fused' (default): every factor of the step
-(any size up to FUSED_MAX_N) in ONE ragged launch sequence per stage: the
-fused tridiagonal reduction (csrc/eig_reduce.hip), the batched divide and
-conquer (csrc/eig_dc.hip), the compact-WY back-transformation.
-Per-class paths (opt-in, round 1):
-  * n <= 192: every such factor of the step is solved by ONE launch of the
-    batched LDS Jacobi kernel (csrc/eig_jacobi.hip), one workgroup per matrix.
-  * larger n: grouped by size class; classes run concurrently on a pool of
-    side streams.  LARGE_PATH selects the solver of a class ('auto':
-    'tridiag' for n >= TRIDIAG_MIN_N, else 'syevd'):
-      'tridiag'  the hand-written blocked Householder reduction
-                 (csrc/eig_tridiag.hip: 3 launches per column for the whole
-                 class, captured into one hipGraph) + rocSOLVER's tridiagonal
-                 divide and conquer and back-transformation per matrix
-      'syevd'    one strided-batched rocSOLVER syevd call per class, whose
-                 reduction is latency bound per column
-                 (profiles/r1_rocsolver_fill_split.log)
+GPU path (MI355X), hand-written end to end (no vendor solver is linked):
+every factor of the step (any size from 2 up to FUSED_MAX_N) goes through
+ONE ragged launch sequence per stage -- the fused tridiagonal reduction
+(csrc/eig_reduce.hip), the batched divide and conquer (csrc/eig_dc.hip) and
+the compact-WY back-transformation (csrc/eig_backtransform.hip) -- split
+over two streams by size (_fused_groups).  1x1 factors, and the opt-in
+solver='jacobi' for n <= SMALL_N, use the batched LDS Jacobi kernel
+(csrc/eig_jacobi.hip).  Factors above FUSED_MAX_N (a 16384^2 fp32 factor is
+1 GiB) are refused on the GPU.
 CPU path: torch.linalg.eigh (the reference semantics, kfac/layers/utils.py:45-74).
 
 Results: ascending eigenvalues clipped at `clip` (reference default 0.0),
@@ -31,24 +23,8 @@ from . import _lib
 __all__ = ['symeig_many', 'inverse_many', 'SMALL_N']
 
 SMALL_N = 192
-# 'fused' (default): every large factor through ONE ragged fused reduction, ONE
-# batched divide and conquer and the WY back-transformation (no library
-# solver); 'auto' / 'tridiag' / 'syevd': the per-size-class paths of round 1
-LARGE_PATH = os.environ.get('KFAC_EIG_LARGE', 'fused')
-FUSED_MAX_N = 16384   # csrc/eig_reduce.hip NMAX (larger factors: per-class path)
-# 'auto': the hand-written path from this n up (it wins from 2048 on, rocSOLVER
-# syevd's latency per column wins below: profiles/r1_tridiag_vs_syevd.log)
-TRIDIAG_MIN_N = int(os.environ.get('KFAC_TRIDIAG_MIN_N', '2048'))
-TRIDIAG_GRAPH = bool(int(os.environ.get('KFAC_TRIDIAG_GRAPH', '1')))
-TRIDIAG_BACK = os.environ.get('KFAC_TRIDIAG_BACK', 'wy')   # 'wy' (batched GEMMs) | 'ormtr'
-# tridiagonal eigensolver: 'dc' = the hand-written batched divide and conquer
-# (csrc/eig_dc.hip), 'stedc' = rocSOLVER (A/B comparisons only)
-TRIDIAG_SOLVER = os.environ.get('KFAC_TRIDIAG_SOLVER', 'dc')
-BT = 128   # back-transformation block (csrc/eig_library.hip)
-# size classes from this n up are solved as concurrent single-matrix jobs
-# (default: never; rocSOLVER syevd batches beat concurrent singles,
-# r1_eigh_split.log; KFAC_EIG_SPLIT_N re-evaluates it for the tridiag path)
-SPLIT_N = int(os.environ.get('KFAC_EIG_SPLIT_N', str(1 << 30)))
+FUSED_MAX_N = 16384   # csrc/eig_reduce.hip NMAX
+BT = 128   # back-transformation block (csrc/eig_backtransform.hip)
 _streams = {}
 
 
@@ -88,40 +64,6 @@ def _jacobi_small(mats, clip, max_sweeps=30, tol=1e-7):
     return outs
 
 
-_pool = None
-
-
-def _thread_pool(k):
-    global _pool
-    if _pool is None or _pool._max_workers < k:
-        import concurrent.futures
-        _pool = concurrent.futures.ThreadPoolExecutor(k, thread_name_prefix='kfac-eigh')
-    return _pool
-
-
-def _syevd_class(mats, clip, stream):
-    """Every matrix of one size n in ONE strided-batched divide-and-conquer
-    call (csrc/eig_library.hip) on `stream`."""
-    n = mats[0].shape[0]
-    dev = mats[0].device
-    with torch.cuda.stream(stream):
-        A = torch.stack(mats) if len(mats) > 1 else mats[0].clone().unsqueeze(0)
-        b = A.shape[0]
-        D = torch.empty(b, n, dtype=torch.float32, device=dev)
-        E = torch.empty(b, n, dtype=torch.float32, device=dev)
-        info = torch.empty(b, dtype=torch.int32, device=dev)
-        _lib.check(_lib.lib().kfac_syevd_batched(_lib.ptr(A), n, b, _lib.ptr(D), _lib.ptr(E),
-                                                  _lib.ptr(info), _lib.c_vp(stream.cuda_stream)),
-                   'kfac_syevd_batched')
-        _INFOS.append(info)
-        del _INFOS[:-256]   # bounded when nobody checks
-        # column-major eigenvector k == row k of the row-major view
-        Q = A.transpose(1, 2).contiguous()
-        if clip is not None:
-            D.clamp_(min=clip)
-    return [(Q[i], D[i]) for i in range(b)]
-
-
 _INFOS = []
 _TRI_BUFS = {}
 
@@ -139,7 +81,6 @@ def _tri_buffers(dev, n, b, slot=0):
         # tiles, zero past n (its symv tiles read whole tiles unmasked; the
         # MFMA GEMMs of the back-transformation step k by 64)
         lda = (n + 127) // 128 * 128
-        wsf = int(L.kfac_sytrd_ws_floats(n))
         f32 = dict(dtype=torch.float32, device=dev)
         nblk = (n + BT - 1) // BT
         wsb = int(L.kfac_dc_ws_bytes(n))
@@ -149,65 +90,13 @@ def _tri_buffers(dev, n, b, slot=0):
                     w=torch.zeros(b, n, **f32), wsb=wsb,
                     dcws=torch.zeros(b * wsb, dtype=torch.uint8, device=dev),
                     rwsf=rwsf, rws=torch.zeros(b * rwsf, **f32),
-                    tau=torch.zeros(b, n, **f32), ws=torch.zeros(b * wsf, **f32),
+                    tau=torch.zeros(b, n, **f32),
                     info=torch.zeros(b, dtype=torch.int32, device=dev),
                     T=torch.zeros(2 * b * nblk * BT * BT, **f32),
                     W1=torch.zeros(b * BT * n, **f32), W2=torch.zeros(b * BT * n, **f32),
                     Vt=torch.zeros(b * BT * lda, **f32))
         _TRI_BUFS[key] = bufs
     return bufs
-
-
-def _tridiag_class(mats, clip, stream, use_graph=None, slot=0):
-    """Every matrix of one size n: hand-written blocked tridiagonalisation
-    (csrc/eig_tridiag.hip), rocSOLVER's tridiagonal divide and conquer per
-    matrix, then the batched compact-WY back-transformation (three strided-
-    batched GEMMs per 128 reflectors for the whole class), on `stream`."""
-    n = mats[0].shape[0]
-    b = len(mats)
-    dev = mats[0].device
-    L = _lib.lib()
-    if use_graph is None:
-        use_graph = TRIDIAG_GRAPH
-    with torch.cuda.stream(stream):
-        B = _tri_buffers(dev, n, b, slot)
-        lda = B['lda']
-        for i, A in enumerate(mats):
-            B['A'][i, :n, :n].copy_(A)
-        sA = B['sA']
-        cs = _lib.c_vp(stream.cuda_stream)
-        _lib.check(L.kfac_sytrd_batched(_lib.ptr(B['A']), lda, sA, n, b, _lib.ptr(B['d']),
-                                        _lib.ptr(B['e']), _lib.ptr(B['tau']), _lib.ptr(B['ws']),
-                                        int(use_graph), cs), 'kfac_sytrd_batched')
-        if TRIDIAG_BACK == 'ormtr':
-            _lib.check(L.kfac_stedc_ormtr_batched(_lib.ptr(B['A']), lda, sA, _lib.ptr(B['d']),
-                                                  _lib.ptr(B['e']), _lib.ptr(B['tau']),
-                                                  _lib.ptr(B['Z']), lda, sA, n, b,
-                                                  _lib.ptr(B['info']), cs),
-                       'kfac_stedc_ormtr_batched')
-            D = B['d'].clone()
-            _INFOS.append(B['info'].clone())
-        elif TRIDIAG_SOLVER == 'stedc':
-            _lib.check(L.kfac_stedc_batched(_lib.ptr(B['d']), _lib.ptr(B['e']), _lib.ptr(B['Z']),
-                                            lda, sA, n, b, _lib.ptr(B['info']), cs),
-                       'kfac_stedc_batched')
-            _lib.check(L.kfac_tridiag_backtransform(*_bt_args(B, n, b), int(use_graph), cs),
-                       'kfac_tridiag_backtransform')
-            D = B['d'].clone()
-            _INFOS.append(B['info'].clone())
-        else:
-            _lib.check(L.kfac_dc_batched(_dc_records(B, n, b), b, int(use_graph), cs),
-                       'kfac_dc_batched')
-            _lib.check(L.kfac_tridiag_backtransform(*_bt_args(B, n, b), int(use_graph), cs),
-                       'kfac_tridiag_backtransform')
-            D = B['w'].clone()
-            _INFOS.append(_dc_info(B, n, b))
-        del _INFOS[:-256]
-        # column-major eigenvector k (row k of Z) -> column k of a row-major Q
-        Q = B['Z'][:, :, :n].transpose(1, 2).contiguous()
-        if clip is not None:
-            D.clamp_(min=clip)
-    return [(Q[i], D[i]) for i in range(b)]
 
 
 def _dc_records(B, n, b):
@@ -273,22 +162,6 @@ def _bt_args(B, n, b):
             n, b, _lib.ptr(B['T']), _lib.ptr(B['W1']), _lib.ptr(B['W2']), _lib.ptr(B['Vt']))
 
 
-def _tridiag_prepare(n, b, dev, slot=0):
-    """Allocate the class buffers and build its reduction hipGraph now, from
-    the calling thread, before concurrent class solves start: a capture must
-    not overlap other threads' library calls (hipBLASLt inside rocBLAS)."""
-    B = _tri_buffers(dev, n, b, slot)
-    lda = B['lda']
-    _lib.check(_lib.lib().kfac_sytrd_prepare(_lib.ptr(B['A']), lda, B['sA'], n, b,
-                                             _lib.ptr(B['d']), _lib.ptr(B['e']),
-                                             _lib.ptr(B['tau']), _lib.ptr(B['ws'])),
-               'kfac_sytrd_prepare')
-    _lib.check(_lib.lib().kfac_backtransform_prepare(*_bt_args(B, n, b)),
-               'kfac_backtransform_prepare')
-    if TRIDIAG_SOLVER == 'dc':
-        _lib.check(_lib.lib().kfac_dc_prepare(_dc_records(B, n, b), b), 'kfac_dc_prepare')
-
-
 def _fused_groups(mats):
     """Split the batch over concurrent streams.  The reduction is a chain of
     n columns per matrix, latency bound with few workgroups: the largest
@@ -313,9 +186,6 @@ def _fused_groups(mats):
 
 
 FUSED_STREAMS = int(os.environ.get('KFAC_EIG_FUSED_STREAMS', '2'))
-# two-stage solver (dense -> band -> tridiagonal, ops/eig2s.py) instead of the
-# one-stage fused reduction
-TWO_STAGE = bool(int(os.environ.get('KFAC_EIG_TWO_STAGE', '0')))
 FUSED_SPLIT = bool(int(os.environ.get('KFAC_EIG_FUSED_SPLIT', '1')))
 
 
@@ -324,7 +194,7 @@ def _large_fused(mats, clip, stream, use_graph=True):
     group (_fused_groups) the fused one-launch-per-column reduction over all
     its matrices (csrc/eig_reduce.hip), the batched divide and conquer over
     all its matrices (csrc/eig_dc.hip), then the compact-WY back-
-    transformation per size class (csrc/eig_library.hip); every further group
+    transformation per size class (csrc/eig_backtransform.hip); every further group
     on a side stream.  No library solver, no host round trip; each stage is
     a cached hipGraph.
 
@@ -353,11 +223,7 @@ def _large_fused(mats, clip, stream, use_graph=True):
 
     def run(slot):
         g, st = groups[slot], streams[slot]
-        solve = _fused_group
-        if TWO_STAGE:
-            from . import eig2s
-            solve = eig2s.two_stage_group
-        for i, r in zip(g, solve([mats[i] for i in g], clip, st, use_graph, slot)):
+        for i, r in zip(g, _fused_group([mats[i] for i in g], clip, st, use_graph, slot)):
             outs[i] = r
 
     key = (str(dev), use_graph, tuple(tuple(mats[i].shape[0] for i in g) for g in groups))
@@ -464,12 +330,6 @@ def _fused_group(mats, clip, stream, use_graph, slot=0):
     return outs
 
 
-def _class_solver(n):
-    if LARGE_PATH == 'tridiag' or (LARGE_PATH == 'auto' and n >= TRIDIAG_MIN_N):
-        return _tridiag_class
-    return _syevd_class
-
-
 def check_solver_status():
     """Host-side check of every divide-and-conquer call issued since the last
     check (info != 0 -> the solver did not converge).  Syncs; call once per
@@ -479,99 +339,6 @@ def check_solver_status():
     bad = [int(i.abs().max().item()) for i in infos if (i != 0).any().item()]
     if bad:
         raise RuntimeError('symmetric eigensolver failed to converge (info={})'.format(bad))
-
-
-def eigh_workers():
-    """Concurrent solver streams; each needs a HW queue to really overlap, so
-    the default follows GPU_MAX_HW_QUEUES (HIP's default 4)."""
-    env = os.environ.get('KFAC_EIGH_WORKERS')
-    if env:
-        return max(1, int(env))
-    return max(1, min(16, int(os.environ.get('GPU_MAX_HW_QUEUES', '4'))))
-
-
-def _jobs(mats):
-    """Size classes; large classes are split into single-matrix jobs (a
-    strided batch of big matrices is nearly serial: r1_rocsolver_variants.log
-    n=4608 x3 228 ms vs 124 ms for one), small ones stay batched."""
-    classes = {}
-    for i, A in enumerate(mats):
-        classes.setdefault(A.shape[0], []).append(i)
-    jobs = []
-    for n, idx in classes.items():
-        if n >= SPLIT_N:
-            jobs += [[i] for i in idx]
-        else:
-            jobs.append(idx)
-    jobs.sort(key=lambda j: -(mats[j[0]].shape[0] ** 3) * (1.0 + 0.3 * (len(j) - 1)))
-    return jobs
-
-
-def _library_eigh(mats, clip, n_workers=None):
-    """Large factors as divide-and-conquer jobs (one strided batch per small
-    size class, one call per big matrix) spread over `n_workers` host threads,
-    each with its own HIP stream: the tridiagonal reduction is panel-latency
-    bound, so independent jobs overlap almost perfectly as long as each stream
-    has its own hardware queue.  The caller's stream is ordered before and
-    after."""
-    if n_workers is None:
-        n_workers = eigh_workers()
-    dev = mats[0].device
-    jobs = _jobs(mats)
-    outs = [None] * len(mats)
-    if n_workers <= 1:
-        cur = torch.cuda.current_stream(dev)
-        for idx in jobs:
-            solve = _class_solver(mats[idx[0]].shape[0])
-            for i, r in zip(idx, solve([mats[i] for i in idx], clip, cur)):
-                outs[i] = r
-        return outs
-    cur = torch.cuda.current_stream(dev)
-    # jobs of one (n, b) run concurrently on distinct buffer slots
-    slot, seen = {}, {}
-    for j, idx in enumerate(jobs):
-        key = (mats[idx[0]].shape[0], len(idx))
-        slot[j] = seen.get(key, 0)
-        seen[key] = slot[j] + 1
-    for j, idx in enumerate(jobs):
-        n = mats[idx[0]].shape[0]
-        if _class_solver(n) is _tridiag_class and TRIDIAG_GRAPH:
-            _tridiag_prepare(n, len(idx), dev, slot[j])
-    k = min(n_workers, len(jobs))
-    pool = _side_streams(dev, k)
-    for s in pool:
-        s.wait_stream(cur)
-    # greedy LPT of the jobs over the workers (cost ~ n^3, a batch nearly free)
-    load = [0.0] * k
-    assign = [[] for _ in range(k)]
-    for jb, idx in enumerate(jobs):
-        j = min(range(k), key=lambda w: load[w])
-        assign[j].append((jb, idx))
-        load[j] += float(mats[idx[0]].shape[0]) ** 3 * (1.0 + 0.3 * (len(idx) - 1))
-
-    def solve(jb, idx, stream):
-        fn = _class_solver(mats[idx[0]].shape[0])
-        sub = [mats[i] for i in idx]
-        if fn is _tridiag_class:
-            return fn(sub, clip, stream, slot=slot[jb])
-        return fn(sub, clip, stream)
-
-    def work(j):
-        torch.cuda.set_device(dev)
-        return [(idx, solve(jb, idx, pool[j])) for jb, idx in assign[j]]
-
-    for res in _thread_pool(k).map(work, range(k)):
-        for idx, rs in res:
-            for i, r in zip(idx, rs):
-                outs[i] = r
-    for j, s in enumerate(pool[:k]):
-        cur.wait_stream(s)
-        for _, idx in assign[j]:
-            for i in idx:
-                mats[i].record_stream(s)
-                outs[i][0].record_stream(cur)
-                outs[i][1].record_stream(cur)
-    return outs
 
 
 def symeig_many(mats, clip=0.0, solver='auto'):
@@ -587,32 +354,31 @@ def symeig_many(mats, clip=0.0, solver='auto'):
                 d = torch.clamp(d, min=clip)
             outs.append((Q, d))
         return outs
-    _lib.check_pgemm_extent(max(A.shape[0] for A in mats))
-    # fused default: EVERY factor rides the ragged launch sequence (a small
-    # factor's reduction columns run alongside the big ones', its divide and
-    # conquer is one or two levels); the batched LDS Jacobi is the small-n
-    # solver of the per-class paths (its latency is the slowest matrix's:
+    nmax = max(A.shape[0] for A in mats)
+    if nmax > FUSED_MAX_N:
+        raise ValueError('factor of size {} exceeds the GPU eigensolver limit {} '
+                         '(csrc/eig_reduce.hip NMAX)'.format(nmax, FUSED_MAX_N))
+    if solver not in ('auto', 'jacobi'):
+        raise ValueError("solver must be 'auto' or 'jacobi', got {!r}".format(solver))
+    _lib.check_pgemm_extent(nmax)
+    # EVERY factor rides the fused ragged launch sequence (a small factor's
+    # reduction columns run alongside the big ones', its divide and conquer is
+    # one or two levels); the batched LDS Jacobi takes 1x1 factors, and every
+    # n <= SMALL_N with solver='jacobi' (its latency is the slowest matrix's:
     # ~40 ms for ResNet-50's 64..192 factors, profiles/r2_eig_kernel_stats.txt)
-    fused_all = (LARGE_PATH == 'fused' and solver == 'auto'
-                 and max(A.shape[0] for A in mats) <= FUSED_MAX_N)
-    small = [i for i, A in enumerate(mats)
-             if (A.shape[0] < 2 if fused_all else A.shape[0] <= SMALL_N)
-             and solver in ('auto', 'jacobi', 'serial')]
-    large = [i for i in range(len(mats)) if i not in set(small)]
+    lim = SMALL_N if solver == 'jacobi' else 1
+    small = [i for i, A in enumerate(mats) if A.shape[0] <= lim]
+    large = [i for i, A in enumerate(mats) if A.shape[0] > lim]
     outs = [None] * len(mats)
     if small:
         for i, r in zip(small, _jacobi_small([mats[i] for i in small], clip)):
             outs[i] = r
     if large:
         sub = [mats[i] for i in large]
-        if LARGE_PATH == 'fused' and max(A.shape[0] for A in sub) <= FUSED_MAX_N:
-            cur = torch.cuda.current_stream(sub[0].device)
-            res = _large_fused(sub, clip, cur)
-            for A in sub:
-                A.record_stream(cur)
-        else:
-            workers = 1 if solver == 'serial' else None
-            res = _library_eigh(sub, clip, workers)
+        cur = torch.cuda.current_stream(sub[0].device)
+        res = _large_fused(sub, clip, cur)
+        for A in sub:
+            A.record_stream(cur)
         for i, r in zip(large, res):
             outs[i] = r
     return outs

@@ -419,7 +419,7 @@ class SplitFused(object):
         self.precision = precision
         self._side = None
         self._top_kl = None
-        self._launched = False
+        self._launched = None      # tag of the pending early launch, or None
         self.early_launches = 0
         self.kl_sum = torch.zeros((), dtype=torch.float64, device=self.device)
 
@@ -436,33 +436,47 @@ class SplitFused(object):
         return self.top._stage_tables
 
     def refresh_eigen(self):
+        self._join_side()
+        self._launched = None      # an early result from the old eigenbasis is stale
         self.bottom.refresh_eigen()
         self.top.refresh_eigen()
+
+    def _join_side(self):
+        if self._side is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
 
     def _side_stream(self):
         if self._side is None:
             self._side = torch.cuda.Stream(device=self.device)
         return self._side
 
-    def launch_top(self, damping=0.0, with_kl=True):
+    def launch_top(self, damping=0.0, with_kl=True, tag=None):
         """Precondition the top layers on the side stream (called from the
-        hook that sees the last top-layer gradient accumulated)."""
+        hook that sees the last top-layer gradient accumulated).  `tag`
+        identifies the step / eigenbasis the launch belongs to: run() reuses
+        the result only under the same tag."""
         cur = torch.cuda.current_stream(self.device)
         side = self._side_stream()
         side.wait_stream(cur)
         with torch.cuda.stream(side):
             self._top_kl = self.top.run(damping=damping, with_kl=with_kl)
-        self._launched = True
+        self._launched = (tag, float(damping), bool(with_kl))
         self.early_launches += 1
 
-    def run(self, damping=0.0, with_kl=True):
+    def run(self, damping=0.0, with_kl=True, tag=None):
         cur = torch.cuda.current_stream(self.device)
-        if not self._launched:
+        early = self._launched
+        self._launched = None
+        reuse = early is not None and early == (tag, float(damping), bool(with_kl))
+        if early is not None and not reuse:
+            # a launch from another step (a backward without KFAC.step()) or
+            # another eigenbasis: drain it, then precondition afresh
+            cur.wait_stream(self._side)
+        if not reuse:
             self._top_kl = self.top.run(damping=damping, with_kl=with_kl)
         klb = self.bottom.run(damping=damping, with_kl=with_kl)
-        if self._launched:
+        if reuse:
             cur.wait_stream(self._side)
-        self._launched = False
         if not with_kl:
             return None
         torch.add(klb, self._top_kl, out=self.kl_sum)

@@ -250,6 +250,7 @@ class KFAC(optim.Optimizer):
         self.overlap_precondition = bool(overlap_precondition)
         self._top_hooks = []
         self._top_seen = 0
+        self._eigen_gen = 0         # bumped whenever new eigendata is in place
         # all factors of a step in a few grouped launches (GPU)
         self.grouped_factors = True
         self.fused = None
@@ -483,7 +484,15 @@ class KFAC(optim.Optimizer):
         p = self.param_groups[0]
         return (isinstance(self.fused, precond_fused.SplitFused) and self._have_inverses
                 and self._pending_inv is None and p['step'] % p['inv_update_freq'] != 0
-                and not self._graph_eligible() and torch.is_grad_enabled() is False)
+                and not self._graph_eligible() and torch.is_grad_enabled() is False
+                # a segmented GraphedTrainStep capture: the side-stream fork would
+                # be joined only in the separately captured update graph
+                and not torch.cuda.is_current_stream_capturing())
+
+    def _early_tag(self):
+        """Identifies the step and eigenbasis an early top-half launch
+        belongs to (SplitFused.run reuses it only under the same tag)."""
+        return (self.param_groups[0]['step'], self._eigen_gen)
 
     def _top_grad_hook(self, param):
         self._top_seen += 1
@@ -491,7 +500,7 @@ class KFAC(optim.Optimizer):
             self._top_seen = 0
             if self._early_launch_ok():
                 self.fused.launch_top(damping=self.param_groups[0]['damping'],
-                                      with_kl=self._fused_all)
+                                      with_kl=self._fused_all, tag=self._early_tag())
 
     def _register_top_hooks(self):
         for h in self._top_hooks:
@@ -921,6 +930,7 @@ class KFAC(optim.Optimizer):
     def _eigendata_updated(self):
         """New eigendata is in place: refresh the fused kernels' operand copies."""
         self._sync_before_replay = True
+        self._eigen_gen += 1
         if self.fused is not None:
             self.fused.refresh_eigen()
 
@@ -967,7 +977,11 @@ class KFAC(optim.Optimizer):
     def compute_preconditioned_gradients(self, damping=0.001):
         self._fused_kl = None
         if self.fused is not None:
-            self._fused_kl = self.fused.run(damping=damping, with_kl=self._fused_all)
+            if isinstance(self.fused, precond_fused.SplitFused):
+                self._fused_kl = self.fused.run(damping=damping, with_kl=self._fused_all,
+                                                tag=self._early_tag())
+            else:
+                self._fused_kl = self.fused.run(damping=damping, with_kl=self._fused_all)
             return
         for layer in self.layers:
             layer.compute_preconditioned_gradient(damping=damping)
@@ -1034,7 +1048,12 @@ class KFAC(optim.Optimizer):
             # buffers of a superseded plan stay alive: a captured graph may
             # still address them (GraphedTrainStep re-captures on the new
             # plan_generation)
-            self._retired_plans.append((self.plan, self.fused))
+            # Only the latest superseded plan is kept: GraphedTrainStep keys
+            # its graphs on plan_generation and KFAC's tail graph on buffer
+            # pointers, so no graph older than that can replay again, and
+            # work already enqueued on the old buffers is ordered before
+            # anything that reuses their memory on the same stream.
+            self._retired_plans = [(self.plan, self.fused)]
         self.plan = ExecutionPlan(self.layers, world, rank, a_locs, g_locs, allocator,
                                   self.use_eigen_decomp, self.precompute_outer_eigen,
                                   self.inv_dtype, build_eig_arena=True, device=device)

@@ -1,5 +1,5 @@
 """NumPy model of the fused one-launch-per-column tridiagonalisation in
-csrc/eig_tridiag.hip (kernel `sytrd_col_kernel`).
+csrc/eig_reduce.hip (the F / U / S launches of one column).
 
 Launch K(j), j = 0 .. n-1, does in ONE kernel what LAPACK latrd spreads over a
 chain of BLAS-2 calls, using only data the previous launch left behind:

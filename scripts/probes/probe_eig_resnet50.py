@@ -37,41 +37,18 @@ def main():
         x = torch.randn(n, max(64, n // 2), device=dev, generator=g)
         mats.append(x @ x.t() / x.shape[1] + 1e-3 * torch.eye(n, device=dev))
     print('factors', len(ns), 'sum n^3 %.3g' % sum(float(n) ** 3 for n in ns), flush=True)
-    variants = [('default', {}), ('r1_auto', {'LARGE': 'auto', 'SOLVER': 'stedc'}),
-                ('auto_dc', {'LARGE': 'auto'}), ('split4608', {'SPLIT_N': 4096}),
-                ('split2048', {'SPLIT_N': 2048}),
-                ('split4608_w6', {'SPLIT_N': 4096, 'W': 6}),
-                ('w8', {'W': 8}),
-                ('tri1000', {'TRIDIAG_MIN_N': 1000}), ('tri500', {'TRIDIAG_MIN_N': 500}),
-                ('tri240', {'TRIDIAG_MIN_N': 240}), ('tri193', {'TRIDIAG_MIN_N': 193}),
-                ('stedc', {'SOLVER': 'stedc'}), ('stedc_tri193', {'SOLVER': 'stedc', 'TRIDIAG_MIN_N': 193}),
-                ('w2', {'W': 2}), ('w1', {'W': 1}),
-                ('nothreads', {'TH': False}), ('fs1', {'FS': 1}), ('fs3', {'FS': 3}),
-                ('fs4', {'FS': 4}), ('noprio', {'PR': False}),
-                ('noprio_nothreads', {'PR': False, 'TH': False}),
-                ('two_stage', {'TS': True}), ('two_stage_fs1', {'TS': True, 'FS': 1}),
+    variants = [('default', {}), ('fs1', {'FS': 1}), ('fs3', {'FS': 3}),
+                ('threads', {'TH': True}), ('prio', {'PR': True}),
                 ('only_big', {'SEL': 'big'}), ('only_rest', {'SEL': 'rest'}),
                 ('only_big_fs1', {'SEL': 'big', 'FS': 1}), ('only_rest_fs1', {'SEL': 'rest', 'FS': 1})]
     if len(sys.argv) > 1:
         variants = [v for v in variants if v[0] in sys.argv[1:]]
     res = {}
-    base = dict(SPLIT_N=eigen.SPLIT_N, TRIDIAG_MIN_N=eigen.TRIDIAG_MIN_N,
-                SOLVER=eigen.TRIDIAG_SOLVER, LARGE=eigen.LARGE_PATH,
-                FS=eigen.FUSED_STREAMS, TH=eigen.FUSED_THREADS, PR=eigen.FUSED_PRIORITY,
-                TS=eigen.TWO_STAGE)
+    base = dict(FS=eigen.FUSED_STREAMS, TH=eigen.FUSED_THREADS, PR=eigen.FUSED_PRIORITY)
     for name, cfg in variants:
-        eigen.LARGE_PATH = cfg.get('LARGE', base['LARGE'])
-        eigen.TRIDIAG_SOLVER = cfg.get('SOLVER', base['SOLVER'])
-        eigen.SPLIT_N = cfg.get('SPLIT_N', base['SPLIT_N'])
-        eigen.TRIDIAG_MIN_N = cfg.get('TRIDIAG_MIN_N', base['TRIDIAG_MIN_N'])
         eigen.FUSED_STREAMS = cfg.get('FS', base['FS'])
         eigen.FUSED_THREADS = cfg.get('TH', base['TH'])
         eigen.FUSED_PRIORITY = cfg.get('PR', base['PR'])
-        eigen.TWO_STAGE = cfg.get('TS', base['TS'])
-        if 'W' in cfg:
-            os.environ['KFAC_EIGH_WORKERS'] = str(cfg['W'])
-        else:
-            os.environ.pop('KFAC_EIGH_WORKERS', None)
         nmax = max(A.shape[0] for A in mats)
         sel = cfg.get('SEL')
         run_mats = mats if sel is None else [A for A in mats if (2 * A.shape[0] > nmax) == (sel == 'big')]

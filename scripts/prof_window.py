@@ -23,14 +23,12 @@ def category(name):
         return 'kfac: factor SYRK + EMA'
     if 'jacobi' in n:
         return 'kfac: small-n Jacobi eigensolver'
-    if 'sytrd_' in n:
+    if 'red_fin' in n or 'red_symv' in n or 'red_upd' in n:
         return 'kfac: eigensolver tridiagonal reduction'
     if 'dc_' in n:
         return 'kfac: eigensolver divide and conquer'
     if 'larft' in n or 'make_v' in n or 'zero_kernel' in n:
         return 'kfac: eigensolver back-transform (aux)'
-    if 'sy2sb_' in n or 'sb2st_' in n or 'q2_' in n:
-        return 'kfac: two-stage eigensolver'
     if 'chol' in n or 'trtri' in n or 'potrf' in n:
         return 'kfac: Cholesky inverse path'
     if 'tile_reduce' in n or 'syrk_vec' in n:
@@ -39,8 +37,8 @@ def category(name):
         return 'kfac: grad gather / KL / apply'
     if '::bn_' in n:
         return 'model: batchnorm (fused, csrc/bn.hip)'
-    if 'rocsolver' in n or 'rocblas' in n or n.startswith('Cijk'):
-        return 'rocSOLVER/rocBLAS (large-n eigensolver)'
+    if n.startswith('Cijk') or 'hipblaslt' in n.lower():
+        return 'model: torch GEMMs (Tensile / hipBLASLt: fc, matmul)'
     if 'triu' in n:
         return 'kfac: triu pack/unpack'
     if 'BatchNorm' in n or 'bn_' in n.lower():

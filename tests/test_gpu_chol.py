@@ -39,3 +39,18 @@ def test_chol_inverse_not_positive_definite():
     A[3, 3] = -1.0
     with pytest.raises(torch.linalg.LinAlgError):
         eigen.inverse_many([A], 1e-3)
+
+
+def test_chol_plan_cache_bounded_over_damping_schedule():
+    """A damping schedule and fresh factor snapshots make a new plan key per
+    call; the plan cache evicts (LRU, kMaxPlans = 16) and stays correct."""
+    n = 200
+    A64 = _factor(n, 3)
+    eye = torch.eye(n, device=DEV, dtype=torch.float64)
+    for k in range(40):
+        damping = 1e-3 * (1.0 + 0.05 * k)
+        X = eigen.inverse_many([A64.float().clone()], damping)[0]
+        if k % 13 == 0 or k == 39:
+            res = ((A64 + damping * eye) @ X.double() - eye).abs().max().item()
+            assert res <= 1e-3, (k, res)
+    torch.cuda.synchronize()

@@ -77,7 +77,7 @@ def _kfac_factor(n, seed):
 def test_large_factor_eigensolver_resnet50_sizes(n, b):
     """Verdict criterion: residual <= 2e-5 and orthogonality <= 1e-4 at
     n in {1152, 2304, 4608} on the default (rocSOLVER-free) path."""
-    assert eigen.TRIDIAG_SOLVER == 'dc' and eigen.LARGE_PATH == 'fused'
+    assert not hasattr(eigen, 'LARGE_PATH')     # one hand-written path, no library solver
     mats64 = [_kfac_factor(n, 3 + s) for s in range(b)]
     mats = [m.float() for m in mats64]
     for _ in range(2):
@@ -115,7 +115,7 @@ def test_fused_path_beyond_5120(n):
 def test_fused_ragged_large_path():
     """The default large-factor path: every size in ONE fused reduction (one
     launch per column for the ragged batch), one batched D&C, WY back-transform."""
-    assert eigen.LARGE_PATH == 'fused'
+    assert not hasattr(eigen, 'LARGE_PATH')
     sizes = [193, 256, 256, 300, 577, 1000, 1152, 2049]
     mats64 = [_kfac_factor(n, 40 + i) for i, n in enumerate(sizes)]
     mats = [m.float() for m in mats64]
@@ -136,7 +136,7 @@ def test_fused_ragged_large_path():
 def test_fused_path_small_and_odd_sizes():
     """The fused default takes every factor size (no Jacobi split): tiny,
     single-leaf, one-tile and odd sizes next to a large one, in one call."""
-    assert eigen.LARGE_PATH == 'fused'
+    assert not hasattr(eigen, 'LARGE_PATH')
     sizes = [2, 3, 17, 64, 65, 127, 128, 147, 192, 300, 1025]
     mats64 = [_kfac_factor(n, 70 + i) for i, n in enumerate(sizes)]
     mats = [m.float() for m in mats64]

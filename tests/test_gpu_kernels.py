@@ -176,7 +176,7 @@ def test_symeig_large_path():
     assert resid < 1e-4
 
 
-@pytest.mark.parametrize('solver', ['auto', 'serial'])
+@pytest.mark.parametrize('solver', ['auto', 'jacobi'])
 def test_symeig_size_classes(solver):
     """Several factors per size class (strided batch) + several classes
     (concurrent streams); order and per-matrix results must be preserved."""

@@ -59,3 +59,45 @@ def test_overlap_matches_single_chain(use_graphs):
     num = sum(((a - b).double().norm() ** 2 for a, b in zip(p0, p1))) ** 0.5
     den = sum((a.double().norm() ** 2 for a in p0)) ** 0.5
     assert float(num / den) < 1e-5, float(num / den)
+
+
+def test_stale_early_launch_is_recomputed():
+    """An early top-half launch from another step / eigenbasis (a backward not
+    followed by KFAC.step(), new eigendata) must not be reused: run() checks
+    the launch's tag and preconditions afresh."""
+    from distributed_kfac_pytorch_amd.ops import precond_fused
+
+    def build(overlap):
+        torch.manual_seed(0)
+        m = resnet.resnet_tiny(num_classes=10).cuda().to(memory_format=torch.channels_last)
+        pre = kfac.KFAC(m, factor_update_freq=1, inv_update_freq=3, lr=0.05,
+                        precond_precision='fp32', overlap_precondition=overlap,
+                        use_hip_graphs=False)
+        return m, pre
+
+    g = torch.Generator(device='cuda').manual_seed(7)
+    x = torch.randn(8, 3, 32, 32, device='cuda', generator=g).contiguous(
+        memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device='cuda', generator=g)
+    grads = []
+    for overlap in (False, True):
+        m, pre = build(overlap)
+        for _ in range(2):          # inverses exist, next step is a plain one
+            m.zero_grad(set_to_none=False)
+            F.cross_entropy(m(x), y).backward()
+            pre.step()
+        m.zero_grad(set_to_none=False)
+        F.cross_entropy(m(x), y).backward()
+        if overlap:
+            assert isinstance(pre.fused, precond_fused.SplitFused)
+            assert pre.fused._launched is not None
+            # the launch belongs to other gradients: scale them, and retag the
+            # launch as stale (as a grad-only backward of another step would)
+            pre.fused._launched = (('stale',),) + pre.fused._launched[1:]
+        for p in m.parameters():
+            p.grad.mul_(2.0)
+        pre.step()
+        torch.cuda.synchronize()
+        grads.append([p.grad.detach().clone() for p in m.parameters()])
+    for a, b in zip(*grads):
+        assert torch.allclose(a, b, atol=1e-6, rtol=1e-4), (a - b).abs().max()
