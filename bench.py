@@ -83,10 +83,13 @@ def parse():
     ap.add_argument('--inverse-lag', type=int, default=0,
                     help='KFAC(inverse_lag=L): eigendecompositions of an inverse step run on a '
                          'side stream and take effect L steps later (0 = reference schedule)')
-    ap.add_argument('--assignment-strategy', default='measured',
-                    choices=['measured', 'compute', 'memory'],
-                    help="LPT cost of a factor's inverse: 'measured' = the MI355X fused-solver "
-                         "table (preconditioner.MEASURED_COST_MS), 'compute' = n^3 (reference)")
+    ap.add_argument('--assignment-strategy', default='batched',
+                    choices=['batched', 'measured', 'compute', 'memory'],
+                    help="inverse work distribution: 'batched' = makespan over the MI355X "
+                         "batched per-rank solve model + eigendata arena balance "
+                         "(preconditioner.BATCHED_COST_MS, profiles/r3_inverse_share.log); "
+                         "'measured' = additive per-factor table + LPT; 'compute' = n^3 LPT "
+                         "(reference)")
     ap.add_argument('--overlap-grad-comm', type=int, default=1,
                     help='world > 1 with graphs: backward in two graph segments, the top '
                          "half's gradient all-reduce overlapped with the bottom half's backward "

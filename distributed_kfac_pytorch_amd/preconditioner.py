@@ -133,6 +133,26 @@ def measured_cost(n):
     return a * n + c2 * n * n + c3 * n ** 3
 
 
+# Batched per-rank cost (ms) of the fused solver on MI355X: a rank solves all
+# its factors in ONE ragged launch sequence, so its time is a set function --
+# the column chain of its largest factor (latency per column) plus the
+# traffic / flops of all of them -- not a sum of single-factor costs (the
+# 'measured' table summed to 1,432 ms for ResNet-50's 108 factors against
+# 157 ms measured batched).  T(S) = a n_max + b3 sum n^3 + b2 sum n^2 + b0 |S|,
+# least-squares fit to one-GPU solves of per-rank sets
+# (scripts/probes/probe_inverse_share.py, profiles/r3_inverse_share.log).
+BATCHED_COST_MS = (1.023e-2, 7.213e-11, 2.027e-7, 8.069e-2)
+
+
+def batched_cost(sizes):
+    """Modelled wall time (ms) of solving every factor in `sizes` together."""
+    if not sizes:
+        return 0.0
+    a, b3, b2, b0 = BATCHED_COST_MS
+    return (a * max(sizes) + b3 * sum(float(n) ** 3 for n in sizes) +
+            b2 * sum(float(n) ** 2 for n in sizes) + b0 * len(sizes))
+
+
 def assignment_cost(strategy):
     """n -> LPT cost of a factor: 'compute' n^3 and 'memory' n^2 (reference
     semantics, kfac/preconditioner.py:625-631), 'measured' the MI355X table,
@@ -140,7 +160,7 @@ def assignment_cost(strategy):
     if callable(strategy):
         return strategy
     return {'compute': lambda n: n ** 3, 'memory': lambda n: n ** 2,
-            'measured': measured_cost}[strategy]
+            'measured': measured_cost, 'batched': measured_cost}[strategy]
 
 
 class KFAC(optim.Optimizer):
@@ -173,8 +193,9 @@ class KFAC(optim.Optimizer):
             warnings.warn('It is suggested that inv_update_freq be a multiple of '
                           'factor_update_freq')
         if not callable(assignment_strategy) and \
-                assignment_strategy not in ('compute', 'memory', 'measured'):
-            raise ValueError('assignment_strategy must be "compute", "memory", "measured" or '
+                assignment_strategy not in ('compute', 'memory', 'measured', 'batched'):
+            raise ValueError('assignment_strategy must be "compute", "memory", "measured", '
+                             '"batched" or '
                              'a callable n -> cost')
         if not isinstance(comm_method, CommMethod):
             raise ValueError('comm_method must be a kfac.CommMethod')
@@ -1031,7 +1052,9 @@ class KFAC(optim.Optimizer):
         g_times = [cost(n) for n in g_sizes]
         world = comm.backend.size()
         rank = comm.backend.rank()
-        if self.distribute_layer_factors:
+        if self.assignment_strategy == 'batched':
+            a_locs, g_locs = self._assign_batched(world, a_sizes, g_sizes)
+        elif self.distribute_layer_factors:
             locs = distribution.load_balance(world, a_times + g_times)
             a_locs, g_locs = locs[:len(a_times)], locs[len(a_times):]
         else:
@@ -1061,6 +1084,32 @@ class KFAC(optim.Optimizer):
         self.plan_generation += 1
         self._graph = None
         self._build_fused()
+
+    def _assign_batched(self, world, a_sizes, g_sizes):
+        """assignment_strategy='batched': makespan-greedy over the batched
+        per-rank solve model (batched_cost), then byte balancing of the
+        eigendata all-gather slots (utils.distribution.balance_batched)."""
+        esize = 4 if self.inv_dtype == torch.float32 else 2
+        pre = self.use_eigen_decomp and self.precompute_outer_eigen
+
+        def nbytes(nA, nG, which):
+            if not self.use_eigen_decomp:
+                return esize * ((nA * nA if 'A' in which else 0) + (nG * nG if 'G' in which else 0))
+            b = (nA * nA + (0 if pre else nA)) if 'A' in which else 0
+            b += (nG * nG + (0 if pre else nG)) if 'G' in which else 0
+            if pre and 'A' in which:
+                b += nA * nG         # dGdA lives with the A owner (parallel/plan.py)
+            return esize * b
+        if self.distribute_layer_factors:
+            units = [[n] for n in a_sizes] + [[n] for n in g_sizes]
+            ub = ([nbytes(a, g, 'A') for a, g in zip(a_sizes, g_sizes)] +
+                  [nbytes(a, g, 'G') for a, g in zip(a_sizes, g_sizes)])
+            locs = distribution.balance_batched(world, units, batched_cost, ub)
+            return locs[:len(a_sizes)], locs[len(a_sizes):]
+        units = [[a, g] for a, g in zip(a_sizes, g_sizes)]
+        ub = [nbytes(a, g, 'AG') for a, g in zip(a_sizes, g_sizes)]
+        locs = distribution.balance_batched(world, units, batched_cost, ub)
+        return locs, locs
 
     def _factor_shapes(self):
         return tuple((tuple(l.state['A'].shape), tuple(l.state['G'].shape)) for l in self.layers)

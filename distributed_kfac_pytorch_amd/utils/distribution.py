@@ -3,6 +3,9 @@
 Parity targets (reference, read-only at /root/reference):
   * `load_balance`           ~ kfac/utils.py:169-196 (greedy LPT, goldens in
                                tests/load_balance.py)
+  * `balance_batched`        MI355X-specific: makespan greedy for a set-valued
+                               rank cost (the batched eigensolver) + byte
+                               balancing of the padded eigendata arena
   * `partition_grad_ranks`   ~ kfac/utils.py:150-153 (strided groups)
   * `partition_inv_ranks`    ~ kfac/utils.py:156-159 (contiguous blocks)
   * `WorkerAllocator`        ~ kfac/utils.py:59-147
@@ -15,7 +18,7 @@ sub-communicator once, in a rank-independent order, at plan build time.
 """
 import heapq
 
-__all__ = ['load_balance', 'partition_grad_ranks', 'partition_inv_ranks',
+__all__ = ['load_balance', 'balance_batched', 'partition_grad_ranks', 'partition_inv_ranks',
            'WorkerAllocator', 'get_block_boundary', 'try_contiguous']
 
 
@@ -38,6 +41,90 @@ def load_balance(n_workers, work):
         load, w = heapq.heappop(heap)
         assignment[i] = w
         heapq.heappush(heap, (load + work[i], w))
+    return assignment
+
+
+def balance_batched(n_workers, units, rank_cost, unit_bytes=None, ms_per_byte=3.3e-9,
+                    max_moves=10000):
+    """Assign `units` (each a list of factor sizes solved on one rank, e.g. a
+    layer's [nA, nG]) to workers for a solver that batches every factor of a
+    rank into one launch sequence, so a rank's time is a set function
+    `rank_cost(sizes)` (ms: the chain length of its largest factor plus the
+    bandwidth of all), not a sum of per-factor costs.
+
+    1. Greedy makespan: units in decreasing (largest size, sum n^3); each goes
+       to the worker whose new cost keeps the running makespan smallest (ties:
+       smaller new cost, fewer bytes, lower index).
+    2. Arena balance (`unit_bytes`: the eigendata each unit adds to its
+       owner's slot of the padded all-gather arena, parallel/plan.py, where
+       every slot is as large as the largest): move single units off the
+       byte-heaviest worker while the objective
+           makespan + ms_per_byte * n_workers * max slot bytes
+       (solve time + all-gather time of the padded arena; 3.3e-9 ms/B ~ 300
+       GB/s effective all-gather bandwidth per rank over xGMI) decreases.
+    Deterministic (a pure function of the arguments): every rank computes the
+    same assignment.  Returns assignment[i] = worker of unit i.
+    """
+    if n_workers <= 0:
+        raise ValueError('n_workers must be > 0')
+    if len(units) == 0:
+        raise ValueError('units cannot be an empty list')
+    units = [list(u) for u in units]
+    nbytes = list(unit_bytes) if unit_bytes is not None else [0] * len(units)
+    order = sorted(range(len(units)),
+                   key=lambda i: (-max(units[i]), -sum(float(n) ** 3 for n in units[i]), i))
+    members = [[] for _ in range(n_workers)]
+    cost = [0.0] * n_workers
+    load = [0] * n_workers
+    assignment = [0] * len(units)
+
+    def sizes_of(idx):
+        return [n for j in idx for n in units[j]]
+    for i in order:
+        best = None
+        for w in range(n_workers):
+            c = rank_cost(sizes_of(members[w]) + units[i])
+            span = max([c] + [cost[v] for v in range(n_workers) if v != w])
+            key = (span, c, load[w] + nbytes[i], w)
+            if best is None or key < best[0]:
+                best = (key, w, c)
+        _, w, c = best
+        assignment[i] = w
+        members[w].append(i)
+        cost[w] = c
+        load[w] += nbytes[i]
+    if unit_bytes is None or n_workers == 1:
+        return assignment
+
+    def objective(cst, ld):
+        return max(cst) + ms_per_byte * n_workers * max(ld)
+    obj = objective(cost, load)
+    for _ in range(max_moves):
+        hi = max(range(n_workers), key=lambda w: (load[w], -w))
+        best = None
+        for i in sorted(members[hi], key=lambda i: (nbytes[i], i)):
+            rest = [j for j in members[hi] if j != i]
+            c_hi = rank_cost(sizes_of(rest)) if rest else 0.0
+            for w in sorted(range(n_workers), key=lambda w: (load[w], w)):
+                if w == hi:
+                    continue
+                c_w = rank_cost(sizes_of(members[w]) + units[i])
+                cst, ld = list(cost), list(load)
+                cst[hi], cst[w] = c_hi, c_w
+                ld[hi] -= nbytes[i]
+                ld[w] += nbytes[i]
+                o = objective(cst, ld)
+                if o < obj - 1e-9 and (best is None or o < best[0]):
+                    best = (o, i, w, c_hi, c_w)
+        if best is None:
+            break
+        obj, i, w, c_hi, c_w = best
+        members[hi].remove(i)
+        members[w].append(i)
+        cost[hi], cost[w] = c_hi, c_w
+        load[hi] -= nbytes[i]
+        load[w] += nbytes[i]
+        assignment[i] = w
     return assignment
 
 

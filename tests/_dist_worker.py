@@ -66,7 +66,8 @@ def kfac_strategy(rank, world, port, out_dir, cfg):
                     distribute_layer_factors=cfg.get('distribute', False),
                     precompute_outer_eigen=cfg.get('prediv', True),
                     use_eigen_decomp=cfg.get('eigen', True),
-                    inverse_lag=cfg.get('lag', 0))
+                    inverse_lag=cfg.get('lag', 0),
+                    assignment_strategy=cfg.get('assign', 'compute'))
     calls = _count_collectives(pre)
     grads, factors = run_steps(model, pre, data, cfg['steps'])
     torch.save({'grads': grads, 'factors': factors, 'calls': calls},

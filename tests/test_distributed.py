@@ -64,6 +64,10 @@ CASES = [
     (8, {'method': 'COMM_OPT'}),
     (8, {'method': 'MEM_OPT'}),
     (8, {'method': 'HYBRID_OPT', 'fraction': 0.25}),
+    # the batched-solver assignment (set-valued rank cost + arena byte balance)
+    (4, {'method': 'COMM_OPT', 'assign': 'batched'}),
+    (4, {'method': 'HYBRID_OPT', 'fraction': 0.5, 'assign': 'batched', 'distribute': True,
+         'prediv': False}),
 ]
 
 
