@@ -113,14 +113,16 @@ template <int PREC, int BM, int BN, int WM, int WN, int WPE = 1, bool DBUF = fal
 __global__ __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(WPE)))
 void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict__ kl) {
   constexpr bool X3 = (PREC == PREC_BF16X3), X6 = (PREC == PREC_BF16X6);
-  constexpr bool SPL = X3 || X6;                  // split-bf16 planes
+  constexpr bool X6F = (PREC == PREC_BF16X6F);     // fp32 in memory, planes in LDS
+  constexpr bool SPL = X3 || X6;                  // split-bf16 planes in memory
+  constexpr bool IMG16 = SPL || X6F;              // bf16 plane image in LDS
   constexpr int NT = 64 * WM * WN;                // threads
   constexpr int MI = BM / WM / 32, NJ = BN / WN / 32;
   constexpr int LDB16 = TK + 8;   // 80-byte rows: conflict-free ds_read_b128 (guide: LDS banking)
   constexpr int LDF32 = TK + 4;   // 16-byte aligned chunk writes
   // one LDS array (guide: a second __shared__ object can de-pipeline loads)
-  constexpr int PL = X6 ? 3 : (X3 ? 2 : 1);       // planes
-  constexpr int LDS_BYTES = SPL ? (PL * (BM + BN) * LDB16 * 2) : ((BM + BN) * LDF32 * 4);
+  constexpr int PL = (X6 || X6F) ? 3 : (X3 ? 2 : 1);   // planes
+  constexpr int LDS_BYTES = IMG16 ? (PL * (BM + BN) * LDB16 * 2) : ((BM + BN) * LDF32 * 4);
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES * (DBUF ? 2 : 1)];
 
   const int pi = find_problem(table, count, blockIdx.x);
@@ -149,7 +151,8 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   // ---- loader: 16-byte chunks.  bf16 planes: per operand 2 planes x rows x 4
   // chunks (8 elements); f32: rows x 8 chunks (4 elements)
   constexpr int CPR = SPL ? TK / 8 : TK / 4;      // chunks per row and plane
-  constexpr int CA = PL * BM * CPR, CB = PL * BN * CPR;
+  constexpr int MPL = SPL ? PL : 1;               // planes in memory
+  constexpr int CA = MPL * BM * CPR, CB = MPL * BN * CPR;
   constexpr int QA = CA / NT, QB = CB / NT;
   static_assert(CA % NT == 0 && CB % NT == 0, "loader split");
   // a chunk round stays in one plane: the plane index is a compile-time
@@ -203,19 +206,36 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
     }
   };
   // LDS image: [A planes | B planes] rows of LDB16 bf16 (X3 / X6) or [A | B] rows of LDF32 f32
+  // X6F: four fp32 values -> hi / mid / lo bf16 quads, one 8-byte LDS write
+  // per plane (the split of split_bf16_3, so results equal PREC_BF16X6's)
+  auto store_split = [&](uint16_t* dst, long long plane_stride, const u32x4n& v) {
+    uint16_t h[4], m[4], l[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) split_bf16_3(__uint_as_float(v[e]), h[e], m[e], l[e]);
+    typedef unsigned u32x2n __attribute__((ext_vector_type(2)));
+    const u32x2n ph = {h[0] | ((unsigned)h[1] << 16), h[2] | ((unsigned)h[3] << 16)};
+    const u32x2n pm = {m[0] | ((unsigned)m[1] << 16), m[2] | ((unsigned)m[3] << 16)};
+    const u32x2n pl = {l[0] | ((unsigned)l[1] << 16), l[2] | ((unsigned)l[3] << 16)};
+    *(u32x2n*)dst = ph;
+    *(u32x2n*)(dst + plane_stride) = pm;
+    *(u32x2n*)(dst + 2 * plane_stride) = pl;
+  };
   auto store = [&](unsigned char* img) {
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
       const int c = tid + NT * q;
       const int plane = c / (BM * CPR), row = (c % (BM * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
-      if (SPL) *(u32x4n*)((uint16_t*)img + (plane * BM + row) * LDB16 + kof) = ra[q];
+      if (X6F) store_split((uint16_t*)img + row * LDB16 + kof, (long long)BM * LDB16, ra[q]);
+      else if (SPL) *(u32x4n*)((uint16_t*)img + (plane * BM + row) * LDB16 + kof) = ra[q];
       else *(u32x4n*)((float*)img + row * LDF32 + kof) = (row & 16) ? ra[q].zwxy : ra[q];
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
       const int c = tid + NT * q;
       const int plane = c / (BN * CPR), row = (c % (BN * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
-      if (SPL) *(u32x4n*)((uint16_t*)img + (PL * BM + plane * BN + row) * LDB16 + kof) = rb[q];
+      if (X6F) store_split((uint16_t*)img + (PL * BM + row) * LDB16 + kof, (long long)BN * LDB16,
+                           rb[q]);
+      else if (SPL) *(u32x4n*)((uint16_t*)img + (PL * BM + plane * BN + row) * LDB16 + kof) = rb[q];
       else *(u32x4n*)((float*)img + (BM + row) * LDF32 + kof) = (row & 16) ? rb[q].zwxy : rb[q];
     }
   };
@@ -270,7 +290,7 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
           }
         }
       }
-    } else if constexpr (X6) {
+    } else if constexpr (X6 || X6F) {
       const uint16_t* sA0 = (const uint16_t*)cur;
       const uint16_t* sB0 = sA0 + 3 * BM * LDB16;
 #pragma unroll
@@ -593,6 +613,27 @@ KFAC_API int kfac_pgemm(int prec, int tile, const void* dev_table, int count, in
     // default tile only (the 3-plane image is 60 KB of LDS per workgroup)
     hipLaunchKernelGGL((pgemm_kernel<PREC_BF16X6, 128, 128, 2, 2, 2>), g, dim3(256), 0, stream, t,
                        count, kl);
+  } else if (prec == PREC_BF16X6F) {
+    // bigger tiles for problems with M, N >= 256: less operand traffic per
+    // FLOP (the chain reads its operands at ~5 TB/s from L2 / MALL)
+    if (tile == 1)
+      hipLaunchKernelGGL((pgemm_kernel<PREC_BF16X6F, 256, 256, 2, 4>), g, dim3(512), 0, stream, t,
+                         count, kl);
+    else if (tile == 6)
+      hipLaunchKernelGGL((pgemm_kernel<PREC_BF16X6F, 256, 128, 4, 2>), g, dim3(512), 0, stream, t,
+                         count, kl);
+    else if (tile == 7)
+      hipLaunchKernelGGL((pgemm_kernel<PREC_BF16X6F, 128, 256, 2, 4>), g, dim3(512), 0, stream, t,
+                         count, kl);
+    else if (tile == 9)
+      hipLaunchKernelGGL((pgemm_kernel<PREC_BF16X6F, 128, 128, 2, 2, 2, true>), g, dim3(256), 0,
+                         stream, t, count, kl);
+    else if (tile == 8)
+      hipLaunchKernelGGL((pgemm_kernel<PREC_BF16X6F, 128, 128, 2, 2, 1>), g, dim3(256), 0, stream,
+                         t, count, kl);
+    else
+      hipLaunchKernelGGL((pgemm_kernel<PREC_BF16X6F, 128, 128, 2, 2, 2>), g, dim3(256), 0, stream,
+                         t, count, kl);
   } else if (prec == PREC_F32) {
     KFAC_PGEMM_LAUNCH(PREC_F32)
   } else {

@@ -19,6 +19,10 @@ Precision (`precision=`):
   'bf16x6'  operands as three bf16 planes (hi, mid, lo = the fp32
             significand), six bf16 MFMAs per product (every term above 2^-24
             relative), fp32 accumulation: fp32-level error at the bf16 rate.
+            The operands stay fp32 in memory and are split into the planes
+            while the kernel stages them into LDS (PREC_BF16X6F: 4 bytes per
+            element from L2 / HBM instead of 6, no plane copies);
+            KFAC_X6_PLANES=1 keeps the round-2 plane-stored operands.
   'fp32'    fp32 operands on the exact f32 MFMA (the reference's fp32 math).
 
 Static GEMM tables (all pointers are arena/buffer pointers that never move)
@@ -39,6 +43,9 @@ __all__ = ['FusedPreconditioner', 'PRECISIONS']
 
 PRECISIONS = {'fp32': 0, 'bf16x3': 1, 'bf16x6': 2}
 PLANES = {'fp32': 1, 'bf16x3': 2, 'bf16x6': 3}
+PREC_BF16X6F = 3   # csrc/pgemm.h: bf16x6 products on fp32 operands
+X6_PLANES = bool(int(os.environ.get('KFAC_X6_PLANES', '0')))
+X6_BIG = int(os.environ['KFAC_X6_BIG']) if os.environ.get('KFAC_X6_BIG') else None
 EPI_STORE, EPI_HADAMARD, EPI_HADAMARD_VEC, EPI_FINAL = 0, 1, 2, 3
 TILE = 128        # small tile class (csrc/precond_gemm.hip)
 BIG_TILE = 256    # big tile class: half the operand traffic per FLOP
@@ -66,7 +73,12 @@ def _tile_class(M, N, precision):
     waves per tile win over bigger tiles; the big class stays available for
     experiments."""
     if precision == 'bf16x6':
-        return 0      # the one instantiated 3-plane configuration
+        # the instantiated configurations: 0 (2 waves / SIMD), 8 (uncapped
+        # registers), 9 (two LDS images); X6_BIG (1 = 256 x 256, 6 = 256 x 128,
+        # 7 = 128 x 256, fp32-operand mode only) for problems with M, N >= 256
+        if X6_BIG is not None and M >= 256 and N >= 256:
+            return X6_BIG
+        return TILE_CFG if TILE_CFG in (8, 9) else 0
     if BIG_TILES and M >= 256 and N >= 256:
         return 1
     return TILE_CFG if TILE_CFG is not None else TILE_CFG_DEFAULT[precision]
@@ -185,6 +197,10 @@ class FusedPreconditioner(object):
         self.prec = PRECISIONS[precision]
         self.x3 = precision == 'bf16x3'
         self.planes = PLANES[precision]
+        # precision of the stored operands (gather / split launches)
+        self.store_prec = self.prec
+        if precision == 'bf16x6' and not X6_PLANES:
+            self.prec, self.store_prec, self.planes = PREC_BF16X6F, 0, 1
         self.device = self.layers[0].module.weight.device if self.layers else None
         # the damped-inverse path (K9): V = G_inv Grad A_inv, two grouped stages
         self.inverse = bool(self.layers) and not self.layers[0].use_eigen_decomp
@@ -312,7 +328,7 @@ class FusedPreconditioner(object):
                 add(fjobs, D, _F32Dst(b.Dt), True)
         stream = _lib.stream(self.device)
         L = _lib.lib()
-        for lst, prec in ((jobs, self.prec), (fjobs, 0)):
+        for lst, prec in ((jobs, self.store_prec), (fjobs, 0)):
             if not lst:
                 continue
             tiles = 0
@@ -382,7 +398,8 @@ class FusedPreconditioner(object):
         L = _lib.lib()
         stream = _lib.stream(self.device)
         recs = self._gather_table()
-        _lib.check(L.kfac_gather_grad(self.prec, recs, len(recs), stream), 'kfac_gather_grad')
+        _lib.check(L.kfac_gather_grad(self.store_prec, recs, len(recs), stream),
+                   'kfac_gather_grad')
         final = len(self._stage_tables) - 1
         for i, launches in enumerate(self._stage_tables):
             slot = 1

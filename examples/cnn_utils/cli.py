@@ -52,7 +52,7 @@ def base_parser(desc, d):
     p.add_argument('--kfac-comm-method', default='comm-opt',
                    choices=['comm-opt', 'mem-opt', 'hybrid-opt'])
     p.add_argument('--kfac-grad-worker-fraction', type=float, default=0.25)
-    p.add_argument('--precond-precision', default='fp32', choices=['fp32', 'bf16x3', 'bf16x6'],
+    p.add_argument('--precond-precision', default='bf16x6', choices=['fp32', 'bf16x3', 'bf16x6'],
                    help='fused preconditioning GEMMs: fp32 (exact-f32 MFMA), bf16x6 (three bf16 '
                         'planes, fp32-level error at the bf16 MFMA rate; the bench default) or '
                         'bf16x3 (~1e-5 relative error)')

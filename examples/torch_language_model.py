@@ -74,7 +74,9 @@ def parse(argv=None):
     p.add_argument('--skip-layers', nargs='+', default=['embedding'])
     p.add_argument('--kfac-comm-method', default='hybrid-opt', choices=sorted(COMM))
     p.add_argument('--kfac-grad-worker-fraction', type=float, default=0.25)
-    p.add_argument('--precond-precision', default='fp32', choices=['fp32', 'bf16x3'])
+    p.add_argument('--precond-precision', default='bf16x6', choices=['bf16x6', 'fp32', 'bf16x3'],
+                   help='preconditioning GEMMs: bf16x6 = six bf16 MFMA products per fp32 '
+                        'product (fp32-level error), fp32 = exact f32 MFMA, bf16x3 = ~1e-5')
     p.add_argument('--verbose', action='store_true')
     return p.parse_args(argv)
 

@@ -75,5 +75,5 @@ for i, launches in enumerate(fz._stage_tables):
     desc = ' '.join('%s:%d' % ('big' if tl else 'small', n) for tl, _, _, n in launches)
     print('  stage %d: %.3f ms  %6.1f GFLOP  %6.1f TFLOP/s  tiles %s' % (i + 1, t, flops[i] / 1e9, flops[i] / t / 1e9, desc))
 recs = fz._gather_table()
-t = timeit(lambda: L.kfac_gather_grad(fz.prec, recs, len(recs), stream))
+t = timeit(lambda: L.kfac_gather_grad(fz.store_prec, recs, len(recs), stream))
 print('  gather: %.3f ms' % t)

@@ -65,16 +65,25 @@ def _pdiff(pa, pb):
 
 def test_graphed_matches_eager():
     # 14 steps: eager inverse steps 0 and 10, factor steps, plain steps
+    # bf16 autocast runs are not bitwise reproducible run to run: MIOpen's
+    # bf16 convolution algorithms and the eigensolver back-transformation's
+    # split-K f32 atomics (the factor SYRK is deterministic); fp32 runs are
+    # (test_graphed_equals_eager_deterministic).  Bounds: 0.5 % or 4x the
+    # eager run-to-run spread at that step.
     le, pe, se = _train(False, steps=14)
-    le2, pe2, _ = _train(False, steps=14)     # run-to-run noise (f32 atomics in the SYRK)
+    le2, pe2, _ = _train(False, steps=14)
     lg, pg, sg = _train(True, steps=14)
     assert sg.replays > 0 and len(sg.graphs) == 2      # 'plain' and 'factor' graphs
     assert se.replays == 0
     noise = _pdiff(pe, pe2)
     diff = _pdiff(pe, pg)
-    for a, b in zip(le, lg):
-        assert abs(a - b) < 2e-2 * max(1.0, abs(a)), (le, lg)
+    _check_losses(le, le2, lg, 5e-3)
     assert diff < max(5e-3, 20 * noise), (diff, noise, le, lg)
+
+
+def _check_losses(le, le2, lg, rel):
+    for a, a2, b in zip(le, le2, lg):
+        assert abs(a - b) <= max(rel * max(1.0, abs(a)), 4 * abs(a - a2)), (le, le2, lg)
 
 
 def test_graphed_equals_eager_deterministic():
@@ -103,8 +112,7 @@ def test_segmented_graphs_match_eager():
     le2, pe2, _ = _train(False, steps=14, segmented=True)
     ls, ps, ss = _train(True, steps=14, segmented=True)
     assert ss.replays > 0 and len(ss.graphs) == 4      # fb/update x plain/factor
-    for a, b in zip(le, ls):
-        assert abs(a - b) < 2e-2 * max(1.0, abs(a)), (le, ls)
+    _check_losses(le, le2, ls, 5e-3)
     noise, diff = _pdiff(pe, pe2), _pdiff(pe, ps)
     assert diff < max(1e-2, 20 * noise), (diff, noise)
 
@@ -116,8 +124,7 @@ def test_graphed_set_to_none_matches_eager():
     le2, pe2, _ = _train(False, steps=14, set_to_none=True)
     lg, pg, sg = _train(True, steps=14, set_to_none=True)
     assert sg.replays > 0
-    for a, b in zip(le, lg):
-        assert abs(a - b) < 2e-2 * max(1.0, abs(a)), (le, lg)
+    _check_losses(le, le2, lg, 5e-3)
     noise, diff = _pdiff(pe, pe2), _pdiff(pe, pg)
     assert diff < max(5e-3, 20 * noise), (diff, noise)
 
@@ -131,11 +138,9 @@ def test_graphed_lagged_inverses_match_eager(segmented):
     le2, pe2, _ = _train(False, steps=25, lag=4, segmented=segmented)
     lg, pg, sg = _train(True, steps=25, lag=4, segmented=segmented)
     assert sg.replays > 0 and sg.eager_steps == 5     # 0, 10, 14, 20, 24
-    # 25 bf16-autocast steps amplify the f32-atomic SYRK noise (one GPU run
-    # drifted 2.1 % at step ~20): bound each loss by 3 % or 4x the eager
-    # run-to-run spread at that step, whichever is larger
-    for a, a2, b in zip(le, le2, lg):
-        assert abs(a - b) < max(3e-2 * max(1.0, abs(a)), 4 * abs(a - a2)), (le, le2, lg)
+    # 25 bf16-autocast steps with three inverse updates amplify the run-to-run
+    # noise (see test_graphed_matches_eager): 1 % or 4x the eager spread
+    _check_losses(le, le2, lg, 1e-2)
     noise, diff = _pdiff(pe, pe2), _pdiff(pe, pg)
     assert diff < max(1e-2, 20 * noise), (diff, noise)
 

@@ -46,8 +46,19 @@ def _train(overlap, use_graphs, steps=14):
     return losses, [p.detach().clone() for p in m.parameters()], pre
 
 
+@pytest.fixture
+def deterministic_convs():
+    # MIOpen's algorithm choice (benchmark mode) and its non-deterministic
+    # kernels differ run to run (step-0 losses of two identical runs differed
+    # in the 7th digit): compare the two chains on deterministic convolutions
+    prev = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    yield
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = prev
+
+
 @pytest.mark.parametrize('use_graphs', [False, True])
-def test_overlap_matches_single_chain(use_graphs):
+def test_overlap_matches_single_chain(use_graphs, deterministic_convs):
     l0, p0, pre0 = _train(False, use_graphs)
     l1, p1, pre1 = _train(True, use_graphs)
     from distributed_kfac_pytorch_amd.ops import precond_fused
@@ -61,7 +72,7 @@ def test_overlap_matches_single_chain(use_graphs):
     assert float(num / den) < 1e-5, float(num / den)
 
 
-def test_stale_early_launch_is_recomputed():
+def test_stale_early_launch_is_recomputed(deterministic_convs):
     """An early top-half launch from another step / eigenbasis (a backward not
     followed by KFAC.step(), new eigendata) must not be reused: run() checks
     the launch's tag and preconditions afresh."""
