@@ -9,6 +9,7 @@
 // vendor library is linked.
 #include "pgemm.h"
 
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -38,6 +39,13 @@ namespace {
 constexpr int BT = 128;       // reflectors per block
 constexpr int KCH = 512;      // split-K chunk of S1
 constexpr int TILE_F32 = 0;   // pgemm 128 x 128 fp32, 4 waves (best since round 2: profiles/r2_pgemm_sweep.log)
+// GEMM precision of the back-transformation: bf16x6 on the fp32 operands
+// (PREC_BF16X6F: six bf16 MFMA products, fp32-level error, at the bf16 MFMA
+// rate) unless KFAC_EIG_GEMM=fp32 (exact f32 MFMA)
+const int g_bt_prec = [] {
+  const char* e = getenv("KFAC_EIG_GEMM");
+  return (e && !strcmp(e, "fp32")) ? (int)PREC_F32 : (int)PREC_BF16X6F;
+}();
 
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
@@ -203,7 +211,7 @@ int run_plan(const BtArgs& a, const BtPlan& plan, hipStream_t stream) {
     int err = 0;
     const unsigned char* t = (const unsigned char*)plan.tables + op.off;
     switch (op.kind) {
-      case 0: err = kfac_pgemm(PREC_F32, TILE_F32, t, op.count, op.tiles, nullptr, stream); break;
+      case 0: err = kfac_pgemm(g_bt_prec, TILE_F32, t, op.count, op.tiles, nullptr, stream); break;
       case 1: err = kfac_split_copy(PREC_F32, t, op.count, op.tiles, stream); break;
       case 2: {
         const long long n4 = (long long)(op.bytes / 16);

@@ -40,6 +40,7 @@
 // Reference semantics: kfac/layers/utils.py:45-74 (symeig, ascending).
 #include "pgemm.h"
 
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -59,6 +60,13 @@ constexpr double EPS64 = 1.1102230246251565e-16;   // 2^-53
 constexpr int MAX_IT = 64;
 constexpr int RPB = 4;            // secular: roots (waves) per block
 constexpr int TILE_F32 = 0;       // pgemm 128 x 128, 4 waves (profiles/r2_pgemm_sweep.log)
+// GEMM precision of the merge (eigenvector update): bf16x6 on the fp32 operands
+// (PREC_BF16X6F: six bf16 MFMA products, fp32-level error, at the bf16 MFMA
+// rate) unless KFAC_EIG_GEMM=fp32 (exact f32 MFMA)
+const int g_dc_prec = [] {
+  const char* e = getenv("KFAC_EIG_GEMM");
+  return (e && !strcmp(e, "fp32")) ? (int)PREC_F32 : (int)PREC_BF16X6F;
+}();
 constexpr int TYP_SHIFT = 28;
 constexpr int SRC_MASK = (1 << TYP_SHIFT) - 1;
 
@@ -833,7 +841,7 @@ int enqueue(const DcPlan& P, hipStream_t stream) {
     const int sec_lds = L.mmax <= LDS_M_MAX;
     hipLaunchKernelGGL(dc_secular_kernel, dim3(cdiv(L.mmax, RPB), L.count), dim3(64 * RPB),
                        sec_lds ? (size_t)L.mmax * 16 : 0, stream, P.d_mats, nodes, sec_lds);
-    int err = kfac_pgemm(PREC_F32, TILE_F32, tab, 2 * L.count, L.gemm_tiles, nullptr, stream);
+    int err = kfac_pgemm(g_dc_prec, TILE_F32, tab, 2 * L.count, L.gemm_tiles, nullptr, stream);
     if (err) return err;
   }
   hipLaunchKernelGGL(dc_final_kernel, dim3(P.nmax, P.nmats), dim3(256), 0, stream, P.d_mats);
