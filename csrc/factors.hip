@@ -24,6 +24,8 @@
 // kfac/layers/utils.py:4-43,164-178 (A_conv = P^T P / (B * S^3), G_conv =
 // g^T g / (B * S^3), linear: a^T a / rows).
 #include "common.h"
+
+#include <cstdlib>
 #include "devtable.h"
 #include <type_traits>
 
@@ -377,8 +379,7 @@ __global__ __launch_bounds__(256) void syrk_patch_kernel(PatchArgs p) {
 // internal order back to the reference order (c, i, j) (factor_ema perm).
 // Requirements (checked on the host): 16-bit dtype, channel stride 1,
 // C % 8 == 0, every other stride % 8 == 0, 16-byte aligned base.
-constexpr int VBK = 64;                 // patch rows per k-step
-constexpr int VLDK = VBK + 8;           // 144-byte LDS rows: conflict-free b128 reads
+constexpr int VBK = 64;                 // patch rows per k-step (default configuration)
 
 __device__ __forceinline__ uint32_t pack_lo(uint32_t a, uint32_t b) { return (a & 0xffffu) | (b << 16); }
 __device__ __forceinline__ uint32_t pack_hi(uint32_t a, uint32_t b) { return (a >> 16) | (b & 0xffff0000u); }
@@ -387,11 +388,19 @@ __device__ __forceinline__ uint32_t u4get(const uint4& v, int i) {
 }
 
 // One (upper-triangular tile pair, row split) work item of syrk_vec.
-template <int DT>
+// VB: patch rows per k-step (LDS rows of VB + 8 elements keep the b128
+// fragment reads conflict-free); the next k-step's loads are in flight under
+// this one's MFMAs.  Measured on ResNet-50's factor step (SPLIT_ROWS 2048,
+// profiles/r3_factors_cfg*.log): 64 rows 4.11 ms; 128 rows 4.95 ms (two
+// workgroups per CU instead of three); two k-steps of loads in flight 7.9-8.0
+// ms (a second register set halves occupancy) -- 64 rows, one ahead, stays.
+template <int DT, int VB = VBK>
 __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int split,
                                               uint16_t* smem) {
+  constexpr int VLD = VB + 8;
+  constexpr int RG = VB / 64;           // 64-row groups per k-step and loader thread
   uint16_t* sA = smem;
-  uint16_t* sB = smem + BT * VLDK;
+  uint16_t* sB = smem + BT * VLD;
 
   int t = tile, ti = 0, rem = p.ntiles;
   while (t >= rem) { t -= rem; ++ti; --rem; }
@@ -402,7 +411,7 @@ __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int 
   long long r_end = r_begin + p.rows_per_split;
   if (r_end > p.M) r_end = p.M;
   if (r_begin >= r_end) return;
-  const int nk = (int)((r_end - r_begin + VBK - 1) / VBK);
+  const int nk = (int)((r_end - r_begin + VB - 1) / VB);
 
   const uint16_t* x = (const uint16_t*)p.x;
   const int tid = threadIdx.x;
@@ -414,7 +423,7 @@ __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int 
   // conflicts, 72 % of the kernel's LDS cycles, profiles/README.md.)  A wave's
   // global loads still read 128 contiguous bytes per patch row.
   const int op = tid >> 7;
-  const int rg = tid & 7;               // rows rg*8 .. rg*8+7 of the k-step
+  const int rg = tid & 7;               // rows rg*8 .. rg*8+7 of each 64-row group
   const int cc = (tid & 127) >> 3;      // columns cc*8 .. cc*8+7 of the tile
   const bool loader = !(diag && op == 1);
   const int gcol = (op ? tj : ti) * BT + cc * 8;
@@ -431,52 +440,58 @@ __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int 
   }
   const uint16_t one = DTypeTraits<DT>::from_f32(1.0f);
 
-  uint4 blk[8];
-  auto load_step = [&](int k) {
-    const long long r0 = r_begin + (long long)k * VBK + rg * 8;
-    long long rs = r0 < r_end ? r0 : r_begin;
-    const long long ohw = (long long)p.OH * p.OW;
-    long long b = rs / ohw;
-    int rr = (int)(rs - b * ohw);
-    int oh = rr / p.OW, ow = rr - oh * p.OW;
+  uint4 blk[RG][8];
+  auto load_step = [&](int k, uint4 (&dst)[RG][8]) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (loader && (r0 + q) < r_end) {
-        if (kind == 0) {
-          const int h = oh * p.sth - p.ph + di, w = ow * p.stw - p.pw + dj;
-          if ((unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W) {
-            const long long off = b * p.sb + (long long)(oh * p.sth - p.ph) * p.sh +
-                                  (long long)(ow * p.stw - p.pw) * p.sw + coff;
-            v = *(const uint4*)(x + off);
+    for (int g = 0; g < RG; ++g) {
+      const long long r0 = r_begin + (long long)k * VB + g * 64 + rg * 8;
+      long long rs = r0 < r_end ? r0 : r_begin;
+      const long long ohw = (long long)p.OH * p.OW;
+      long long b = rs / ohw;
+      int rr = (int)(rs - b * ohw);
+      int oh = rr / p.OW, ow = rr - oh * p.OW;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (loader && (r0 + q) < r_end) {
+          if (kind == 0) {
+            const int h = oh * p.sth - p.ph + di, w = ow * p.stw - p.pw + dj;
+            if ((unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W) {
+              const long long off = b * p.sb + (long long)(oh * p.sth - p.ph) * p.sh +
+                                    (long long)(ow * p.stw - p.pw) * p.sw + coff;
+              v = *(const uint4*)(x + off);
+            }
+          } else if (kind == 1) {
+            v.x = one;
           }
-        } else if (kind == 1) {
-          v.x = one;
         }
+        dst[g][q] = v;
+        if (++ow == p.OW) { ow = 0; if (++oh == p.OH) { oh = 0; ++b; } }
       }
-      blk[q] = v;
-      if (++ow == p.OW) { ow = 0; if (++oh == p.OH) { oh = 0; ++b; } }
     }
   };
-  auto store_step = [&]() {
+  auto store_step = [&](const uint4 (&src)[RG][8]) {
     if (!loader) return;
-    uint16_t* dst = (op ? sB : sA) + (cc * 8) * VLDK + rg * 8;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const int d = c >> 1;
-      uint4 o;
-      if (c & 1) {
-        o.x = pack_hi(u4get(blk[0], d), u4get(blk[1], d));
-        o.y = pack_hi(u4get(blk[2], d), u4get(blk[3], d));
-        o.z = pack_hi(u4get(blk[4], d), u4get(blk[5], d));
-        o.w = pack_hi(u4get(blk[6], d), u4get(blk[7], d));
-      } else {
-        o.x = pack_lo(u4get(blk[0], d), u4get(blk[1], d));
-        o.y = pack_lo(u4get(blk[2], d), u4get(blk[3], d));
-        o.z = pack_lo(u4get(blk[4], d), u4get(blk[5], d));
-        o.w = pack_lo(u4get(blk[6], d), u4get(blk[7], d));
+    for (int g = 0; g < RG; ++g) {
+      uint16_t* dst = (op ? sB : sA) + (cc * 8) * VLD + g * 64 + rg * 8;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const int d = c >> 1;
+        uint4 o;
+        if (c & 1) {
+          o.x = pack_hi(u4get(src[g][0], d), u4get(src[g][1], d));
+          o.y = pack_hi(u4get(src[g][2], d), u4get(src[g][3], d));
+          o.z = pack_hi(u4get(src[g][4], d), u4get(src[g][5], d));
+          o.w = pack_hi(u4get(src[g][6], d), u4get(src[g][7], d));
+        } else {
+          o.x = pack_lo(u4get(src[g][0], d), u4get(src[g][1], d));
+          o.y = pack_lo(u4get(src[g][2], d), u4get(src[g][3], d));
+          o.z = pack_lo(u4get(src[g][4], d), u4get(src[g][5], d));
+          o.w = pack_lo(u4get(src[g][6], d), u4get(src[g][7], d));
+        }
+        *(uint4*)(dst + c * VLD) = o;
       }
-      *(uint4*)(dst + c * VLDK) = o;
     }
   };
 
@@ -491,21 +506,17 @@ __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int 
       for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
   const uint16_t* sBr = diag ? sA : sB;
 
-  load_step(0);
-  for (int k = 0; k < nk; ++k) {
-    store_step();
-    __syncthreads();
-    if (k + 1 < nk) load_step(k + 1);
+  auto mfma_step = [&]() {
     typedef typename std::conditional<DT == KDT_BF16, bf16x8_t, f16x8_t>::type frag_t;
 #pragma unroll
-    for (int ks = 0; ks < VBK / 16; ++ks) {
+    for (int ks = 0; ks < VB / 16; ++ks) {
       frag_t a[2], bb[2];
 #pragma unroll
       for (int m = 0; m < 2; ++m)
-        a[m] = *(const frag_t*)(sA + (wr * 64 + m * 32 + lr) * VLDK + ks * 16 + lh * 8);
+        a[m] = *(const frag_t*)(sA + (wr * 64 + m * 32 + lr) * VLD + ks * 16 + lh * 8);
 #pragma unroll
       for (int n = 0; n < 2; ++n)
-        bb[n] = *(const frag_t*)(sBr + (wc * 64 + n * 32 + lr) * VLDK + ks * 16 + lh * 8);
+        bb[n] = *(const frag_t*)(sBr + (wc * 64 + n * 32 + lr) * VLD + ks * 16 + lh * 8);
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -516,6 +527,14 @@ __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int 
             acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[m], bb[n], acc[m][n], 0, 0, 0);
         }
     }
+  };
+
+  load_step(0, blk);
+  for (int k = 0; k < nk; ++k) {
+    store_step(blk);
+    __syncthreads();
+    if (k + 1 < nk) load_step(k + 1, blk);
+    mfma_step();
     __syncthreads();
   }
 
@@ -524,7 +543,7 @@ __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int 
 
 template <int DT>
 __global__ __launch_bounds__(256) void syrk_vec_kernel(PatchArgs p) {
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BT * VLDK];
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BT * (VBK + 8)];
   syrk_vec_tile<DT>(p, blockIdx.x, blockIdx.y, smem);
 }
 
@@ -546,9 +565,9 @@ struct SyrkBatch {
 };
 static_assert(sizeof(SyrkBatch) <= 4096, "kernel arguments are limited to 4 KB");
 
-template <int DT>
+template <int DT, int VB = VBK>
 __global__ __launch_bounds__(256) void syrk_vec_grouped_kernel(const SyrkBatch* __restrict__ batch) {
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BT * VLDK];
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BT * (VB + 8)];
   const SyrkProblem* t = batch->prob;
   const int count = batch->count;
   int lo = 0, hi = count - 1;
@@ -560,7 +579,7 @@ __global__ __launch_bounds__(256) void syrk_vec_grouped_kernel(const SyrkBatch* 
   const SyrkProblem& P = t[lo];
   const int local = b - P.block_begin;
   const int tiles = P.p.ntiles * (P.p.ntiles + 1) / 2;
-  syrk_vec_tile<DT>(P.p, local % tiles, local / tiles, smem);
+  syrk_vec_tile<DT, VB>(P.p, local % tiles, local / tiles, smem);
 }
 
 // Grouped EMA (with the internal->reference permutation): one block row per
