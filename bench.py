@@ -37,6 +37,7 @@ from distributed_kfac_pytorch_amd.parallel import launch  # noqa: E402
 from distributed_kfac_pytorch_amd import graphs  # noqa: E402
 from distributed_kfac_pytorch_amd.parallel import grad_sync as grad_sync_mod  # noqa: E402
 from distributed_kfac_pytorch_amd.parallel import overlap  # noqa: E402
+from distributed_kfac_pytorch_amd.ops import mixed  # noqa: E402
 
 METRIC = 'images/sec (whole node) ResNet-50 K-FAC+SGD'
 # the reference K-FAC on one MI355X, same config and timing (not a BASELINE number)
@@ -103,6 +104,11 @@ def parse():
     ap.add_argument('--fused-sgd', type=int, default=1,
                     help='torch.optim.SGD(fused=True): one multi-tensor kernel for the whole '
                          'momentum + weight-decay update (same math as the reference optimizer)')
+    ap.add_argument('--bf16-weights', type=int, default=1,
+                    help='graphed steps: Conv/Linear weights stored in bf16 with fp32 masters in '
+                         'the optimizer and K-FAC (ops/mixed.BF16Weights): the numerics of '
+                         'autocast without its ~110 per-tensor cast launches per step, two '
+                         'grouped cast launches instead')
     ap.add_argument('--ddp', action='store_true',
                     help='eager torch DDP instead of the graphed flat-arena all-reduce')
     return ap.parse_args()
@@ -128,13 +134,15 @@ def step_kind(pre):
 
 
 def time_sgd_only(args, model, opt, pre, forward_backward, grad_sync, use_graphs, device,
-                  communicate=None, stream=None):
+                  communicate=None, stream=None, weights=None):
     """The same training step without K-FAC (hooks removed, plain SGD update),
     timed over the same number of steps: the baseline for kfac_step_ms."""
     pre.remove_hooks()
 
     def update():
         opt.step()
+        if weights is not None:
+            weights.master_to_model()
 
     if grad_sync is not None:
         step = graphs.GraphedTrainStep(None, None, [opt], enabled=use_graphs,
@@ -182,6 +190,16 @@ def main():
     model = model.to(memory_format=mf)
     use_graphs = bool(args.graphs) and device.type == 'cuda' and not args.profile_phases
     grad_sync = None
+    # bf16-stored weights + fp32 masters (autocast numerics, two grouped cast
+    # launches per step instead of one per tensor and direction); the masters
+    # are derived after rank 0's weights are broadcast
+    weights = None
+    if args.bf16_weights and device.type == 'cuda' and use_graphs and not args.ddp \
+            and not args.overlap_precond:
+        if world > 1:
+            grad_sync_mod.GradientAllreduce.broadcast_model(model)
+        weights = mixed.BF16Weights(model)
+    bcast = None if weights is not None else 0
     if args.ddp or not use_graphs:
         model = launch.wrap_ddp(model, device, broadcast_buffers=False)
     elif world > 1 and args.overlap_grad_comm and hasattr(model, 'forward_bottom'):
@@ -189,15 +207,18 @@ def main():
         # while the bottom half's backward replays (parallel/overlap.py)
         grad_sync = overlap.SplitBackward(
             model, lambda out: F.cross_entropy(out, y, label_smoothing=0.1), lambda: x,
-            autocast=torch.bfloat16)
+            autocast=torch.bfloat16, weights=weights, broadcast_from=bcast)
     elif world > 1:
         # one flat-arena all-reduce between graph replays (parallel/grad_sync.py)
-        grad_sync = grad_sync_mod.GradientAllreduce(model)
+        grad_sync = grad_sync_mod.GradientAllreduce(
+            model, params=weights.parameters(model) if weights is not None else None,
+            broadcast_from=bcast)
     base_lr = 0.0125 * world
     sgd_kw = dict(lr=base_lr, momentum=0.9, weight_decay=5e-5)
     if args.fused_sgd and device.type == 'cuda':
         sgd_kw['fused'] = True
-    opt = torch.optim.SGD(model.parameters(), **sgd_kw)
+    opt = torch.optim.SGD(weights.parameters(model) if weights is not None
+                          else model.parameters(), **sgd_kw)
     pre = None
     if not args.no_kfac:
         method = {'comm-opt': kfac.CommMethod.COMM_OPT, 'mem-opt': kfac.CommMethod.MEM_OPT,
@@ -213,6 +234,8 @@ def main():
                         inverse_lag=args.inverse_lag,
                         overlap_precondition=bool(args.overlap_precond) and world == 1,
                         use_hip_graphs=not os.environ.get('KFAC_NO_TAIL_GRAPH'))
+        if weights is not None:
+            pre.set_grad_params(weights.grad_params())
 
     B, S = args.batch_size, args.image_size
     g = torch.Generator(device=device).manual_seed(rank)
@@ -222,18 +245,28 @@ def main():
     def forward_backward():
         if grad_sync is not None:
             grad_sync.zero_grad()            # one fill of the gradient arena
+            if weights is not None:
+                weights.zero_model_grads()
+        elif weights is not None:
+            # the module gradients (bf16 weights, fp32 BN); the masters' .grad
+            # is overwritten by grads_to_master
+            model.zero_grad(set_to_none=bool(args.set_to_none))
         else:
             opt.zero_grad(set_to_none=bool(args.set_to_none))
         with torch.autocast(device_type=device.type, dtype=torch.bfloat16):
             out = model(x)
             loss = F.cross_entropy(out, y, label_smoothing=0.1)
         loss.backward()
+        if weights is not None:
+            weights.grads_to_master()
         return loss
 
     def update():
         if pre is not None:
             pre.step()
         opt.step()
+        if weights is not None:
+            weights.master_to_model()
 
     def train_step():
         loss = forward_backward()
@@ -302,7 +335,7 @@ def main():
         # nodes live on it (a new stream makes every backward sync across)
         sgd_ms = time_sgd_only(args, model, opt, pre, fb_segments, grad_sync, use_graphs,
                                device, communicate=comm_segments,
-                               stream=getattr(step, 'side', None))
+                               stream=getattr(step, 'side', None), weights=weights)
     if rank == 0:
         rec = {
             'metric': METRIC if pre is not None else 'images/sec (whole node) ResNet-50 SGD-only',
@@ -331,6 +364,8 @@ def main():
                            'overlap_precondition': bool(args.overlap_precond) and world == 1},
                        'hip_graphs': use_graphs,
                        'fused_sgd': bool(args.fused_sgd and device.type == 'cuda'),
+                       'weights': 'bf16 + fp32 masters' if weights is not None
+                                  else 'fp32 (autocast casts)',
                        'grad_allreduce': 'ddp' if grad_sync is None and world > 1 else
                                          (('split-backward-overlap' if split else 'flat-arena')
                                           if world > 1 else None),

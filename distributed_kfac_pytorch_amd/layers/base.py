@@ -257,25 +257,38 @@ class KFACLayer(object):
         return inv.to(self.inv_dtype)
 
     # -------------------------------------------------------- preconditioning
+    # The parameters whose .grad K-FAC reads and rewrites: the module's own, or
+    # fp32 masters of bf16-stored weights (KFAC.set_grad_params, ops/mixed.py)
+    grad_weight_param = None
+    grad_bias_param = None
+
+    def _wparam(self):
+        return self.grad_weight_param if self.grad_weight_param is not None else self.module.weight
+
+    def _bparam(self):
+        return self.grad_bias_param if self.grad_bias_param is not None else self.module.bias
+
     def _get_weight_grad(self):
-        return self.module.weight.grad
+        return self._wparam().grad
 
     def _get_bias_grad(self):
-        return self.module.bias.grad
+        return self._bparam().grad
 
     def _set_weight_grad(self, grad):
-        g = self.module.weight.grad
+        prm = self._wparam()
+        g = prm.grad
         if g is not None and g.shape == grad.shape:
             g.copy_(grad)
         else:
-            self.module.weight.grad = grad.contiguous()
+            prm.grad = grad.contiguous()
 
     def _set_bias_grad(self, grad):
-        g = self.module.bias.grad
+        prm = self._bparam()
+        g = prm.grad
         if g is not None and g.shape == grad.shape:
             g.copy_(grad)
         else:
-            self.module.bias.grad = grad.contiguous()
+            prm.grad = grad.contiguous()
 
     def weight_grad_2d(self):
         g = self._get_weight_grad()

@@ -44,7 +44,7 @@ class Conv2dLayer(KFACLayer):
                          self.padding[0], self.padding[1], m.dilation[0], m.dilation[1])
 
     def weight_grad_2d(self):
-        g = self.module.weight.grad
+        g = self._get_weight_grad()
         return g.reshape(g.size(0), -1)
 
     def _patches(self, x):

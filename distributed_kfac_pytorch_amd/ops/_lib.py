@@ -105,6 +105,7 @@ _SIGS = {
     'kfac_split_record_size': [],
     'kfac_graph_fix_memsets': [c_vp, c_int, ctypes.POINTER(c_ll)],
     'kfac_dc_batched': [ctypes.POINTER(DcRecord), c_int, c_int, c_vp],
+    'kfac_cast_grouped': [c_vp, c_int, c_int, c_vp],
     'kfac_reduce_batched': [ctypes.POINTER(ReduceRecord), c_int, c_int, c_vp],
     'kfac_reduce_prepare': [ctypes.POINTER(ReduceRecord), c_int],
     'kfac_reduce_ws_floats': [c_int],

@@ -58,6 +58,16 @@ class GradientAllreduce(object):
                 for t in list(model.parameters()) + list(model.buffers()):
                     dist.broadcast(t.data, src=broadcast_from, group=group)
 
+    @staticmethod
+    def broadcast_model(model, group=None, src=0):
+        """Broadcast every parameter and buffer of `model` from rank `src`
+        (what construction does with broadcast_from=src), e.g. before fp32
+        masters are derived from the weights (ops/mixed.BF16Weights)."""
+        if dist.is_initialized() and dist.get_world_size(group) > 1:
+            with torch.no_grad():
+                for t in list(model.parameters()) + list(model.buffers()):
+                    dist.broadcast(t.data, src=src, group=group)
+
     def zero_grad(self):
         """One fill per arena instead of one per parameter."""
         for arena in self.arenas:

@@ -34,14 +34,24 @@ class SplitBackward(object):
     input tensor; autocast: dtype or None.
     """
 
-    def __init__(self, model, loss_fn, inputs, autocast=None, group=None):
+    def __init__(self, model, loss_fn, inputs, autocast=None, group=None, weights=None,
+                 broadcast_from=0):
         self.model = model
         self.loss_fn = loss_fn
         self.inputs = inputs
         self.autocast = autocast
         bottom, top = model.split_parameters()
+        # bf16-stored weights (ops/mixed.BF16Weights): each segment widens its
+        # bf16 weight gradients into the fp32 masters, and the masters' .grad
+        # are what the arenas all-reduce (fp32, as with autocast)
+        self.w_top = weights.subset(top) if weights is not None else None
+        self.w_bottom = weights.subset(bottom) if weights is not None else None
+        if weights is not None:
+            top = [weights.master_of(p) for p in top]
+            bottom = [weights.master_of(p) for p in bottom]
         # top first: rank 0's parameters / buffers are broadcast once
-        self.sync_top = GradientAllreduce(model, group=group, params=top)
+        self.sync_top = GradientAllreduce(model, group=group, params=top,
+                                          broadcast_from=broadcast_from)
         self.sync_bottom = GradientAllreduce(model, group=group, params=bottom,
                                              broadcast_from=None)
         self._mid = None
@@ -51,6 +61,9 @@ class SplitBackward(object):
     def zero_grad(self):
         self.sync_top.zero_grad()
         self.sync_bottom.zero_grad()
+        for w in (self.w_top, self.w_bottom):
+            if w is not None:
+                w.zero_model_grads()
 
     def segment_top(self):
         self.zero_grad()
@@ -62,11 +75,15 @@ class SplitBackward(object):
             mid_in = mid.detach().requires_grad_(True)
             loss = self.loss_fn(self.model.forward_top(mid_in))
         loss.backward()
+        if self.w_top is not None:
+            self.w_top.grads_to_master()
         self._mid, self._mid_in = mid, mid_in
         return loss
 
     def segment_bottom(self):
         self._mid.backward(self._mid_in.grad)
+        if self.w_bottom is not None:
+            self.w_bottom.grads_to_master()
         return None
 
     def comm_top(self):

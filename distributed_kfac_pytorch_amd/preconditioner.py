@@ -492,6 +492,25 @@ class KFAC(optim.Optimizer):
             with self._no_autocast(grad):
                 layer.update_G_factor(alpha=self.param_groups[0]['factor_decay'])
 
+    def set_grad_params(self, mapping):
+        """Precondition the gradients of other parameters than the modules'
+        own: `mapping` {module parameter: parameter whose .grad K-FAC reads and
+        rewrites}, e.g. the fp32 masters of bf16-stored weights
+        (ops/mixed.BF16Weights.grad_params()).  Factors still come from the
+        modules' hooks.  The caller fills the masters' .grad between backward
+        and step() (BF16Weights.grads_to_master)."""
+        if self.overlap_precondition:
+            raise ValueError('overlap_precondition launches from gradient hooks on the module '
+                             'parameters; it cannot precondition remapped gradients')
+        for layer in self.layers:
+            m = layer.module
+            layer.grad_weight_param = mapping.get(m.weight)
+            bias = getattr(m, 'bias', None)
+            layer.grad_bias_param = mapping.get(bias) if bias is not None else None
+        self._graph = None            # the tail graph addressed the old .grad tensors
+        if self.fused is not None:
+            self.fused._gather_sig = None
+
     def remove_hooks(self):
         for h in self._hook_handles:
             h.remove()

@@ -222,6 +222,47 @@ def split_backward(rank, world, port, out_dir, cfg):
     dist.destroy_process_group()
 
 
+def split_backward_bf16_weights(rank, world, port, out_dir, cfg):
+    """SplitBackward over bf16-stored weights (ops/mixed.BF16Weights: each
+    segment widens its weight gradients into the fp32 masters, the arenas
+    all-reduce the masters' gradients) vs fp32 weights under bf16 autocast
+    with one backward + one flat-arena all-reduce: identical gradients."""
+    _init(rank, world, port)
+    import copy
+    import torch.nn.functional as F
+    from distributed_kfac_pytorch_amd.models import resnet
+    from distributed_kfac_pytorch_amd.ops.mixed import BF16Weights
+    from distributed_kfac_pytorch_amd.parallel.grad_sync import GradientAllreduce
+    from distributed_kfac_pytorch_amd.parallel.overlap import SplitBackward
+    torch.manual_seed(rank)           # ranks start different: rank 0's weights win
+    m1 = resnet.resnet_tiny(num_classes=10)
+    m2 = copy.deepcopy(m1)
+    GradientAllreduce.broadcast_model(m1)
+    w = BF16Weights(m1)
+    g = torch.Generator().manual_seed(rank)
+    x = torch.randn(4, 3, 32, 32, generator=g)
+    y = torch.randint(0, 10, (4,), generator=g)
+    sb = SplitBackward(m1, lambda out: F.cross_entropy(out, y), lambda: x,
+                       autocast=torch.bfloat16, weights=w, broadcast_from=None)
+    loss1 = None
+    for i, (seg, cm) in enumerate(zip(sb.segments, sb.communicate)):
+        out = seg()
+        loss1 = out if i == 0 else loss1
+        cm()
+    ga = GradientAllreduce(m2)       # broadcasts rank 0's fp32 weights
+    ga.zero_grad()
+    with torch.autocast('cpu', dtype=torch.bfloat16):
+        loss2 = F.cross_entropy(m2(x), y)
+    loss2.backward()
+    ga()
+    same = all(torch.equal(w.master_of(p).grad, q.grad)
+               for p, q in zip(m1.parameters(), m2.parameters()))
+    torch.save({'same': same, 'loss': (loss1.item(), loss2.item())},
+               os.path.join(out_dir, 'rank{}.pt'.format(rank)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def example_graphs(rank, world, port, out_dir, cfg):
     """The ImageNet example at world 2 (gloo), --graphs 1 (flat-arena gradient
     all-reduce between step segments, factors in hooks, deferred factor

@@ -186,6 +186,16 @@ def test_split_backward_overlap_equals_single(tmp_path):
         assert res['loss'][0] == res['loss'][1]
 
 
+def test_split_backward_bf16_weights_equals_autocast(tmp_path):
+    """bf16-stored weights + fp32 masters through the overlapped two-segment
+    all-reduce give the gradients of fp32 weights under bf16 autocast."""
+    _spawn(_dist_worker.split_backward_bf16_weights, 2, tmp_path, {})
+    for r in range(2):
+        res = torch.load(os.path.join(str(tmp_path), 'rank{}.pt'.format(r)), weights_only=True)
+        assert res['same'], res
+        assert res['loss'][0] == res['loss'][1]
+
+
 def test_deferred_factor_allreduce(tmp_path):
     """Verdict r2 item 3: the factor all-reduce is issued in step() and
     joined only by its consumers (next EMA / inverse update / state_dict):
