@@ -282,7 +282,9 @@ def main():
         step = graphs.GraphedTrainStep(None, pre, [opt], enabled=use_graphs,
                                        forward_backward=fb_segments,
                                        communicate=comm_segments, update=update,
-                                       phased_update=True)
+                                       phased_update=True,
+                                       post_update=weights.master_to_model
+                                       if weights is not None else None)
     else:
         step = graphs.GraphedTrainStep(train_step, pre, [opt], enabled=use_graphs)
 

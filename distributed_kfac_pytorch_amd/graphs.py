@@ -85,7 +85,7 @@ def _world_size():
 class GraphedTrainStep(object):
     def __init__(self, step_fn=None, preconditioner=None, optimizers=(), warmup=2, enabled=True,
                  forward_backward=None, communicate=None, update=None, phased_update=False,
-                 stream=None):
+                 stream=None, post_update=None):
         if step_fn is None and (forward_backward is None or update is None):
             raise ValueError('give step_fn, or forward_backward and update')
         self.step_fn = step_fn
@@ -98,6 +98,10 @@ class GraphedTrainStep(object):
         else:
             self.fbs, self.comms = [forward_backward], [communicate]
         self.fb, self.comm, self.update = forward_backward, communicate, update
+        # phased updates run KFAC.step_finish + the optimizers themselves (not
+        # `update`): `post_update` is what `update` does after the optimizer
+        # (e.g. ops/mixed.BF16Weights.master_to_model)
+        self.post_update = post_update
         self.segmented = step_fn is None
         self.pre = preconditioner
         # 'force' phases the update even when it issues no collective (tests)
@@ -177,6 +181,10 @@ class GraphedTrainStep(object):
         pre = self.pre
         if pre is None:
             return True
+        if getattr(pre, 'comm_check', False):
+            # the consistency checks join collectives and read checksums on
+            # the host: never inside a capture (KFAC_COMM_CHECK=1 debug runs)
+            return False
         from . import comm
         if comm.backend is None or comm.backend.size() == 1:
             return True
@@ -288,6 +296,8 @@ class GraphedTrainStep(object):
         self.pre.step_finish()
         for opt in self.optimizers:
             opt.step()
+        if self.post_update is not None:
+            self.post_update()
 
     def _eager(self):
         if not self.enabled:
