@@ -42,6 +42,11 @@ from distributed_kfac_pytorch_amd.ops import mixed  # noqa: E402
 METRIC = 'images/sec (whole node) ResNet-50 K-FAC+SGD'
 # the reference K-FAC on one MI355X, same config and timing (not a BASELINE number)
 REFERENCE_MI355X_IMG_S = 296.8
+# ...its step time by kind (ms) and the same model's stock-module SGD-only eager
+# step (profiles/r2_reference_kfac_mi355x.log, profiles/README.md): the
+# reference's K-FAC cost per step kind is the difference
+REFERENCE_MI355X_STEP_MS = {'plain': 25.283, 'factor': 45.982, 'inverse': 1655.206}
+REFERENCE_MI355X_SGD_MS = 13.8
 
 
 def parse():
@@ -401,6 +406,17 @@ def main():
             rec['reference_kfac_same_gpu'] = {
                 'images_per_sec': REFERENCE_MI355X_IMG_S,
                 'speedup': round(value / REFERENCE_MI355X_IMG_S, 2)}
+            if sgd_ms is not None and per_kind:
+                # K-FAC's own cost per step kind (step minus the same model's
+                # SGD-only step), ours vs the reference's: separates the K-FAC
+                # speedup from the model-side one (graphs, channels_last, BN)
+                ours = {k: round(sum(v) / len(v) - sgd_ms, 3) for k, v in per_kind.items()}
+                rec['reference_kfac_same_gpu']['kfac_cost_ms_by_kind'] = {
+                    k: {'ours': ours[k],
+                        'reference': round(REFERENCE_MI355X_STEP_MS[k] - REFERENCE_MI355X_SGD_MS, 3),
+                        'speedup': round((REFERENCE_MI355X_STEP_MS[k] - REFERENCE_MI355X_SGD_MS) /
+                                         max(ours[k], 1e-3), 2)}
+                    for k in ours if k in REFERENCE_MI355X_STEP_MS}
         if phases is not None:
             rec['kfac_phase_ms_total'] = {k: round(v, 2) for k, v in phases.items()}
             rec['kfac_phase_ms_per_step'] = round(sum(phases.values()) / args.steps, 3)

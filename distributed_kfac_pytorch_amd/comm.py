@@ -71,6 +71,8 @@ def _can_split():
     with dist.split_group.  Identical on every rank."""
     if not (_dist_ready() and hasattr(dist, 'split_group')):
         return False
+    if os.environ.get('KFAC_COMM_SPLIT', '1') == '0':
+        return False        # plain new_group communicators (debugging / old RCCL)
     if dist.get_backend() != 'nccl':
         return False
     pg = dist.distributed_c10d._get_default_group()
@@ -83,7 +85,13 @@ def _new_world_group():
         return None
     ranks = list(range(world))
     if _can_split():
-        return dist.split_group(split_ranks=[ranks], group_desc='kfac_world')
+        try:
+            return dist.split_group(split_ranks=[ranks], group_desc='kfac_world')
+        except Exception as e:   # pragma: no cover - depends on the RCCL build
+            # an API-level refusal is the same on every rank: all fall back
+            import warnings
+            warnings.warn('ncclCommSplit of the K-FAC world failed ({}); using new_group'
+                          .format(e))
     return dist.new_group(ranks)
 
 
