@@ -68,32 +68,62 @@ __global__ __launch_bounds__(256) void make_v_kernel(float* A, int lda, long lon
 
 // T_k (upper triangular, ROW-major BT x BT, zero beyond kb) from
 // G_k = V_k V_k^T (row-major, ld BT) and tau (LAPACK larft, forward /
-// columnwise): T(i,i) = tau_i, T(0:i, i) = -tau_i T(0:i, 0:i) G(0:i, i).
-__global__ __launch_bounds__(BT) void larft_kernel(const float* G, float* T, const float* tau,
+// columnwise).  larft's column recursion T(0:i, i) = -tau_i T(0:i, 0:i)
+// G(0:i, i) is BT dependent steps (~320 us per launch at BT = 128,
+// profiles/r3_eig_kernel_stats.csv); the same T is the inverse of the upper
+// triangular U = diag(1 / tau) + striu(G), computed here by recursive
+// doubling: T12 = -T11 U12 T22 for diagonal blocks of 1, 2, 4, .. 64 --
+// seven levels of two small products, all 256 threads busy.  A reflector
+// with tau = 0 (H_i = I) has row and column i of T zero: its row / column of
+// U is decoupled (U_ii = 1) and zeroed in T afterwards.
+constexpr int LT = 256;   // larft threads
+__global__ __launch_bounds__(LT) void larft_kernel(const float* G, float* T, const float* tau,
                                                    int n, int nblk) {
+  __shared__ float sU[BT][BT + 1];
   __shared__ float sT[BT][BT + 1];
-  __shared__ float sG[BT][BT + 1];
-  const int k = blockIdx.x, mat = blockIdx.y, r = threadIdx.x;
+  __shared__ float sW[BT / 2][BT / 2 + 1];
+  __shared__ int live[BT];
+  const int k = blockIdx.x, mat = blockIdx.y, tid = threadIdx.x;
   const long long off = ((long long)mat * nblk + k) * BT * BT;
   const int j0 = k * BT;
   const int kb = (n - j0) < BT ? (n - j0) : BT;
-  for (int i = 0; i < BT; ++i) {
-    sG[r][i] = (r < kb && i < kb) ? G[off + (long long)r * BT + i] : 0.f;
-    sT[r][i] = 0.f;
+  const float* tj = tau + (long long)mat * n + j0;
+  for (int r = tid; r < BT; r += LT) live[r] = (r < kb) && (tj[r] != 0.f);
+  __syncthreads();
+  for (int e = tid; e < BT * BT; e += LT) {
+    const int r = e / BT, c = e % BT;
+    float u = 0.f;
+    if (r == c) u = live[r] ? 1.f / tj[r] : 1.f;
+    else if (c > r && live[r] && live[c]) u = G[off + (long long)r * BT + c];
+    sU[r][c] = u;
+    sT[r][c] = (r == c) ? 1.f / u : 0.f;
   }
   __syncthreads();
-  const float* tj = tau + (long long)mat * n + j0;
-  for (int i = 0; i < kb; ++i) {
-    const float ti = tj[i];
-    float acc = 0.f;
-    if (r < i)
-      for (int q = r; q < i; ++q) acc += sT[r][q] * sG[q][i];
+  for (int b = 1; b < BT; b *= 2) {
+    const int pairs = BT / (2 * b), per = b * b;
+    // W = U12 T22 for every pair (U12: rows p0 .. p0+b, cols p0+b .. p0+2b)
+    for (int e = tid; e < pairs * per; e += LT) {
+      const int p = e / per, w = e % per, r = w / b, c = w % b;
+      const int p0 = 2 * p * b;
+      float acc = 0.f;
+      for (int q = 0; q <= c; ++q) acc = fmaf(sU[p0 + r][p0 + b + q], sT[p0 + b + q][p0 + b + c], acc);
+      sW[(p * b + r) % (BT / 2)][c] = acc;
+    }
     __syncthreads();
-    if (r < i) sT[r][i] = -ti * acc;
-    else if (r == i) sT[r][i] = ti;
+    // T12 = -T11 W
+    for (int e = tid; e < pairs * per; e += LT) {
+      const int p = e / per, w = e % per, r = w / b, c = w % b;
+      const int p0 = 2 * p * b;
+      float acc = 0.f;
+      for (int q = r; q < b; ++q) acc = fmaf(sT[p0 + r][p0 + q], sW[(p * b + q) % (BT / 2)][c], acc);
+      sT[p0 + r][p0 + b + c] = -acc;
+    }
     __syncthreads();
   }
-  for (int i = 0; i < BT; ++i) T[off + (long long)r * BT + i] = sT[r][i];
+  for (int e = tid; e < BT * BT; e += LT) {
+    const int r = e / BT, c = e % BT;
+    T[off + (long long)r * BT + c] = (live[r] && live[c]) ? sT[r][c] : 0.f;
+  }
 }
 
 struct BtArgs {
@@ -226,7 +256,7 @@ int run_plan(const BtArgs& a, const BtPlan& plan, hipStream_t stream) {
         err = (int)hipGetLastError();
         break;
       default:
-        hipLaunchKernelGGL(larft_kernel, dim3(nblk, a.batch), dim3(BT), 0, stream, a.Tbuf,
+        hipLaunchKernelGGL(larft_kernel, dim3(nblk, a.batch), dim3(LT), 0, stream, a.Tbuf,
                            a.Tbuf + tstride * a.batch, a.tau, a.n, nblk);
         err = (int)hipGetLastError();
     }

@@ -8,6 +8,9 @@
 // PREC_BF16X6F: the bf16x6 products of PREC_BF16X6 on fp32 operands, split
 // into the three planes while they are staged into LDS (4 B per element
 // from memory instead of 6, no plane copies of the operands)
+// (a register-split variant -- fp32 LDS image, planes split per MFMA
+// fragment -- measured 2.55 vs 2.28 ms on ResNet-50: 2.3x the VALU work,
+// profiles/r3_pgemm_mode_r.log; removed)
 enum { PREC_F32 = 0, PREC_BF16X3 = 1, PREC_BF16X6 = 2, PREC_BF16X6F = 3 };
 // EPI_SUB: C -= A B^T (f32); EPI_ATOMIC: C += A B^T with f32 atomics (split-K)
 enum { EPI_STORE = 0, EPI_HADAMARD = 1, EPI_HADAMARD_VEC = 2, EPI_FINAL = 3, EPI_SUB = 4,

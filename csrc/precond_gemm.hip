@@ -118,7 +118,14 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   constexpr bool IMG16 = SPL || X6F;              // bf16 plane image in LDS
   constexpr int NT = 64 * WM * WN;                // threads
   constexpr int MI = BM / WM / 32, NJ = BN / WN / 32;
-  constexpr int LDB16 = TK + 8;   // 80-byte rows: conflict-free ds_read_b128 (guide: LDS banking)
+  // 80-byte rows: conflict-free ds_read_b128 (guide: LDS banking).  X6F
+  // writes 8-byte plane quads, and 80-byte rows put the two rows of a
+  // ds_write_b64 lane group on overlapping banks (bank-conflict cycles ~ LDS-
+  // active cycles, profiles/r3_pmc_x6f_a.csv): X6F keeps 64-byte rows with the
+  // 16-byte pieces XOR-swizzled by (row >> 2) & 3 -- writes (two rows = 32
+  // banks) and the b128 fragment reads (16 rows = 16 disjoint 4-bank spans)
+  // both conflict-free
+  constexpr int LDB16 = (PREC == PREC_BF16X6F) ? TK : TK + 8;
   constexpr int LDF32 = TK + 4;   // 16-byte aligned chunk writes
   // one LDS array (guide: a second __shared__ object can de-pipeline loads)
   constexpr int PL = (X6 || X6F) ? 3 : (X3 ? 2 : 1);   // planes
@@ -161,6 +168,13 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   constexpr bool PLANE_CT = (BM * CPR) % NT == 0 && (BN * CPR) % NT == 0;
   static_assert(!X6 || PLANE_CT, "3-plane loader needs whole chunk rounds per plane");
   constexpr int ESZ = SPL ? 2 : 4;
+  // chunk c -> (row, k offset): chunks fastest, a wave's global loads read
+  // whole 128-byte row segments
+  auto chunk_rc = [&](int c, int rows, int& row, int& kof) {
+    const int cc = c % (rows * CPR);
+    row = cc / CPR;
+    kof = (cc % CPR) * (16 / ESZ);
+  };
   // third plane (X6): one plane stride past the second
   const AS1 unsigned char* const A2 = Al + (Al - Ah);
   const AS1 unsigned char* const B2 = Bl + (Bl - Bh);
@@ -174,14 +188,16 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
 #pragma unroll
   for (int q = 0; q < QA; ++q) {
     const int c = tid + NT * q;
-    const int row = (c % (BM * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
+    int row, kof;
+    chunk_rc(c, BM, row, kof);
     oka[q] = m0 + row < M;
     offa[q] = ((unsigned)(oka[q] ? m0 + row : m0) * (unsigned)lda + kof) * ESZ;
   }
 #pragma unroll
   for (int q = 0; q < QB; ++q) {
     const int c = tid + NT * q;
-    const int row = (c % (BN * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
+    int row, kof;
+    chunk_rc(c, BN, row, kof);
     okb[q] = n0 + row < N;
     offb[q] = ((unsigned)(okb[q] ? n0 + row : n0) * (unsigned)ldb + kof) * ESZ;
   }
@@ -206,6 +222,10 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
     }
   };
   // LDS image: [A planes | B planes] rows of LDB16 bf16 (X3 / X6) or [A | B] rows of LDF32 f32
+  // X6F: element offset of k offset `k` (a multiple of 4) in LDS row `row`
+  auto x6f_off = [&](int row, int k) -> int {
+    return ((((k >> 3) ^ (row >> 2)) & 3) << 3) | (k & 7);
+  };
   // X6F: four fp32 values -> hi / mid / lo bf16 quads, one 8-byte LDS write
   // per plane (the split of split_bf16_3, so results equal PREC_BF16X6's)
   auto store_split = [&](uint16_t* dst, long long plane_stride, const u32x4n& v) {
@@ -224,17 +244,21 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
       const int c = tid + NT * q;
-      const int plane = c / (BM * CPR), row = (c % (BM * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
-      if (X6F) store_split((uint16_t*)img + row * LDB16 + kof, (long long)BM * LDB16, ra[q]);
+      const int plane = c / (BM * CPR);
+      int row, kof;
+      chunk_rc(c, BM, row, kof);
+      if (X6F) store_split((uint16_t*)img + row * LDB16 + x6f_off(row, kof), (long long)BM * LDB16, ra[q]);
       else if (SPL) *(u32x4n*)((uint16_t*)img + (plane * BM + row) * LDB16 + kof) = ra[q];
       else *(u32x4n*)((float*)img + row * LDF32 + kof) = (row & 16) ? ra[q].zwxy : ra[q];
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
       const int c = tid + NT * q;
-      const int plane = c / (BN * CPR), row = (c % (BN * CPR)) / CPR, kof = (c % CPR) * (16 / ESZ);
-      if (X6F) store_split((uint16_t*)img + (PL * BM + row) * LDB16 + kof, (long long)BN * LDB16,
-                           rb[q]);
+      const int plane = c / (BN * CPR);
+      int row, kof;
+      chunk_rc(c, BN, row, kof);
+      if (X6F) store_split((uint16_t*)img + (PL * BM + row) * LDB16 + x6f_off(row, kof),
+                           (long long)BN * LDB16, rb[q]);
       else if (SPL) *(u32x4n*)((uint16_t*)img + (PL * BM + plane * BN + row) * LDB16 + kof) = rb[q];
       else *(u32x4n*)((float*)img + (BM + row) * LDF32 + kof) = (row & 16) ? rb[q].zwxy : rb[q];
     }
@@ -298,13 +322,15 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
         bf16x8_t bp[3][NJ];
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-          const int off = (brow0 + j * 32 + lr) * LDB16 + kk * 16 + lh * 8;
+          const int row = brow0 + j * 32 + lr;
+          const int off = row * LDB16 + (X6F ? x6f_off(row, kk * 16 + lh * 8) : kk * 16 + lh * 8);
 #pragma unroll
           for (int p = 0; p < 3; ++p) bp[p][j] = *(const bf16x8_t*)(sB0 + p * BN * LDB16 + off);
         }
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
-          const int off = (arow0 + i * 32 + lr) * LDB16 + kk * 16 + lh * 8;
+          const int row = arow0 + i * 32 + lr;
+          const int off = row * LDB16 + (X6F ? x6f_off(row, kk * 16 + lh * 8) : kk * 16 + lh * 8);
           bf16x8_t ap[3];
 #pragma unroll
           for (int p = 0; p < 3; ++p) ap[p] = *(const bf16x8_t*)(sA0 + p * BM * LDB16 + off);

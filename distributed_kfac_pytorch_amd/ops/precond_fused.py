@@ -43,8 +43,9 @@ __all__ = ['FusedPreconditioner', 'PRECISIONS']
 
 PRECISIONS = {'fp32': 0, 'bf16x3': 1, 'bf16x6': 2}
 PLANES = {'fp32': 1, 'bf16x3': 2, 'bf16x6': 3}
-PREC_BF16X6F = 3   # csrc/pgemm.h: bf16x6 products on fp32 operands
-X6_PLANES = bool(int(os.environ.get('KFAC_X6_PLANES', '0')))
+PREC_BF16X6F = 3   # csrc/pgemm.h: bf16x6 products on fp32 operands, planes split into LDS
+# KFAC_X6_PLANES=1: the round-2 kernel on plane-stored operands (A/B comparisons)
+X6_PLANES = os.environ.get('KFAC_X6_PLANES') == '1'
 X6_BIG = int(os.environ['KFAC_X6_BIG']) if os.environ.get('KFAC_X6_BIG') else None
 EPI_STORE, EPI_HADAMARD, EPI_HADAMARD_VEC, EPI_FINAL = 0, 1, 2, 3
 TILE = 128        # small tile class (csrc/precond_gemm.hip)

@@ -79,3 +79,21 @@ def test_fused_kl_matches_reference_dot():
     assert pre._fused_kl is not None
     assert torch.isfinite(pre._fused_kl).item()
     assert vg.item() > 0
+
+
+@pytest.mark.parametrize('channels_last', [False, True])
+def test_bf16x6_fp32_operands_equal_plane_operands(channels_last, monkeypatch):
+    """The default bf16x6 kernel splits fp32 operands into the three bf16
+    planes while staging them into LDS (PREC_BF16X6F); KFAC_X6_PLANES=1 runs
+    the round-2 kernel on plane-stored operands.  Same split, same products in
+    the same order: the preconditioned gradients are bitwise equal."""
+    from distributed_kfac_pytorch_amd.ops import precond_fused
+    monkeypatch.setattr(precond_fused, 'X6_PLANES', False)
+    a, pre_a = _grads(True, 'bf16x6', channels_last=channels_last)
+    assert pre_a.fused.prec == precond_fused.PREC_BF16X6F
+    monkeypatch.setattr(precond_fused, 'X6_PLANES', True)
+    b, pre_b = _grads(True, 'bf16x6', channels_last=channels_last)
+    assert pre_b.fused.prec == precond_fused.PRECISIONS['bf16x6']
+    for gs, hs in zip(a, b):
+        for x, y in zip(gs, hs):
+            assert torch.equal(x, y), (x - y).abs().max()
