@@ -383,9 +383,8 @@ constexpr int VBK = 64;                 // patch rows per k-step (default config
 
 __device__ __forceinline__ uint32_t pack_lo(uint32_t a, uint32_t b) { return (a & 0xffffu) | (b << 16); }
 __device__ __forceinline__ uint32_t pack_hi(uint32_t a, uint32_t b) { return (a >> 16) | (b & 0xffff0000u); }
-__device__ __forceinline__ uint32_t u4get(const uint4& v, int i) {
-  return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
-}
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));   // native vector: selects stay in VGPRs
+__device__ __forceinline__ uint32_t u4get(const u32x4_t& v, int i) { return v[i]; }
 
 // One (upper-triangular tile pair, row split) work item of syrk_vec.
 // VB: patch rows per k-step (LDS rows of VB + 8 elements keep the b128
@@ -394,6 +393,9 @@ __device__ __forceinline__ uint32_t u4get(const uint4& v, int i) {
 // profiles/r3_factors_cfg*.log): 64 rows 4.11 ms; 128 rows 4.95 ms (two
 // workgroups per CU instead of three); two k-steps of loads in flight 7.9-8.0
 // ms (a second register set halves occupancy) -- 64 rows, one ahead, stays.
+// The gather goes through global-address-space loads: with flat loads the
+// MFMA step's LDS waits (lgkmcnt) also waited for the next k-step's gather,
+// so nothing overlapped; 4.11 -> 3.66 ms (profiles/r3_factors_global_loads.log).
 template <int DT, int VB = VBK>
 __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int split,
                                               uint16_t* smem) {
@@ -413,7 +415,10 @@ __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int 
   if (r_begin >= r_end) return;
   const int nk = (int)((r_end - r_begin + VB - 1) / VB);
 
-  const uint16_t* x = (const uint16_t*)p.x;
+  // global address space: a plain pointer from the problem table compiles to
+  // flat loads, which count on lgkmcnt too, so the MFMA step's LDS fragment
+  // waits would also wait for the next k-step's gather (no overlap)
+  const AS1 uint16_t* x = gptr((const uint16_t*)p.x);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   // loader role: operand (0 = A tile ti, 1 = B tile tj), row group, column chunk.
@@ -440,37 +445,43 @@ __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int 
   }
   const uint16_t one = DTypeTraits<DT>::from_f32(1.0f);
 
-  uint4 blk[RG][8];
-  auto load_step = [&](int k, uint4 (&dst)[RG][8]) {
+  u32x4_t blk[RG][8];
+  // Branch-free gather: every load is issued from a valid address (the
+  // tensor base when the element is padding, a bias / zero column or past the
+  // split) and masked by a select, so all 8 RG loads of a k-step are in flight
+  // together (a branch per row made the compiler wait for each load before
+  // the next row's branch: ~8 serial round trips per k-step).
+  const u32x4_t z4 = {0u, 0u, 0u, 0u};
+  const long long ohw = (long long)p.OH * p.OW;
+  auto load_step = [&](int k, u32x4_t (&dst)[RG][8]) {
 #pragma unroll
     for (int g = 0; g < RG; ++g) {
       const long long r0 = r_begin + (long long)k * VB + g * 64 + rg * 8;
       long long rs = r0 < r_end ? r0 : r_begin;
-      const long long ohw = (long long)p.OH * p.OW;
       long long b = rs / ohw;
       int rr = (int)(rs - b * ohw);
       int oh = rr / p.OW, ow = rr - oh * p.OW;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (loader && (r0 + q) < r_end) {
-          if (kind == 0) {
-            const int h = oh * p.sth - p.ph + di, w = ow * p.stw - p.pw + dj;
-            if ((unsigned)h < (unsigned)p.H && (unsigned)w < (unsigned)p.W) {
-              const long long off = b * p.sb + (long long)(oh * p.sth - p.ph) * p.sh +
-                                    (long long)(ow * p.stw - p.pw) * p.sw + coff;
-              v = *(const uint4*)(x + off);
-            }
-          } else if (kind == 1) {
-            v.x = one;
-          }
-        }
+        const int hb = oh * p.sth - p.ph, wb = ow * p.stw - p.pw;
+        const bool row_ok = loader & ((r0 + q) < r_end);
+        const bool in = row_ok & (kind == 0) & ((unsigned)(hb + di) < (unsigned)p.H) &
+                        ((unsigned)(wb + dj) < (unsigned)p.W);
+        const long long off = in ? b * p.sb + (long long)hb * p.sh + (long long)wb * p.sw + coff : 0;
+        u32x4_t v = *(const AS1 u32x4_t*)(x + off);
+        v = in ? v : z4;
+        v[0] = (row_ok & (kind == 1)) ? (uint32_t)one : v[0];
         dst[g][q] = v;
-        if (++ow == p.OW) { ow = 0; if (++oh == p.OH) { oh = 0; ++b; } }
+        // next row: ow, oh, b with selects (no branches in the load section)
+        const bool wrap_w = (ow + 1 == p.OW);
+        const bool wrap_h = wrap_w & (oh + 1 == p.OH);
+        ow = wrap_w ? 0 : ow + 1;
+        oh = wrap_h ? 0 : (wrap_w ? oh + 1 : oh);
+        b += wrap_h ? 1 : 0;
       }
     }
   };
-  auto store_step = [&](const uint4 (&src)[RG][8]) {
+  auto store_step = [&](const u32x4_t (&src)[RG][8]) {
     if (!loader) return;
 #pragma unroll
     for (int g = 0; g < RG; ++g) {
