@@ -380,6 +380,16 @@ __global__ __launch_bounds__(256) void syrk_patch_kernel(PatchArgs p) {
 // Requirements (checked on the host): 16-bit dtype, channel stride 1,
 // C % 8 == 0, every other stride % 8 == 0, 16-byte aligned base.
 constexpr int VBK = 64;                 // patch rows per k-step (default configuration)
+// LDS of one syrk_vec workgroup: two [BT][VB + 8] operand images and the
+// double-buffered row table (VB 16-byte entries per slot)
+template <int VB> struct SyrkVecLds {
+  static_assert(VB == 64, "the row decode is one wave: VB rows per k-step");
+  static constexpr int ELEMS = 2 * BT * (VB + 8) + 2 * VB * 8;
+};
+// 16-byte gather constants: zeros, and the ones column's first chunk [1, 0 x 7]
+// as bf16 and as f16
+__device__ __attribute__((aligned(16))) const uint16_t g_syrk_const[3][8] = {
+    {0, 0, 0, 0, 0, 0, 0, 0}, {0x3f80, 0, 0, 0, 0, 0, 0, 0}, {0x3c00, 0, 0, 0, 0, 0, 0, 0}};
 
 __device__ __forceinline__ uint32_t pack_lo(uint32_t a, uint32_t b) { return (a & 0xffffu) | (b << 16); }
 __device__ __forceinline__ uint32_t pack_hi(uint32_t a, uint32_t b) { return (a >> 16) | (b & 0xffff0000u); }
@@ -396,6 +406,9 @@ __device__ __forceinline__ uint32_t u4get(const u32x4_t& v, int i) { return v[i]
 // The gather goes through global-address-space loads: with flat loads the
 // MFMA step's LDS waits (lgkmcnt) also waited for the next k-step's gather,
 // so nothing overlapped; 4.11 -> 3.66 ms (profiles/r3_factors_global_loads.log).
+// The per-row decode moved into an LDS row table (below): 3.66 -> 3.34 ms
+// (profiles/r3_factors_rowtable.log); what remains is mostly waiting on the
+// one-k-step-ahead gather (SQ_WAIT_ANY 53 % of wave cycles, no LDS conflicts).
 template <int DT, int VB = VBK>
 __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int split,
                                               uint16_t* smem) {
@@ -443,41 +456,64 @@ __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int 
   } else if (gcol < p.ncols) {
     kind = 1;
   }
-  const uint16_t one = DTypeTraits<DT>::from_f32(1.0f);
 
   u32x4_t blk[RG][8];
-  // Branch-free gather: every load is issued from a valid address (the
-  // tensor base when the element is padding, a bias / zero column or past the
-  // split) and masked by a select, so all 8 RG loads of a k-step are in flight
-  // together (a branch per row made the compiler wait for each load before
-  // the next row's branch: ~8 serial round trips per k-step).
-  const u32x4_t z4 = {0u, 0u, 0u, 0u};
-  const long long ohw = (long long)p.OH * p.OW;
+  // Row table: the (b, oh, ow) decode of a patch row is shared by the 16
+  // column chunks (and both operands) of the tile, so one wave decodes the
+  // next k-step's VB rows into LDS (16 B per row: the pixel's element offset
+  // and its top-left (h, w)) and every loader reads it back -- the per-row
+  // 64-bit divisions / multiplies made the gather VALU-bound (~45 vector
+  // instructions per 16-B load; the MFMAs of a k-step hide ~24 cycles each).
+  // Padding / bias / zero / past-the-split elements load from a 16-B constant
+  // (zeros, or the ones column's [1, 0, ...]) instead of being masked: no
+  // select on the loaded data, one pointer select per row.
+  int4* rtab = (int4*)(smem + 2 * BT * VLD);            // [2][VB] entries
+  constexpr int ROW_NONE = -(1 << 30);                  // hs of a row past the split
+  const AS1 u32x4_t* zeros = gptr((const u32x4_t*)g_syrk_const[0]);
+  const AS1 u32x4_t* alt = (kind == 1) ? gptr((const u32x4_t*)g_syrk_const[DT == KDT_BF16 ? 1 : 2])
+                                      : zeros;
+  // kind != 0: no (h, w) passes the bounds test
+  if (kind != 0) { di = ROW_NONE; dj = 0; }
+  auto decode_rows = [&](int k) {
+    if (tid < VB) {                                     // wave 0 (VB = 64)
+      const long long r = r_begin + (long long)k * VB + tid;
+      int4 e = make_int4(0, 0, ROW_NONE, 0);
+      if (r < r_end) {
+        const long long ohw = (long long)p.OH * p.OW;
+        long long b;
+        int rr;
+        if (p.M < (1ll << 31)) {      // wave-uniform: 32-bit divisions
+          const unsigned bu = (unsigned)r / (unsigned)ohw;
+          b = bu;
+          rr = (int)((unsigned)r - bu * (unsigned)ohw);
+        } else {
+          b = r / ohw;
+          rr = (int)(r - b * ohw);
+        }
+        const int oh = (int)((unsigned)rr / (unsigned)p.OW), ow = rr - oh * p.OW;
+        const int hs = oh * p.sth - p.ph, ws = ow * p.stw - p.pw;
+        const long long off = b * p.sb + (long long)hs * p.sh + (long long)ws * p.sw;
+        e = make_int4((int)(unsigned)(off & 0xffffffffll), (int)(off >> 32), hs, ws);
+      }
+      // row j at slot j ^ ((j >> 3) & 7): conflict-free for this store (slots
+      // mod 8 distinct in each 8-lane group) and for the loaders' reads (rows
+      // rg*8 + q of the 8 loader groups land on 8 distinct slots mod 16)
+      const int j = tid;
+      rtab[(k & 1) * VB + (j ^ ((j >> 3) & 7))] = e;
+    }
+  };
   auto load_step = [&](int k, u32x4_t (&dst)[RG][8]) {
+    const int4* rt = rtab + (k & 1) * VB;
 #pragma unroll
     for (int g = 0; g < RG; ++g) {
-      const long long r0 = r_begin + (long long)k * VB + g * 64 + rg * 8;
-      long long rs = r0 < r_end ? r0 : r_begin;
-      long long b = rs / ohw;
-      int rr = (int)(rs - b * ohw);
-      int oh = rr / p.OW, ow = rr - oh * p.OW;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const int hb = oh * p.sth - p.ph, wb = ow * p.stw - p.pw;
-        const bool row_ok = loader & ((r0 + q) < r_end);
-        const bool in = row_ok & (kind == 0) & ((unsigned)(hb + di) < (unsigned)p.H) &
-                        ((unsigned)(wb + dj) < (unsigned)p.W);
-        const long long off = in ? b * p.sb + (long long)hb * p.sh + (long long)wb * p.sw + coff : 0;
-        u32x4_t v = *(const AS1 u32x4_t*)(x + off);
-        v = in ? v : z4;
-        v[0] = (row_ok & (kind == 1)) ? (uint32_t)one : v[0];
-        dst[g][q] = v;
-        // next row: ow, oh, b with selects (no branches in the load section)
-        const bool wrap_w = (ow + 1 == p.OW);
-        const bool wrap_h = wrap_w & (oh + 1 == p.OH);
-        ow = wrap_w ? 0 : ow + 1;
-        oh = wrap_h ? 0 : (wrap_w ? oh + 1 : oh);
-        b += wrap_h ? 1 : 0;
+        const int4 e = rt[g * 64 + rg * 8 + (q ^ rg)];
+        const long long off = ((long long)e.y << 32) | (unsigned)e.x;
+        const bool in = ((unsigned)(e.z + di) < (unsigned)p.H) & ((unsigned)(e.w + dj) < (unsigned)p.W);
+        const AS1 u32x4_t* src = in ? (const AS1 u32x4_t*)(x + off + coff)
+                                    : (e.z != ROW_NONE ? alt : zeros);
+        dst[g][q] = *src;
       }
     }
   };
@@ -540,11 +576,14 @@ __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int 
     }
   };
 
-  load_step(0, blk);
+  decode_rows(0);
+  __syncthreads();
+  if (loader) load_step(0, blk);
   for (int k = 0; k < nk; ++k) {
+    if (k + 1 < nk) decode_rows(k + 1);     // slot (k+1)&1: last read by load_step(k-1)
     store_step(blk);
     __syncthreads();
-    if (k + 1 < nk) load_step(k + 1, blk);
+    if (loader && k + 1 < nk) load_step(k + 1, blk);
     mfma_step();
     __syncthreads();
   }
@@ -554,7 +593,7 @@ __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int 
 
 template <int DT>
 __global__ __launch_bounds__(256) void syrk_vec_kernel(PatchArgs p) {
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BT * (VBK + 8)];
+  __shared__ __attribute__((aligned(16))) uint16_t smem[SyrkVecLds<VBK>::ELEMS];
   syrk_vec_tile<DT>(p, blockIdx.x, blockIdx.y, smem);
 }
 
@@ -578,7 +617,7 @@ static_assert(sizeof(SyrkBatch) <= 4096, "kernel arguments are limited to 4 KB")
 
 template <int DT, int VB = VBK>
 __global__ __launch_bounds__(256) void syrk_vec_grouped_kernel(const SyrkBatch* __restrict__ batch) {
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BT * (VB + 8)];
+  __shared__ __attribute__((aligned(16))) uint16_t smem[SyrkVecLds<VB>::ELEMS];
   const SyrkProblem* t = batch->prob;
   const int count = batch->count;
   int lo = 0, hi = count - 1;
