@@ -323,6 +323,8 @@ def main():
     if dist.is_initialized():
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if device.type == 'cuda' and os.environ.get('KFAC_PROFILE_MARKER'):
+        torch.cuda._sleep(1000)   # end of the timed window (the SGD-only run follows)
     per_kind = {}
     for k, a, b in zip(kinds, events[:-1], events[1:]):
         per_kind.setdefault(k, []).append(a.elapsed_time(b) if device.type == 'cuda'

@@ -31,6 +31,7 @@
 namespace {
 
 typedef unsigned u32x4n __attribute__((ext_vector_type(4)));
+typedef float fx2 __attribute__((ext_vector_type(2)));
 
 constexpr int NT = 256;              // threads per block
 constexpr int TARGET_BLOCKS = 1024;  // stats / reduce grid (4 per CU; fewer chunk partials)
@@ -138,12 +139,17 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(const uint16_t* __restrict
   block_reduce16(acc, red, rr, cv, g.tpr, g.rpi);
   if (rr == 0) {
     const float n = (float)(m1 - m0);
-    float* o = part + ((long long)chunk * C + c0) * 2;
+    // channel-major partials [c][chunk][2]: the finalize wave of a channel
+    // reads its chunks as one contiguous run (chunk-major put each lane of
+    // that wave on its own cache line)
+    AS1 float* o = gptr(part) + ((long long)c0 * g.nchunks + chunk) * 2;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float s1 = acc[i], s2 = acc[8 + i];
-      o[2 * i] = k[i] + s1 / n;                       // chunk mean
-      o[2 * i + 1] = fmaxf(s2 - s1 * (s1 / n), 0.f);  // chunk M2
+      fx2 v;
+      v.x = k[i] + s1 / n;                        // chunk mean
+      v.y = fmaxf(s2 - s1 * (s1 / n), 0.f);       // chunk M2
+      *(AS1 fx2*)(o + (long long)i * g.nchunks * 2) = v;
     }
   }
 }
@@ -160,15 +166,17 @@ __global__ __launch_bounds__(NT) void bn_finalize_kernel(
   const int c = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
   if (blockIdx.x == 0 && threadIdx.x == 0 && nbt != nullptr) nbt[0] += 1;
   if (c >= C) return;
-  const double K = (double)part[(long long)c * 2];
+  const AS1 fx2* pc = (const AS1 fx2*)(gptr(part) + (long long)c * g.nchunks * 2);
+  const double K = (double)pc[0].x;
   double s1 = 0.0, s2 = 0.0;
 #pragma unroll 8
   for (int k = lane; k < g.nchunks; k += 64) {
     const long long r0 = (long long)k * g.rows;
     const double nb = (double)((M - r0) < g.rows ? (M - r0) : g.rows);
-    const double d = (double)part[((long long)k * C + c) * 2] - K;
+    const fx2 e = pc[k];
+    const double d = (double)e.x - K;
     s1 = fma(nb, d, s1);
-    s2 += (double)part[((long long)k * C + c) * 2 + 1] + nb * d * d;
+    s2 += (double)e.y + nb * d * d;
   }
   s1 = wave_reduce_sum_d(s1);
   s2 = wave_reduce_sum_d(s2);
@@ -305,11 +313,13 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(
   }
   block_reduce16(acc, red, rr, cv, g.tpr, g.rpi);
   if (rr == 0) {
-    float* o = part + ((long long)chunk * C + c0) * 2;
+    AS1 float* o = gptr(part) + ((long long)c0 * g.nchunks + chunk) * 2;   // [c][chunk][2]
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      o[2 * i] = acc[i];
-      o[2 * i + 1] = acc[8 + i];
+      fx2 v;
+      v.x = acc[i];
+      v.y = acc[8 + i];
+      *(AS1 fx2*)(o + (long long)i * g.nchunks * 2) = v;
     }
   }
 }
@@ -323,11 +333,13 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(
   const int lane = threadIdx.x & 63;
   const int c = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
   if (c >= C) return;
+  const AS1 fx2* pc = (const AS1 fx2*)(gptr(part) + (long long)c * g.nchunks * 2);
   double sg = 0.0, sgx = 0.0;
 #pragma unroll 8
   for (int k = lane; k < g.nchunks; k += 64) {
-    sg += (double)part[((long long)k * C + c) * 2];
-    sgx += (double)part[((long long)k * C + c) * 2 + 1];
+    const fx2 e = pc[k];
+    sg += (double)e.x;
+    sgx += (double)e.y;
   }
   sg = wave_reduce_sum_d(sg);
   sgx = wave_reduce_sum_d(sgx);

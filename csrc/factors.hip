@@ -621,6 +621,8 @@ __global__ __launch_bounds__(256) void syrk_vec_grouped_kernel(const SyrkBatch* 
   const SyrkProblem* t = batch->prob;
   const int count = batch->count;
   int lo = 0, hi = count - 1;
+  // hardware order: an XCD-contiguous remap (a split's tiles on one L2)
+  // measured 3.34 -> 3.43 ms (profiles/r3_factors_xcd_remap.log)
   const int b = blockIdx.x;
   while (lo < hi) {
     int mid = (lo + hi + 1) >> 1;

@@ -132,6 +132,10 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   constexpr int LDS_BYTES = IMG16 ? (PL * (BM + BN) * LDB16 * 2) : ((BM + BN) * LDF32 * 4);
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES * (DBUF ? 2 : 1)];
 
+  // Workgroups stay in hardware order (round-robin over the 8 XCDs).  An
+  // XCD-contiguous remap (guide T1) measured 2.11 -> 4.62 ms on the ResNet-50
+  // chain (profiles/r3_pgemm_xcd_remap.log): over a ragged grouped grid it
+  // hands one XCD all the tiles of the big-K problems.
   const int pi = find_problem(table, count, blockIdx.x);
   const PGemm P = table[pi];                      // uniform: scalar registers
   const AS1 unsigned char* const Ah = (const AS1 unsigned char*)P.a_hi;

@@ -55,14 +55,21 @@ def main():
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 1
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
-    start = None
-    for r in rows:
-        if 'sleep' in r['Kernel_Name'].lower() or 'spin' in r['Kernel_Name'].lower():
-            start = int(r['Start_Timestamp'])
-    if start is None:
+    # bench.py (KFAC_PROFILE_MARKER=1) launches a spin kernel right before and
+    # right after the timed window; later work (the SGD-only baseline run) is
+    # outside the window
+    marks = [int(r['Start_Timestamp']) for r in rows
+             if 'sleep' in r['Kernel_Name'].lower() or 'spin' in r['Kernel_Name'].lower()]
+    end = None
+    if len(marks) >= 2:
+        start, end = marks[-2], marks[-1]
+    elif marks:
+        start = marks[-1]
+    else:
         print('marker kernel not found; using the whole trace')
         start = int(rows[0]['Start_Timestamp'])
-    win = [r for r in rows if int(r['Start_Timestamp']) > start]
+    win = [r for r in rows if int(r['Start_Timestamp']) > start
+           and (end is None or int(r['Start_Timestamp']) < end)]
     tot = collections.Counter()
     cnt = collections.Counter()
     names = collections.defaultdict(collections.Counter)
