@@ -12,7 +12,7 @@
 //                       x - x[first row] and their squares (one 16-byte load =
 //                       8 channels per thread), block-reduced in a fixed
 //                       order -> chunk (mean, M2)
-//             finalize  one wave per channel: the chunks merged in fp64
+//             finalize  one workgroup per channel: the chunks merged in fp64
 //                       about a common shift -> mean, 1/sqrt(var + eps); running
 //                       stats (unbiased var) and num_batches_tracked updated
 //                       in place; scale = w / sigma, shift = b - mean scale
@@ -154,23 +154,37 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(const uint16_t* __restrict
   }
 }
 
-// one wave per channel: the chunk (mean, M2) pairs merged in fp64 about a
-// common shift (the first chunk's mean): S1 = sum n_k (mean_k - K),
-// S2 = sum M2_k + n_k (mean_k - K)^2 -- FMAs only, no per-chunk divisions
+// fp64 sums of a workgroup (one channel per workgroup): waves reduced in
+// lane order, then the 4 wave sums in wave order -- fixed, deterministic
+__device__ __forceinline__ void block_sum2_d(double& a, double& b) {
+  __shared__ double sh[2][NT / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  a = wave_reduce_sum_d(a);
+  b = wave_reduce_sum_d(b);
+  if (lane == 0) { sh[0][w] = a; sh[1][w] = b; }
+  __syncthreads();
+  a = 0.0; b = 0.0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) { a += sh[0][i]; b += sh[1][i]; }
+}
+
+// one workgroup per channel (the chunks of a channel spread over 256 lanes:
+// the chunk loop is 4 iterations at ResNet-50's 1024 chunks, not 16 on one
+// wave): the chunk (mean, M2) pairs merged in fp64 about a common shift (the
+// first chunk's mean): S1 = sum n_k (mean_k - K), S2 = sum M2_k + n_k
+// (mean_k - K)^2 -- FMAs only, no per-chunk divisions
 __global__ __launch_bounds__(NT) void bn_finalize_kernel(
     const float* __restrict__ part, long long M, int C, Geo g, float eps, float momentum,
     const float* __restrict__ w, const float* __restrict__ b, float* __restrict__ rmean,
     float* __restrict__ rvar, long long* __restrict__ nbt, float* __restrict__ save_mean,
     float* __restrict__ save_invstd, float* __restrict__ scale, float* __restrict__ shift) {
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
-  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt != nullptr) nbt[0] += 1;
-  if (c >= C) return;
+  const int c = blockIdx.x, t = threadIdx.x;
+  if (c == 0 && t == 0 && nbt != nullptr) nbt[0] += 1;
   const AS1 fx2* pc = (const AS1 fx2*)(gptr(part) + (long long)c * g.nchunks * 2);
   const double K = (double)pc[0].x;
   double s1 = 0.0, s2 = 0.0;
-#pragma unroll 8
-  for (int k = lane; k < g.nchunks; k += 64) {
+#pragma unroll 4
+  for (int k = t; k < g.nchunks; k += NT) {
     const long long r0 = (long long)k * g.rows;
     const double nb = (double)((M - r0) < g.rows ? (M - r0) : g.rows);
     const fx2 e = pc[k];
@@ -178,11 +192,10 @@ __global__ __launch_bounds__(NT) void bn_finalize_kernel(
     s1 = fma(nb, d, s1);
     s2 += (double)e.y + nb * d * d;
   }
-  s1 = wave_reduce_sum_d(s1);
-  s2 = wave_reduce_sum_d(s2);
-  const double mean = K + s1 / (double)M;
-  const double m2 = s2 - s1 * (s1 / (double)M);
-  if (lane == 0) {
+  block_sum2_d(s1, s2);
+  if (t == 0) {
+    const double mean = K + s1 / (double)M;
+    const double m2 = s2 - s1 * (s1 / (double)M);
     const double var = m2 / (double)M;
     const float invstd = (float)(1.0 / sqrt(var + (double)eps));
     save_mean[c] = (float)mean;
@@ -324,26 +337,23 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(
   }
 }
 
-// one wave per channel: fp64 chunk sums -> dw, db and the planar (A, B, X)
-// of dx = a (g - k1 - x_hat k2) = A g + B + X x
+// one workgroup per channel: fp64 chunk sums -> dw, db and the planar
+// (A, B, X) of dx = a (g - k1 - x_hat k2) = A g + B + X x
 __global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(
     const float* __restrict__ part, long long M, int C, Geo g, const float* __restrict__ w,
     const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ dw, float* __restrict__ db,
     float* __restrict__ coef) {
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
-  if (c >= C) return;
+  const int c = blockIdx.x, t = threadIdx.x;
   const AS1 fx2* pc = (const AS1 fx2*)(gptr(part) + (long long)c * g.nchunks * 2);
   double sg = 0.0, sgx = 0.0;
-#pragma unroll 8
-  for (int k = lane; k < g.nchunks; k += 64) {
+#pragma unroll 4
+  for (int k = t; k < g.nchunks; k += NT) {
     const fx2 e = pc[k];
     sg += (double)e.x;
     sgx += (double)e.y;
   }
-  sg = wave_reduce_sum_d(sg);
-  sgx = wave_reduce_sum_d(sgx);
-  if (lane == 0) {
+  block_sum2_d(sg, sgx);
+  if (t == 0) {
     if (dw) dw[c] = (float)sgx;
     if (db) db[c] = (float)sg;
     // dx = a (g - k1 - (x - mean) invstd k2) as an affine map of (g, x):
@@ -436,7 +446,7 @@ KFAC_API int kfac_bn_forward(const void* x, const void* z, const float* w, const
   float* shift = scale + C;
   hipLaunchKernelGGL(bn_stats_kernel, dim3(g.ncg, g.nchunks), dim3(NT), 0, stream,
                      (const uint16_t*)x, M, C, g, part);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 3) / 4), dim3(NT), 0, stream, part, M, C, g,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(NT), 0, stream, part, M, C, g,
                      eps, momentum, w, b, rmean, rvar, nbt, save_mean, save_invstd, scale, shift);
   const long long nvec = M * C / 8;
   const dim3 grid(apply_grid(nvec));
@@ -474,7 +484,7 @@ KFAC_API int kfac_bn_backward(const void* dy, const void* y, const void* x, cons
   else
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, dim3(g.ncg, g.nchunks), dim3(NT), 0, stream,
                        DY, Y, X, save_mean, save_invstd, M, C, g, part);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(NT), 0, stream, part, M, C,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(NT), 0, stream, part, M, C,
                      g, w, save_mean, save_invstd, dw, db, coef);
   const long long nvec = M * C / 8;
   const dim3 grid(apply_grid(nvec));

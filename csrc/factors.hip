@@ -409,6 +409,10 @@ __device__ __forceinline__ uint32_t u4get(const u32x4_t& v, int i) { return v[i]
 // The per-row decode moved into an LDS row table (below): 3.66 -> 3.34 ms
 // (profiles/r3_factors_rowtable.log); what remains is mostly waiting on the
 // one-k-step-ahead gather (SQ_WAIT_ANY 53 % of wave cycles, no LDS conflicts).
+// An LDS-DMA version (global_load_lds into a ring of [64][128] images read
+// with ds_read_b64_tr_b16, no staging registers) measured 3.46 ms with two
+// stages (2 workgroups / CU) and 4.70 ms with three (1 / CU; hipcc still waits
+// vmcnt(0) before some ring reads): not kept (profiles/r3_factors_dma*.log).
 template <int DT, int VB = VBK>
 __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int split,
                                               uint16_t* smem) {

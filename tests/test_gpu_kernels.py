@@ -57,6 +57,30 @@ def test_syrk_patch_matches_unfold(dtype, layout, geom):
     assert err < tol, err
 
 
+def test_grouped_syrk_matches_unfold():
+    """The grouped factor-step SYRK (every factor in one launch) against fp64
+    unfold covariances: padding, strides, dilation, the bias chunk, tiles
+    crossing 128 and diagonal tiles."""
+    torch.manual_seed(0)
+    geoms = [(16, 9, 9, 3, 2, 1, 1, True), (24, 10, 12, 3, 1, 2, 2, True),
+             (136, 6, 6, 3, 1, 1, 1, True), (48, 14, 14, 1, 2, 0, 1, False),
+             (64, 7, 7, 3, 1, 1, 1, False), (8, 30, 30, 3, 1, 1, 1, False)]
+    items, refs = [], []
+    for C, H, W, k, s_, p_, d, bias in geoms:
+        x = torch.randn(5, C, H, W, device=DEV).to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        src = factors.FactorSource(x, factors.Geometry(k, k, s_, s_, p_, p_, d, d), bias, 1.0)
+        assert factors._vec_eligible(src)
+        n = src.ncols
+        items.append((torch.zeros(n, n, device=DEV), [src], torch.float32))
+        refs.append(_cov_patches_ref(x.float(), k, s_, p_, d, bias))
+    outs = factors.update_factors_grouped(items, 0.5)
+    for got, want in zip(outs, refs):
+        got = 2.0 * got.double()
+        err = (got - want).abs().max().item() / max(1.0, want.abs().max().item())
+        assert err < 2e-3, err
+
+
 def test_syrk_vec_path_is_taken():
     x = torch.randn(2, 16, 5, 5, device=DEV).to(torch.bfloat16).contiguous(
         memory_format=torch.channels_last)
