@@ -106,6 +106,10 @@ def parse():
                          'backward (KFAC(overlap_precondition=True)); off by default: the '
                          'backward already fills the GPU, 11.05 vs 10.91 ms per plain step '
                          '(profiles/r2_final_bench20*.log)')
+    ap.add_argument('--early-factors', type=int, default=0,
+                    help='factor steps: the A factors (layer inputs) are computed on a side '
+                         'stream from the first gradient hook, under the backward '
+                         '(KFAC(early_factors=True)); bitwise the same factors')
     ap.add_argument('--fused-sgd', type=int, default=1,
                     help='torch.optim.SGD(fused=True): one multi-tensor kernel for the whole '
                          'momentum + weight-decay update (same math as the reference optimizer)')
@@ -238,6 +242,7 @@ def main():
                         compute_factor_in_hook=grad_sync is not None,
                         inverse_lag=args.inverse_lag,
                         overlap_precondition=bool(args.overlap_precond) and world == 1,
+                        early_factors=bool(args.early_factors),
                         use_hip_graphs=not os.environ.get('KFAC_NO_TAIL_GRAPH'))
         if weights is not None:
             pre.set_grad_params(weights.grad_params())
@@ -370,7 +375,8 @@ def main():
                            'damping': args.damping, 'kl_clip': args.kl_clip,
                            'precond_precision': args.precond_precision,
                            'inverse_lag': args.inverse_lag,
-                           'overlap_precondition': bool(args.overlap_precond) and world == 1},
+                           'overlap_precondition': bool(args.overlap_precond) and world == 1,
+                           'early_factors': bool(args.early_factors)},
                        'hip_graphs': use_graphs,
                        'fused_sgd': bool(args.fused_sgd and device.type == 'cuda'),
                        'weights': 'bf16 + fp32 masters' if weights is not None

@@ -104,6 +104,9 @@ class GraphedTrainStep(object):
         self.post_update = post_update
         self.segmented = step_fn is None
         self.pre = preconditioner
+        if self.segmented and preconditioner is not None:
+            # no side-stream fork may span the fb / update graph boundary
+            preconditioner._segmented_capture = True
         # 'force' phases the update even when it issues no collective (tests)
         self.phased_update = phased_update
         # inverse-update steps replay the factor-step forward/backward graph(s)

@@ -267,7 +267,7 @@ class EmaJob(ctypes.Structure):
 SPLIT_ROWS = 2048   # patch rows per block of the grouped SYRK
 
 
-def update_factors_grouped(items, alpha):
+def update_factors_grouped(items, alpha, tag=''):
     """Running-average update of MANY factors in a fixed number of launches.
 
     items: list of (state_or_None, sources, out_dtype[, keep]) -- keep: None or
@@ -276,7 +276,9 @@ def update_factors_grouped(items, alpha):
     Every factor whose sources all qualify for the channels-contiguous path
     goes through ONE grouped SYRK launch per input dtype plus ONE grouped EMA
     launch; the rest fall back to the per-factor path.  One memset zeroes the
-    shared f32 workspace arena.
+    shared f32 workspace arena.  `tag` names the workspaces: calls that may
+    run concurrently on different streams (KFAC(early_factors=True)) use
+    different tags.
     """
     if not items:
         return []
@@ -301,7 +303,7 @@ def update_factors_grouped(items, alpha):
     sizes = [items[k][1][0].ncols for k in grouped]
     total = sum(n * n for n in sizes)
     # no memset: tile_reduce writes every upper-triangle element the EMA reads
-    arena = _lib.workspace(dev, total, tag='syrk_grouped')
+    arena = _lib.workspace(dev, total, tag='syrk_grouped' + tag)
     psize = L.kfac_syrk_problem_size()
     by_dtype = {}
     ws_of = {}
@@ -336,7 +338,7 @@ def update_factors_grouped(items, alpha):
     # partial tiles of every (problem, split, tile pair): one arena, then the
     # fixed-order tile reduction per factor (sources in order, splits in order)
     tot_parts = sum(sum(nbs) for _, _, _, nbs in launches) * TILE * TILE
-    parts = _lib.workspace(dev, tot_parts, tag='syrk_parts_grouped')
+    parts = _lib.workspace(dev, tot_parts, tag='syrk_parts_grouped' + tag)
     poff = 0
     for dtype, probs, raw, nbs in launches:
         for i, ((k, s), nb) in enumerate(zip(probs, nbs)):

@@ -174,7 +174,7 @@ class KFAC(optim.Optimizer):
                  bucket_cap_mb=64.0, symmetry_aware_comm=True, eigen_solver='auto',
                  profile=False, use_hip_graphs=True, precond_precision='fp32',
                  fused_precondition=True, inverse_lag=0, comm_check=False,
-                 overlap_precondition=False, defer_factor_comm=True):
+                 overlap_precondition=False, defer_factor_comm=True, early_factors=False):
         if not 0.0 <= lr:
             raise ValueError('Invalid learning rate: {}'.format(lr))
         if not 0.0 < factor_decay <= 1:
@@ -274,6 +274,17 @@ class KFAC(optim.Optimizer):
         self._eigen_gen = 0         # bumped whenever new eigendata is in place
         # all factors of a step in a few grouped launches (GPU)
         self.grouped_factors = True
+        # early_factors: on a factor step the A factors (this step's layer
+        # inputs, complete once backward starts) are computed on a side stream
+        # from the first gradient hook, under the backward; step() joins them
+        # before the G factors.  Same kernels, same per-factor reduction order:
+        # bitwise the same factors as computing everything in step()
+        self.early_factors = bool(early_factors)
+        self._factor_stream = None
+        self._early_a = None        # the A jobs in flight (keeps the activations alive)
+        self._early_a_step = None
+        self._reverse_hooked = False
+        self._segmented_capture = False   # set by graphs.GraphedTrainStep
         self.fused = None
         self._fused_kl = None
         self._graph = None
@@ -401,6 +412,8 @@ class KFAC(optim.Optimizer):
                     use_eigen_decomp=self.use_eigen_decomp)
 
     def _attach_hooks(self, module, reverse=False):
+        if reverse:
+            self._reverse_hooked = True   # A of such layers arrives in backward
         h = module.register_forward_hook(functools.partial(self._forward_hook, reverse=reverse))
         self._hook_handles.append(h)
 
@@ -486,11 +499,59 @@ class KFAC(optim.Optimizer):
         if reverse:
             layer.save_inputs((grad,))
             return
+        if self._early_a_due():
+            self._launch_early_a()
         layer.save_grad_outputs((grad,))
         if self.compute_factor_in_hook:
             self.join_factor_comm()
             with self._no_autocast(grad):
                 layer.update_G_factor(alpha=self.param_groups[0]['factor_decay'])
+
+    # ----------------------------------------------- early A factors
+    def _early_a_due(self):
+        p = self.param_groups[0]
+        return (self.early_factors and self._early_a is None and self.grouped_factors
+                and self._early_a_step != p['step'] and not self.compute_factor_in_hook
+                and not self.accumulate_data and not self._reverse_hooked
+                and bool(self.layers) and self.layers[0].module.weight.is_cuda
+                # a segmented capture would fork in the forward/backward graph and
+                # join in the separately captured update graph
+                and not (self._segmented_capture and torch.cuda.is_current_stream_capturing()))
+
+    def _launch_early_a(self):
+        """First gradient hook of a factor step: every layer's A factor (its
+        forward inputs are all saved) on the factor stream, under the backward."""
+        p = self.param_groups[0]
+        self._early_a_step = p['step']
+        self.join_factor_comm()     # the EMA reads the averaged factors
+        items, refs = [], []
+        for layer in self.layers:
+            job = layer.take_factor_job('A')
+            if job is None:
+                continue
+            if layer.state['A'] is None:     # allocated on the main stream
+                n = job[0][0].ncols
+                layer.state['A'] = torch.eye(n, dtype=job[1], device=layer.module.weight.device)
+            items.append((layer.state['A'], job[0], job[1], job[2]))
+            refs.append(layer)
+        if not items:
+            return
+        cur = torch.cuda.current_stream()
+        if self._factor_stream is None:
+            self._factor_stream = torch.cuda.Stream(device=cur.device)
+        side = self._factor_stream
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            outs = factor_ops.update_factors_grouped(items, p['factor_decay'], tag='_early')
+        for layer, st in zip(refs, outs):
+            layer.state['A'] = st
+        self._early_a = items
+
+    def join_early_factors(self):
+        """Order the current stream after an early A-factor update in flight."""
+        if self._early_a is not None:
+            torch.cuda.current_stream().wait_stream(self._factor_stream)
+            self._early_a = None
 
     def set_grad_params(self, mapping):
         """Precondition the gradients of other parameters than the modules'
@@ -952,6 +1013,7 @@ class KFAC(optim.Optimizer):
         through a handful of grouped SYRK + EMA launches (ops/factors.py
         update_factors_grouped) instead of ~3 launches per factor."""
         self.join_factor_comm()     # the EMA reads the averaged factors
+        self.join_early_factors()
         if self.layers and self.layers[0].module.weight.is_cuda and self.grouped_factors:
             items, refs = [], []
             for layer in self.layers:

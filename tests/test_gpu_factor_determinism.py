@@ -136,3 +136,59 @@ def test_lstm_lm_factors_bitwise():
     assert len(a) > 0
     for (A1, G1), (A2, G2) in zip(a, b):
         assert torch.equal(A1, A2) and torch.equal(G1, G2)
+
+
+def _train_factors(early, graphed, steps=7):
+    import distributed_kfac_pytorch_amd as kfac
+    from distributed_kfac_pytorch_amd import graphs
+    from distributed_kfac_pytorch_amd.models import resnet
+    torch.manual_seed(0)
+    m = resnet.resnet_tiny(num_classes=10).cuda().to(memory_format=torch.channels_last)
+    opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9)
+    # damped-inverse path: bitwise reproducible inputs to every later step
+    pre = kfac.KFAC(m, factor_update_freq=1, inv_update_freq=4, lr=0.05, damping=0.003,
+                    use_eigen_decomp=False, early_factors=early)
+    g = torch.Generator(device='cuda').manual_seed(3)
+    xs = [torch.randn(8, 3, 32, 32, device='cuda', generator=g) for _ in range(steps)]
+    ys = [torch.randint(0, 10, (8,), device='cuda', generator=g) for _ in range(steps)]
+    x = torch.empty_like(xs[0]).contiguous(memory_format=torch.channels_last)
+    y = torch.empty_like(ys[0])
+
+    def step_fn():
+        opt.zero_grad(set_to_none=False)
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            loss = F.cross_entropy(m(x), y)
+        loss.backward()
+        pre.step()
+        opt.step()
+        return loss
+
+    step = graphs.GraphedTrainStep(step_fn, pre, [opt], warmup=1, enabled=graphed)
+    for i in range(steps):
+        x.copy_(xs[i])
+        y.copy_(ys[i])
+        step()
+    torch.cuda.synchronize()
+    return ([l.state[w].clone() for l in pre.layers for w in ('A', 'G')],
+            [p.detach().clone() for p in m.parameters()], pre, step)
+
+
+@pytest.mark.parametrize('graphed', [False, True])
+def test_early_factors_bitwise(graphed):
+    """KFAC(early_factors=True) computes the A factors on a side stream from
+    the first gradient hook, under the backward: the factors and the whole
+    trajectory are bitwise those of computing every factor in step()."""
+    prev = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        f0, p0, _, _ = _train_factors(False, graphed)
+        f1, p1, pre, step = _train_factors(True, graphed)
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = prev
+    assert pre._factor_stream is not None and pre._early_a is None
+    if graphed:
+        assert step.replays > 0
+    for a, b in zip(f0, f1):
+        assert torch.equal(a, b), (a - b).abs().max()
+    for a, b in zip(p0, p1):
+        assert torch.equal(a, b), (a - b).abs().max()
