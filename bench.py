@@ -106,7 +106,7 @@ def parse():
                          'backward (KFAC(overlap_precondition=True)); off by default: the '
                          'backward already fills the GPU, 11.05 vs 10.91 ms per plain step '
                          '(profiles/r2_final_bench20*.log)')
-    ap.add_argument('--early-factors', type=int, default=0,
+    ap.add_argument('--early-factors', type=int, default=1,
                     help='factor steps: the A factors (layer inputs) are computed on a side '
                          'stream from the first gradient hook, under the backward '
                          '(KFAC(early_factors=True)); bitwise the same factors')
