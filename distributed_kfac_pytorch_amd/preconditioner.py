@@ -285,6 +285,11 @@ class KFAC(optim.Optimizer):
         self._early_a_step = None
         self._reverse_hooked = False
         self._segmented_capture = False   # set by graphs.GraphedTrainStep
+        # compute_factor_in_hook on the GPU: gradient hooks of this step seen /
+        # registered (the last one runs the grouped factor launches)
+        self._hook_step = None
+        self._g_seen = 0
+        self._g_expected = 0
         self.fused = None
         self._fused_kl = None
         self._graph = None
@@ -481,15 +486,20 @@ class KFAC(optim.Optimizer):
             return
         layer = self.hook_layers[module]
         alpha = self.param_groups[0]['factor_decay']
+        grouped = self._hook_factors_grouped()
+        if grouped:
+            self._hook_counters()
         if reverse:
             layer.save_grad_outputs(input)
         else:
             layer.save_inputs(input)
-            if self.compute_factor_in_hook:
+            if self.compute_factor_in_hook and not grouped:
                 self.join_factor_comm()     # the EMA reads the averaged factors
                 with self._no_autocast(input[0]):
                     layer.update_A_factor(alpha=alpha)
         if isinstance(output, torch.Tensor) and output.requires_grad:
+            if grouped:
+                self._g_expected += 1
             output.register_hook(functools.partial(self._grad_hook, module, reverse))
 
     def _grad_hook(self, module, reverse, grad):
@@ -503,9 +513,34 @@ class KFAC(optim.Optimizer):
             self._launch_early_a()
         layer.save_grad_outputs((grad,))
         if self.compute_factor_in_hook:
+            if self._hook_factors_grouped():
+                # the last gradient hook of this backward: every factor of the
+                # step in the grouped launches, still inside the backward (and
+                # inside a captured forward/backward graph)
+                self._hook_counters()
+                self._g_seen += 1
+                if self._g_seen == self._g_expected:
+                    self._g_seen = self._g_expected = 0
+                    with self._no_autocast(grad):
+                        self.compute_factors(alpha=self.param_groups[0]['factor_decay'])
+                return
             self.join_factor_comm()
             with self._no_autocast(grad):
                 layer.update_G_factor(alpha=self.param_groups[0]['factor_decay'])
+
+    def _hook_factors_grouped(self):
+        """compute_factor_in_hook on the GPU: save in the hooks, and run the
+        grouped SYRK + EMA launches from the backward's last gradient hook
+        instead of ~3 launches per factor from every hook."""
+        return (self.compute_factor_in_hook and self.grouped_factors and bool(self.layers)
+                and self.layers[0].module.weight.is_cuda and not self.accumulate_data
+                and not self._reverse_hooked)
+
+    def _hook_counters(self):
+        st = self.param_groups[0]['step']
+        if self._hook_step != st:
+            self._hook_step = st
+            self._g_seen = self._g_expected = 0
 
     # ----------------------------------------------- early A factors
     def _early_a_due(self):

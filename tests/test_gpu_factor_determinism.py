@@ -138,7 +138,7 @@ def test_lstm_lm_factors_bitwise():
         assert torch.equal(A1, A2) and torch.equal(G1, G2)
 
 
-def _train_factors(early, graphed, steps=7):
+def _train_factors(early, graphed, steps=7, hook=False):
     import distributed_kfac_pytorch_amd as kfac
     from distributed_kfac_pytorch_amd import graphs
     from distributed_kfac_pytorch_amd.models import resnet
@@ -147,7 +147,7 @@ def _train_factors(early, graphed, steps=7):
     opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9)
     # damped-inverse path: bitwise reproducible inputs to every later step
     pre = kfac.KFAC(m, factor_update_freq=1, inv_update_freq=4, lr=0.05, damping=0.003,
-                    use_eigen_decomp=False, early_factors=early)
+                    use_eigen_decomp=False, early_factors=early, compute_factor_in_hook=hook)
     g = torch.Generator(device='cuda').manual_seed(3)
     xs = [torch.randn(8, 3, 32, 32, device='cuda', generator=g) for _ in range(steps)]
     ys = [torch.randint(0, 10, (8,), device='cuda', generator=g) for _ in range(steps)]
@@ -188,6 +188,28 @@ def test_early_factors_bitwise(graphed):
     assert pre._factor_stream is not None and pre._early_a is None
     if graphed:
         assert step.replays > 0
+    for a, b in zip(f0, f1):
+        assert torch.equal(a, b), (a - b).abs().max()
+    for a, b in zip(p0, p1):
+        assert torch.equal(a, b), (a - b).abs().max()
+
+
+@pytest.mark.parametrize('graphed', [False, True])
+def test_hook_factors_grouped_bitwise(graphed):
+    """compute_factor_in_hook=True on the GPU (the multi-rank segmented-graph
+    mode) saves in the hooks and runs the grouped factor launches from the
+    backward's last gradient hook: bitwise the factors and trajectory of
+    computing them in step()."""
+    prev = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        f0, p0, _, _ = _train_factors(False, graphed)
+        f1, p1, pre, step = _train_factors(False, graphed, hook=True)
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = prev
+    assert pre._hook_factors_grouped() and pre._hook_step is not None
+    for l in pre.layers:
+        assert not l.a_inputs and not l.g_outputs
     for a, b in zip(f0, f1):
         assert torch.equal(a, b), (a - b).abs().max()
     for a, b in zip(p0, p1):
