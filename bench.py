@@ -312,11 +312,20 @@ def main():
         torch.cuda.synchronize()
     # per-step device time by step kind: events between steps (graphs stay on)
     kinds, events = [], []
+    kfac_comm = kfac.comm.backend
+    coll_by_kind = {}
     t0 = time.perf_counter()
     for i in range(args.steps):
         kinds.append(step_kind(pre))
         events.append(_mark(device))
+        c0 = kfac_comm.counters() if (kfac_comm is not None and kinds[-1] not in coll_by_kind) \
+            else None
         loss = step()
+        if c0 is not None:
+            # the K-FAC collectives this step kind issued (host-side counters)
+            c1 = kfac_comm.counters()
+            coll_by_kind[kinds[-1]] = {k: [v[0] - c0.get(k, (0, 0))[0], v[1] - c0.get(k, (0, 0))[1]]
+                                       for k, v in c1.items() if v != c0.get(k)}
         if args.check_finite:
             kl = float(pre.fused.kl) if (pre is not None and pre.fused is not None) else 0.0
             print('step', i, 'loss', float(loss.item()), 'kl', kl, flush=True)
@@ -425,6 +434,22 @@ def main():
                         'speedup': round((REFERENCE_MI355X_STEP_MS[k] - REFERENCE_MI355X_SGD_MS) /
                                          max(ours[k], 1e-3), 2)}
                     for k in ours if k in REFERENCE_MI355X_STEP_MS}
+        if pre is not None:
+            # how the communication was built and what it moved: lets a
+            # multi-GPU record be checked from itself (RCCL world size, split vs
+            # new_group communicators, bucket / arena bytes, calls per step kind)
+            cs = pre.comm_summary()
+            cs['kfac_collectives_per_step_kind'] = coll_by_kind
+            if grad_sync is not None:
+                syncs = [grad_sync.sync_top, grad_sync.sync_bottom] if split else [grad_sync]
+                cs['grad_allreduce'] = {
+                    'kind': 'split-backward-overlap' if split else 'flat-arena',
+                    'calls_per_step': sum(len(sy.arenas) for sy in syncs) if world > 1 else 0,
+                    'arena_bytes': [a.numel() * a.element_size() for sy in syncs
+                                    for a in sy.arenas]}
+            elif world > 1:
+                cs['grad_allreduce'] = {'kind': 'ddp'}
+            rec['comm'] = cs
         if phases is not None:
             rec['kfac_phase_ms_total'] = {k: round(v, 2) for k, v in phases.items()}
             rec['kfac_phase_ms_per_step'] = round(sum(phases.values()) / args.steps, 3)

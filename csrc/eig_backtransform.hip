@@ -317,6 +317,21 @@ KFAC_API int kfac_tridiag_backtransform(float* A, int lda, long long strideA, co
   return run_plan(a, *plan, stream);
 }
 
+// The same for the two-stage solver's stage 1 (csrc/eig_sy2sb.hip): reflector
+// j has its implicit 1 at column j + shift (shift = the band's half-bandwidth)
+KFAC_API int kfac_band_backtransform(float* A, int lda, long long strideA, const float* tau,
+                                     float* Z, int ldz, long long strideZ, int n, int batch,
+                                     float* Tbuf, float* W1, float* W2, float* Vt, int shift,
+                                     int use_graph, hipStream_t stream) {
+  if (lda % 64 || ldz % 64 || lda != ldz || n < 2 || shift < 1) return -2;
+  const BtArgs a{A, lda, strideA, tau, Z, ldz, strideZ, n, batch, Tbuf, W1, W2, Vt, shift};
+  int err = 0;
+  BtPlan* plan = plan_for(a, &err);
+  if (!plan) return err ? err : -4;
+  if (use_graph && plan->exec) return (int)hipGraphLaunch(plan->exec, stream);
+  return run_plan(a, *plan, stream);
+}
+
 KFAC_API int kfac_backtransform_prepare(float* A, int lda, long long strideA, const float* tau,
                                         float* Z, int ldz, long long strideZ, int n, int batch,
                                         float* Tbuf, float* W1, float* W2, float* Vt) {

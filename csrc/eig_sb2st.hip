@@ -1,0 +1,443 @@
+// Stage 2 of the two-stage symmetric eigensolver: band (half-bandwidth 16)
+// -> tridiagonal by bulge chasing (reference semantics
+// kfac/layers/utils.py:45-74).  Stage 1 is csrc/eig_sy2sb.hip; the exact
+// operation order is modelled in fp64 by scripts/models/two_stage_model.py
+// (sb2st).
+//
+//   task (s, j):  c = s (j = 0) or s + 1 + (j-1) 16, rows I = r0 .. r1 with
+//                 r0 = s + 1 + 16 j, r1 = min(r0 + 15, n - 1); Householder
+//                 reflector from B[I, c]; B <- H B H on the stored lower band:
+//                 column c, the left block B[I, c+1 .. r0-1], the diagonal
+//                 block B[I, I] (both sides), the block below
+//                 B[r1+1 .. r1+16, I] (the next bulge).
+//   (s+1, j) may run once (s, j+2) is done.
+//
+// Band storage: row r holds B[r][r-31 .. r] (32 floats, row-major, rows n ..
+// n + 31 zero); a task touches the 32 rows r0 .. r0 + 31 only.
+//
+// MI355X mapping: a pipeline of 4-wave workgroups per matrix.  Workgroup g
+// runs the 4 consecutive sweeps 4g .. 4g+3 ("a group"), one per wave, in
+// lockstep ticks -- wave w runs task t - 3 w at tick t, one LDS barrier per
+// tick:
+//   * each wave keeps a 4-block ring of 16-row band blocks in LDS (block k =
+//     rows s+1+16k .. s+16+16k of its sweep); task j works on blocks j, j+1
+//     and fills block j+1 from the previous wave's ring (its blocks j+1 and
+//     j+2, one row shifted), which that wave finished in earlier ticks;
+//   * wave 0 reads its blocks from the band in global memory, two blocks
+//     every other tick, up to five blocks ahead, after polling the previous
+//     workgroup's published block count;
+//   * wave 3 writes each finished block back (sc1 write-through stores) and
+//     publishes its count two ticks later, after its own vmcnt wait (the
+//     guide's sc1-granule hand-off form: stores and loads all sc1, one
+//     publishing wave, one workgroup per CU); workgroup g + 1 -- the next 4
+//     sweeps, on any CU / XCD -- follows ~7 ticks behind.
+// Workgroups are launched in group order (interleaved over the matrices of
+// the batch), so a workgroup only waits on one that was dispatched before
+// it; every wait is bounded (error count, then it proceeds) so a fault can
+// never leave waves spinning.
+// One task = one wave: the reflector on lanes 0-15, then the left block,
+// the diagonal block and the block below side by side on lanes 0-15, 16-31,
+// 32-47 in ONE instruction stream (16 LDS loads, 16 FMAs for the dot, two
+// FMAs per element for the update, 16 LDS stores per lane).
+//
+// Outputs: d, e of the tridiagonal matrix (each finished as the sweep that
+// touched it last leaves it), and the reflectors for the back-transformation
+// (csrc/eig_q2.hip), one 16-float segment per task: v2[s][16 j] = tau,
+// v2[s][16 j + i] = v[i] (v[0] = 1 implicit), zero past the reflector.
+#include "common.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace {
+
+constexpr int SB = 16;            // half-bandwidth
+constexpr int BW = 2 * SB;        // stored floats per band row
+constexpr int RS = 36;            // LDS row stride (16-B aligned rows; conflict-free strides)
+constexpr int NSLOT = 4;          // ring blocks per wave
+constexpr int NW = 4;             // waves (sweeps) per workgroup
+constexpr int LAG = 3;            // ticks between consecutive sweeps
+constexpr int SLOTF = SB * RS;    // floats per ring block
+constexpr int SC1 = 16;           // buffer-op cache policy: sc1 (write-through / L1-bypass)
+constexpr int DONE = 1 << 30;     // published count of a finished sweep
+constexpr int SPIN_MAX = 1 << 22; // bounded waits (~0.3 s)
+constexpr int MAXMAT = 64;
+
+struct SbMat {
+  float* band;            // (n + 32) x 32 band from stage 1, reduced in place
+  float* v2;              // (n - 1) x ldv2 reflectors, zeroed by the caller
+  float* d;
+  float* e;
+  int* prog;              // [groups] published block count of each group's last sweep
+  int* err;               // bounded waits that timed out (0 when healthy)
+  long long ldv2;
+  int n, dbg;             // dbg (timing experiments, KFAC_SB2ST_DBG): 1 = no polls, 2 = no publish wait
+};
+struct SbWg { int mat, g; };
+
+__device__ __forceinline__ int sweep_tasks(int n, int s) {
+  // tasks j with r0 = s + 1 + 16 j <= n - 2 (a reflector of length >= 2)
+  return (s + 1 <= n - 2) ? (n - 3 - s) / SB + 1 : 0;
+}
+
+// 16-lane row sum (DPP inside each row of 16 lanes; every lane gets its row's sum)
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dpp_f<0xB1>(v);     // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);     // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);    // row_half_mirror
+  v += dpp_f<0x140>(v);    // row_mirror
+  return v;
+}
+
+__device__ __forceinline__ float rdlane(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+__device__ __forceinline__ fx4 band_ld(__amdgpu_buffer_rsrc_t rs, int byte_off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, SC1);
+}
+
+// spin (bounded) until *p >= need; sc1 polls
+// (after one timeout anywhere every later wait returns at once: a broken
+// pipeline ends in ~one SPIN_MAX, with garbage results and err > 0)
+__device__ __forceinline__ void wait_count(int* p, int need, int* err) {
+  if (need <= 0) return;
+  int it = 0;
+  while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+    __builtin_amdgcn_s_sleep(1);
+    if ((++it & 1023) == 0 &&
+        __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+      break;
+    if (it == SPIN_MAX) {
+      atomicAdd(err, 1);
+      break;
+    }
+  }
+}
+
+__global__ __launch_bounds__(64 * NW) void sb2st_kernel(const SbMat* __restrict__ mats,
+                                                       const SbWg* __restrict__ wgs) {
+  const SbWg W = wgs[blockIdx.x];
+  const SbMat M = mats[W.mat];
+  const int n = M.n, grp = W.g;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  extern __shared__ float lds[];                 // NW x NSLOT x SLOTF floats (+ padding)
+  float* my = lds + w * (NSLOT * SLOTF);
+  const float* prod = lds + ((w + NW - 1) % NW) * (NSLOT * SLOTF);
+  AS1 float* v2 = gptr(M.v2);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      M.band, 0, (n + BW) * BW * 4, 0x00020000);
+  if (grp == 0 && tid == 0) {
+    const fx4 r0 = band_ld(rs, 28 * 4);
+    M.d[0] = r0.w;
+    if (n == 2) {
+      const fx4 r1 = band_ld(rs, (BW + 28) * 4);
+      M.d[1] = r1.w; M.e[0] = r1.z;
+    }
+  }
+  const int nsw = n - 2;                          // sweeps with tasks: 0 .. n - 3
+  const int s = grp * NW + w;
+  const int J = s < nsw ? sweep_tasks(n, s) : 0;
+  int T = 0;                                      // ticks of the group (uniform)
+#pragma unroll 1
+  for (int ww = 0; ww < NW; ++ww) {
+    const int ss = grp * NW + ww;
+    const int jj = ss < nsw ? sweep_tasks(n, ss) : 0;
+    if (jj > 0) T = max(T, LAG * ww + jj);
+  }
+  // copy lane: block row i = lane >> 2, quarter qd = lane & 3 (8 floats)
+  const int ci = lane >> 2, cq = lane & 3;
+  const int g = lane >> 4, li = lane & 15;
+  int* prev = grp > 0 ? M.prog + grp - 1 : nullptr;
+  int* mine = M.prog + grp;
+  // producer blocks (previous group's last sweep s - 1 of wave 0) that block k
+  // of wave 0's sweep needs: rows s+1+16k .. min(s+16+16k, n-1)
+  auto need_of = [&](int k) {
+    const int rlo = s + 1 + SB * k;
+    if (rlo > n - 1) return 0;
+    const int rhi = min(s + SB + SB * k, n - 1);
+    return (rhi - s) / SB + 1;
+  };
+  fx4 R0[2], R1[2], R2[2], R3[2];
+  auto gload = [&](int k, fx4 (&dst)[2]) {
+    const int r = s + 1 + SB * k + ci;
+    const bool ok = r < n;
+    const int o = ok ? (r * BW + cq * 8) * 4 : 0;
+    const fx4 a = band_ld(rs, o);
+    const fx4 b = band_ld(rs, o + 16);
+    const fx4 z = {0.f, 0.f, 0.f, 0.f};
+    dst[0] = ok ? a : z;
+    dst[1] = ok ? b : z;
+  };
+  auto lput = [&](int k, const fx4 (&src)[2]) {
+    float* dst = my + (k % NSLOT) * SLOTF + ci * RS + cq * 8;
+    *(fx4*)dst = src[0];
+    *(fx4*)(dst + 4) = src[1];
+  };
+  if (w == 0 && J > 0) {
+    if (prev && !(M.dbg & 1)) wait_count(prev, need_of(3), M.err);
+    gload(0, R0); gload(1, R1); gload(2, R2); gload(3, R3);
+    lput(0, R0);
+  }
+  // fill my block k from the previous wave's blocks k (rows 1..15) and
+  // k + 1 (row 0); rows past n read as zero
+  auto ring_fill = [&](int k) {
+    const int r = s + 1 + SB * k + ci;
+    const float* src = (ci < SB - 1) ? prod + (k % NSLOT) * SLOTF + (ci + 1) * RS
+                                     : prod + ((k + 1) % NSLOT) * SLOTF;
+    fx4 a = *(const fx4*)(src + cq * 8);
+    fx4 b = *(const fx4*)(src + cq * 8 + 4);
+    const fx4 z = {0.f, 0.f, 0.f, 0.f};
+    float* dst = my + (k % NSLOT) * SLOTF + ci * RS + cq * 8;
+    *(fx4*)dst = r < n ? a : z;
+    *(fx4*)(dst + 4) = r < n ? b : z;
+  };
+  auto band_st = [&](int k) {
+    const int r = s + 1 + SB * k + ci;
+    const float* src = my + (k % NSLOT) * SLOTF + ci * RS + cq * 8;
+    if (r < n) {
+      __builtin_amdgcn_raw_buffer_store_b128(*(const fx4*)src, rs, (r * BW + cq * 8) * 4, 0, SC1);
+      __builtin_amdgcn_raw_buffer_store_b128(*(const fx4*)(src + 4), rs, (r * BW + cq * 8 + 4) * 4,
+                                             0, SC1);
+    }
+  };
+
+#pragma unroll 1
+  for (int t = 0; t < T; ++t) {
+    const int j = t - LAG * w;
+    if (w > 0 && J > 0 && j == -1) ring_fill(0);
+    if (j >= 0 && j < J) {
+      // ---- block j + 1 (the rows below this task's reflector)
+      if (w == 0) {
+        switch ((j + 1) & 3) {
+          case 0: lput(j + 1, R0); break;
+          case 1: lput(j + 1, R1); break;
+          case 2: lput(j + 1, R2); break;
+          default: lput(j + 1, R3); break;
+        }
+        if ((j & 1) == 0) {
+          // blocks j+4, j+5 into the sets of blocks j, j+1 (both in LDS now)
+          if (prev && !(M.dbg & 1)) wait_count(prev, need_of(j + 5), M.err);
+          if (j & 2) { gload(j + 4, R2); gload(j + 5, R3); }
+          else { gload(j + 4, R0); gload(j + 5, R1); }
+        }
+      } else {
+        ring_fill(j + 1);
+      }
+      if (w == NW - 1) {
+        // publish the blocks stored two tasks ago (their stores are the only
+        // memory ops this wave issued before the last ~4)
+        if (!(M.dbg & 2)) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        __hip_atomic_store(mine, j > 0 ? j - 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const int r0 = s + 1 + SB * j;
+      const int L = min(SB, n - r0);            // >= 2
+      float* S0 = my + (j % NSLOT) * SLOTF;
+      float* S1 = my + ((j + 1) % NSLOT) * SLOTF;
+      // ---- reflector from column c (lanes 0..15: row i = lane)
+      const int xo = (j == 0) ? 30 : 15;        // column c's offset in row i: xo - i
+      const int xa = 35 * (lane & 15) + xo;
+      const float xl = S0[xa];
+      const float x = (lane < L) ? xl : 0.f;
+      const float alpha = rdlane(x, 0);
+      const float sig = wave_sum((lane >= 1 && lane < L) ? x * x : 0.f);
+      float tau = 0.f, beta = alpha, scal = 0.f;
+      if (sig != 0.f) {
+        beta = -copysignf(sqrtf(alpha * alpha + sig), alpha);
+        tau = (beta - alpha) / beta;
+        scal = 1.f / (alpha - beta);
+      }
+      const float v = lane == 0 ? 1.f : ((lane < L) ? x * scal : 0.f);
+      if (lane < L) {
+        S0[xa] = lane == 0 ? beta : 0.f;
+        v2[(long long)s * M.ldv2 + SB * j + lane] = lane == 0 ? tau : v;
+      }
+      if (tau != 0.f) {
+        float vl[SB];
+#pragma unroll
+        for (int l = 0; l < SB; ++l) vl[l] = rdlane(v, l);
+        // ---- element l of this lane's vector:
+        //   g0 (left, j >= 1): column c+1+li, row l     -> S0 + 16 + li + 35 l
+        //   g1 (diagonal, row li): l <= li -> S0 + 35 li + 31 + l
+        //                          l >  li -> S0 + 35 l + li + 31
+        //   g2 (below, row 16+li): column r0+l           -> S1 + 35 li + 15 + l
+        const bool act = (g == 0 && j > 0 && li < SB - 1) || g == 1 || g == 2;
+        float* base;
+        int stride;
+        if (g == 0) { base = S0 + 16 + li; stride = 35; }
+        else if (g == 1) { base = S0 + 35 * li + 31; stride = 1; }
+        else { base = S1 + 35 * li + 15; stride = 1; }
+        if (!act) { base = S0; stride = 0; }
+        float val[SB];
+        float dot = 0.f;
+#pragma unroll
+        for (int l = 0; l < SB; ++l) {
+          const float* pa = (g == 1 && l > li) ? (S0 + 35 * l + li + 31) : (base + stride * l);
+          val[l] = *pa;
+          dot += val[l] * vl[l];
+        }
+        // g1: w = tau D v - K v, K = tau / 2 v^T (tau D v)
+        const float p = tau * dot;
+        const float kk = 0.5f * tau * row_sum16(vl[li] * p);
+        const float wv = p - kk * vl[li];
+        float wl[SB];
+#pragma unroll
+        for (int l = 0; l < SB; ++l) wl[l] = rdlane(wv, 16 + l);
+        // update: g0 / g2 -= (tau dot) v[l]; g1 -= w v[l] + v[li] w[l] (lower only)
+        const float a1 = (g == 1) ? wv : p;
+        const float a2 = (g == 1) ? vl[li] : 0.f;
+#pragma unroll
+        for (int l = 0; l < SB; ++l) {
+          const bool st = act && !(g == 1 && l > li);
+          const float nv = val[l] - (a1 * vl[l] + a2 * wl[l]);
+          float* pa = base + stride * l;
+          if (st) *pa = nv;
+        }
+      }
+      // ---- outputs finished by this task
+      if (j == 0 && lane == 0) {
+        M.d[s + 1] = S0[31];
+        M.e[s] = S0[30];
+        if (s == n - 3) { M.d[n - 1] = S0[RS + 31]; M.e[n - 2] = S0[RS + 30]; }
+      }
+      // ---- the group's last sweep hands its finished blocks to the next group
+      if (w == NW - 1) {
+        band_st(j);
+        if (j == J - 1) {
+          band_st(j + 1);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_store(mine, DONE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+    kfac_lds_barrier();
+  }
+  // a group whose last sweep has no task still releases its successor
+  if (w == NW - 1 && J == 0 && lane == 0)
+    __hip_atomic_store(mine, DONE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(256) void sb2st_zero_kernel(int* p, int n) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) p[i] = 0;
+}
+
+struct SbPlan {
+  SbMat* d_mats = nullptr;
+  SbWg* d_wgs = nullptr;
+  int* d_prog = nullptr;       // all matrices' group counters, then the error count
+  int nprog = 0, nwg = 0;
+  hipGraphExec_t exec = nullptr;
+};
+
+// 37 KB of ring per workgroup, padded so that exactly one workgroup sits on a
+// CU (the sc1 hand-off's measured form)
+constexpr size_t LDS_BYTES = 96 * 1024;
+static_assert((size_t)NW * NSLOT * SLOTF * sizeof(float) <= LDS_BYTES, "ring exceeds LDS");
+
+int enqueue(const SbPlan& P, hipStream_t s) {
+  hipLaunchKernelGGL(sb2st_zero_kernel, dim3(4), dim3(256), 0, s, P.d_prog, P.nprog + 1);
+  hipLaunchKernelGGL(sb2st_kernel, dim3(P.nwg), dim3(64 * NW), LDS_BYTES, s, P.d_mats, P.d_wgs);
+  return (int)hipGetLastError();
+}
+
+std::mutex g_mu;
+std::map<std::string, SbPlan> g_plans;
+
+}  // namespace
+
+struct KfacSb2stRecord {
+  const float* band_in; float* band; float* v2; float* d; float* e; long long ldv2; long long n;
+};
+
+// Band -> tridiagonal for `count` matrices (n >= 2): band ((n+32) x 32, the
+// stage-1 lower band, reduced in place; band_in must equal band), v2 ((n-1) x
+// ldv2, ldv2 >= n + 16, zeroed by the caller), d (n), e (n-1).  A pipeline of
+// ceil((n-2)/4) workgroups per matrix.
+KFAC_API int kfac_sb2st_batched(const KfacSb2stRecord* recs, int count, int use_graph,
+                                hipStream_t stream) {
+  if (count > MAXMAT) return -5;
+  if (count <= 0) return 0;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)sb2st_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)LDS_BYTES) != hipSuccess)
+      return -7;
+    attr = true;
+  }
+  std::vector<SbMat> mats(count);
+  std::vector<int> ngrp(count);
+  int nprog = 0;
+  for (int i = 0; i < count; ++i) {
+    const KfacSb2stRecord& r = recs[i];
+    if (r.n < 2 || r.ldv2 < r.n + SB || r.band_in != r.band) return -2;
+    SbMat& M = mats[i];
+    memset(&M, 0, sizeof(M));
+    M.band = r.band; M.v2 = r.v2; M.d = r.d; M.e = r.e;
+    M.ldv2 = r.ldv2; M.n = (int)r.n;
+    M.dbg = getenv("KFAC_SB2ST_DBG") ? atoi(getenv("KFAC_SB2ST_DBG")) : 0;
+    const int nsw = (int)r.n - 2;
+    ngrp[i] = nsw > 0 ? (nsw + NW - 1) / NW : 1;
+    nprog += ngrp[i];
+  }
+  hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cst) != hipSuccess) return -3;
+  const bool graph = use_graph && stream != nullptr && cst == hipStreamCaptureStatusNone;
+  const std::string key((const char*)mats.data(), sizeof(SbMat) * mats.size());
+  SbPlan* plan;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_plans.find(key);
+    if (it == g_plans.end()) {
+      SbPlan P;
+      int err;
+      if ((err = (int)hipMalloc(&P.d_prog, sizeof(int) * (nprog + 1))) != 0) return err;
+      P.nprog = nprog;
+      int off = 0;
+      for (int i = 0; i < count; ++i) {
+        mats[i].prog = P.d_prog + off;
+        mats[i].err = P.d_prog + nprog;
+        off += ngrp[i];
+      }
+      // launch order: group-major, interleaved over matrices, so every
+      // workgroup's predecessor (same matrix, group - 1) was dispatched first
+      std::vector<SbWg> wgs;
+      int gmax = 0;
+      for (int i = 0; i < count; ++i) gmax = std::max(gmax, ngrp[i]);
+      for (int g = 0; g < gmax; ++g)
+        for (int i = 0; i < count; ++i)
+          if (g < ngrp[i]) wgs.push_back(SbWg{i, g});
+      P.nwg = (int)wgs.size();
+      if ((err = (int)hipMalloc(&P.d_mats, sizeof(SbMat) * count)) != 0) return err;
+      if ((err = (int)hipMemcpy(P.d_mats, mats.data(), sizeof(SbMat) * count,
+                                hipMemcpyHostToDevice)) != 0)
+        return err;
+      if ((err = (int)hipMalloc(&P.d_wgs, sizeof(SbWg) * wgs.size())) != 0) return err;
+      if ((err = (int)hipMemcpy(P.d_wgs, wgs.data(), sizeof(SbWg) * wgs.size(),
+                                hipMemcpyHostToDevice)) != 0)
+        return err;
+      it = g_plans.emplace(key, P).first;
+    }
+    plan = &it->second;
+    if (graph && !plan->exec) {
+      static hipStream_t cap = nullptr;
+      if (!cap && hipStreamCreateWithFlags(&cap, hipStreamNonBlocking) != hipSuccess) cap = nullptr;
+      hipGraph_t gr = nullptr;
+      if (cap && hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal) == hipSuccess) {
+        const int e1 = enqueue(*plan, cap);
+        const hipError_t e2 = hipStreamEndCapture(cap, &gr);
+        if (!e1 && e2 == hipSuccess && gr &&
+            hipGraphInstantiate(&plan->exec, gr, nullptr, nullptr, 0) != hipSuccess)
+          plan->exec = nullptr;
+        if (gr) (void)hipGraphDestroy(gr);
+      }
+      (void)hipGetLastError();
+    }
+  }
+  if (graph && plan->exec) return (int)hipGraphLaunch(plan->exec, stream);
+  return enqueue(*plan, stream);
+}

@@ -39,9 +39,18 @@ import torch
 import torch.distributed as dist
 
 __all__ = ['Ops', 'CommGroup', 'CommBackend', 'TorchBackend', 'Handle',
-           'init_comm_backend', 'reset_comm_backend', 'backend']
+           'init_comm_backend', 'reset_comm_backend', 'backend', 'build_log']
 
 backend = None
+# every communicator construction, in program order (identical on every rank;
+# bench.py reports it so a multi-GPU run says how its groups were built)
+build_log = []
+
+
+def _record(what, method, ranks):
+    build_log.append({'what': what, 'method': method,
+                      'ranks': [list(r) for r in ranks] if ranks and
+                      isinstance(ranks[0], (list, tuple)) else list(ranks)})
 
 
 class Ops(enum.Enum):
@@ -61,6 +70,7 @@ def reset_comm_backend():
     """Forget the selected backend and cached groups (tests / re-init)."""
     global backend
     backend = None
+    del build_log[:]
     CommGroup._cache.clear()
     CommGroup._partitions.clear()
 
@@ -86,12 +96,15 @@ def _new_world_group():
     ranks = list(range(world))
     if _can_split():
         try:
-            return dist.split_group(split_ranks=[ranks], group_desc='kfac_world')
+            g = dist.split_group(split_ranks=[ranks], group_desc='kfac_world')
+            _record('kfac_world', 'split_group', ranks)
+            return g
         except Exception as e:   # pragma: no cover - depends on the RCCL build
             # an API-level refusal is the same on every rank: all fall back
             import warnings
             warnings.warn('ncclCommSplit of the K-FAC world failed ({}); using new_group'
                           .format(e))
+    _record('kfac_world', 'new_group', ranks)
     return dist.new_group(ranks)
 
 
@@ -108,14 +121,18 @@ class CommGroup(object):
     _cache = {}
     _partitions = {}
 
-    def __init__(self, ranks, group=None):
+    def __init__(self, ranks, group=None, create=True):
         self.ranks = sorted(int(r) for r in ranks)
         key = tuple(self.ranks)
         self.group = group
-        if group is None and _dist_ready():
+        # create=False: bookkeeping for a group this rank is not in whose
+        # communicator came from a collective split (new_group is collective
+        # over the world: calling it on some ranks only would mismatch)
+        if group is None and create and _dist_ready():
             world = dist.get_world_size()
             if 1 < len(self.ranks) < world:
                 if key not in CommGroup._cache:
+                    _record('group', 'new_group', self.ranks)
                     CommGroup._cache[key] = dist.new_group(self.ranks)
                 self.group = CommGroup._cache[key]
 
@@ -145,8 +162,9 @@ class CommGroup(object):
                 # every rank in order: parent rank == global rank)
                 mine = dist.split_group(parent_pg=backend.kfac_world, split_ranks=multi,
                                         group_desc='kfac_sub')
-                out = [cls(g, group=mine if (me in g and 1 < len(g) < world) else None)
-                       for g in lists]
+                _record('partition', 'split_group', multi)
+                out = [cls(g, group=mine if (me in g and 1 < len(g) < world) else None,
+                           create=False) for g in lists]
             else:
                 out = [cls(g) for g in lists]
         cls._partitions[key] = out
@@ -217,6 +235,9 @@ class CommBackend(object):
     def barrier(self):
         return None
 
+    def counters(self):
+        return {}
+
     def sync(self, handles):
         if handles is None:
             return
@@ -240,6 +261,16 @@ class TorchBackend(CommBackend):
 
     def __init__(self):
         self.kfac_world = _new_world_group()
+        self.stats = {}     # op -> [calls, bytes] issued by this rank
+
+    def _count(self, op, tensor):
+        st = self.stats.setdefault(op, [0, 0])
+        st[0] += 1
+        st[1] += tensor.numel() * tensor.element_size()
+
+    def counters(self):
+        """{op: (calls, bytes)} of every collective this backend issued."""
+        return {k: tuple(v) for k, v in self.stats.items()}
 
     def size(self):
         return dist.get_world_size()
@@ -270,6 +301,7 @@ class TorchBackend(CommBackend):
         if skip:
             return None
         divisor = gsize if op == Ops.Average else None
+        self._count('all_reduce', tensor)
         work = dist.all_reduce(tensor, async_op=async_op, **kw)
         h = Handle(work if async_op else None, tensor, divisor)
         if not async_op:
@@ -281,6 +313,7 @@ class TorchBackend(CommBackend):
         skip, kw, _ = self._resolve(group)
         if skip:
             return None
+        self._count('broadcast', tensor)
         work = dist.broadcast(tensor, src=src, async_op=async_op, **kw)
         return Handle(work) if async_op else None
 
@@ -288,6 +321,7 @@ class TorchBackend(CommBackend):
         skip, kw, gsize = self._resolve(group)
         if skip:
             return None
+        self._count('reduce', tensor)
         work = dist.reduce(tensor, dst=dst, async_op=async_op, **kw)
         divisor = gsize if (op == Ops.Average and self.rank() == dst) else None
         h = Handle(work if async_op else None, tensor, divisor)
@@ -301,6 +335,7 @@ class TorchBackend(CommBackend):
         if skip:
             outputs[0].copy_(tensor)
             return None
+        self._count('all_gather', tensor)
         work = dist.all_gather(outputs, tensor, async_op=async_op, **kw)
         return Handle(work) if async_op else None
 
@@ -308,6 +343,7 @@ class TorchBackend(CommBackend):
         skip, kw, _ = self._resolve(group)
         if skip:
             return super().allgather_into(output, tensor)
+        self._count('all_gather_into_tensor', output)
         work = dist.all_gather_into_tensor(output, tensor, async_op=async_op, **kw)
         return Handle(work) if async_op else None
 

@@ -57,7 +57,32 @@ class DcRecord(ctypes.Structure):
                 ('ws', c_vp), ('n', c_ll)]
 
 
+class Sy2sbRecord(ctypes.Structure):
+    # csrc/eig_sy2sb.hip KfacSy2sbRecord
+    _fields_ = [('A', c_vp), ('lda', c_ll), ('tau', c_vp), ('band', c_vp), ('ws', c_vp),
+                ('n', c_ll)]
+
+
+class Sb2stRecord(ctypes.Structure):
+    # csrc/eig_sb2st.hip KfacSb2stRecord
+    _fields_ = [('band_in', c_vp), ('band', c_vp), ('v2', c_vp), ('d', c_vp), ('e', c_vp),
+                ('ldv2', c_ll), ('n', c_ll)]
+
+
+class Q2Record(ctypes.Structure):
+    # csrc/eig_q2.hip KfacQ2Record
+    _fields_ = [('Z', c_vp), ('v2', c_vp), ('ldz', c_ll), ('ldv2', c_ll), ('n', c_ll)]
+
+
 _SIGS = {
+    'kfac_sy2sb_batched': [ctypes.POINTER(Sy2sbRecord), c_int, c_int, c_vp],
+    'kfac_sy2sb_ws_floats': [c_ll],
+    'kfac_sy2sb_nmax': [],
+    'kfac_sb2st_batched': [ctypes.POINTER(Sb2stRecord), c_int, c_int, c_vp],
+    'kfac_q2_batched': [ctypes.POINTER(Q2Record), c_int, c_int, c_vp],
+    'kfac_q2_nmax': [],
+    'kfac_band_backtransform': [c_vp, c_int, c_ll, c_vp, c_vp, c_int, c_ll, c_int, c_int,
+                                c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp],
     'kfac_syrk_patch': [c_int, c_vp, c_ll, c_ll, c_ll, c_ll, c_int, c_int, c_int, c_int, c_int,
                         c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_vp, c_int,
                         c_int, c_vp, c_vp, c_vp],
@@ -121,7 +146,7 @@ _SIGS = {
 }
 
 
-_RESTYPES = {'kfac_dc_ws_bytes': c_ll,
+_RESTYPES = {'kfac_dc_ws_bytes': c_ll, 'kfac_sy2sb_ws_floats': c_ll,
              'kfac_reduce_ws_floats': c_ll, 'kfac_syrk_splits': c_ll,
              'kfac_chol_ws_bytes': c_ll, 'kfac_chol_info_offset': c_ll,
              'kfac_syrk_problem_set_part': None, 'kfac_syrk_problem_set_dscale': None,

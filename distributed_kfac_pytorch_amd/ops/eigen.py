@@ -330,6 +330,110 @@ def _fused_group(mats, clip, stream, use_graph, slot=0):
     return outs
 
 
+# Two-stage path (csrc/eig_sy2sb.hip -> eig_sb2st.hip -> eig_dc.hip ->
+# eig_q2.hip -> eig_backtransform.hip with shift 16): dense -> band in 16-wide
+# panels (16x fewer passes over the trailing matrix than the one-stage
+# column chain), bulge chasing with every hand-off inside one CU, then the
+# two back-transformations.  Factors with TWO_STAGE_MIN <= n <= TWO_STAGE_MAX
+# take it when KFAC_EIG_TWO_STAGE=1; the rest stay on the one-stage path, on
+# the other streams.
+TWO_STAGE = bool(int(os.environ.get('KFAC_EIG_TWO_STAGE', '0')))
+TWO_STAGE_MIN = int(os.environ.get('KFAC_EIG_TWO_STAGE_MIN', '1024'))
+TWO_STAGE_MAX = 5120     # csrc/eig_sy2sb.hip NMAX2, csrc/eig_q2.hip 16 x QT
+SB2 = 16                 # band half-bandwidth
+_TS_BUFS = {}
+
+
+def _ts_buffers(dev, n, b, slot=0):
+    key = (str(dev), n, b, slot)
+    bufs = _TS_BUFS.get(key)
+    if bufs is None:
+        L = _lib.lib()
+        lda = (n + 127) // 128 * 128
+        ldv2 = (n + 15) // 16 * 16 + 16
+        f32 = dict(dtype=torch.float32, device=dev)
+        nblk = (n + BT - 1) // BT
+        wsb = int(L.kfac_dc_ws_bytes(n))
+        bufs = dict(lda=lda, ldv2=ldv2, sA=lda * lda,
+                    A=torch.zeros(b, lda, lda, **f32), tau=torch.zeros(b, n, **f32),  # larft: stride n
+                    band=torch.zeros(b, (n + 2 * SB2) * 2 * SB2, **f32),
+                    syws=torch.zeros(b, int(L.kfac_sy2sb_ws_floats(lda)), **f32),
+                    v2=torch.zeros(b, max(n - 1, 1), ldv2, **f32),
+                    d=torch.zeros(b, n, **f32), e=torch.zeros(b, n, **f32),
+                    w=torch.zeros(b, n, **f32), Z=torch.zeros(b, n, lda, **f32),
+                    wsb=wsb, dcws=torch.zeros(b * wsb, dtype=torch.uint8, device=dev),
+                    T=torch.zeros(2 * b * nblk * BT * BT, **f32),
+                    W1=torch.zeros(b * BT * n, **f32), W2=torch.zeros(b * BT * n, **f32),
+                    Vt=torch.zeros(b * BT * lda, **f32))
+        _TS_BUFS[key] = bufs
+    return bufs
+
+
+def _two_stage_group(mats, clip, stream, use_graph=True, slot=0):
+    """Every matrix of `mats` (TWO_STAGE_MIN..TWO_STAGE_MAX) through the
+    two-stage solver on `stream`: one batched launch sequence per stage."""
+    dev = mats[0].device
+    L = _lib.lib()
+    classes = {}
+    for i, A in enumerate(mats):
+        classes.setdefault(A.shape[0], []).append(i)
+    order = sorted(classes.items(), key=lambda kv: -kv[0])
+    total = len(mats)
+    outs = [None] * total
+    with torch.cuda.stream(stream):
+        cs = _lib.c_vp(stream.cuda_stream)
+        r1 = (_lib.Sy2sbRecord * total)()
+        r2 = (_lib.Sb2stRecord * total)()
+        r3 = (_lib.DcRecord * total)()
+        r4 = (_lib.Q2Record * total)()
+        k = 0
+        bufs = []
+        for n, idx in order:
+            b = len(idx)
+            B = _ts_buffers(dev, n, b, slot)
+            bufs.append((n, idx, B))
+            dcr = _dc_records(B, n, b)
+            for i, m in enumerate(idx):
+                B['A'][i, :n, :n].copy_(mats[m])
+                r = r1[k]
+                r.A, r.lda, r.tau = B['A'][i].data_ptr(), B['lda'], B['tau'][i].data_ptr()
+                r.band, r.ws, r.n = B['band'][i].data_ptr(), B['syws'][i].data_ptr(), n
+                q = r2[k]
+                q.band_in = q.band = B['band'][i].data_ptr()
+                q.v2, q.d, q.e = B['v2'][i].data_ptr(), B['d'][i].data_ptr(), B['e'][i].data_ptr()
+                q.ldv2, q.n = B['ldv2'], n
+                r3[k] = dcr[i]
+                z = r4[k]
+                z.Z, z.v2, z.ldz, z.ldv2, z.n = (B['Z'][i].data_ptr(), B['v2'][i].data_ptr(),
+                                                 B['lda'], B['ldv2'], n)
+                k += 1
+        _lib.check(L.kfac_sy2sb_batched(r1, total, int(use_graph), cs), 'kfac_sy2sb_batched')
+        _lib.check(L.kfac_sb2st_batched(r2, total, int(use_graph), cs), 'kfac_sb2st_batched')
+        _lib.check(L.kfac_dc_batched(r3, total, int(use_graph), cs), 'kfac_dc_batched')
+        _lib.check(L.kfac_q2_batched(r4, total, int(use_graph), cs), 'kfac_q2_batched')
+        for n, idx, B in bufs:
+            b = len(idx)
+            lda = B['lda']
+            _lib.check(L.kfac_band_backtransform(
+                _lib.ptr(B['A']), lda, B['sA'], _lib.ptr(B['tau']), _lib.ptr(B['Z']), lda,
+                n * lda, n, b, _lib.ptr(B['T']), _lib.ptr(B['W1']), _lib.ptr(B['W2']),
+                _lib.ptr(B['Vt']), SB2, int(use_graph), cs), 'kfac_band_backtransform')
+            _INFOS.append(_dc_info(B, n, b))
+            Q = B['Z'][:, :, :n].transpose(1, 2).contiguous()
+            D = B['w'].clone()
+            if clip is not None:
+                D.clamp_(min=clip)
+            for i, m in enumerate(idx):
+                outs[m] = (Q[i], D[i])
+    return outs
+
+
+def two_stage_eigh(mats, clip=0.0, use_graph=True):
+    """The two-stage solver on the current stream (tests, probes)."""
+    cur = torch.cuda.current_stream(mats[0].device)
+    return _two_stage_group([A.float().contiguous() for A in mats], clip, cur, use_graph)
+
+
 def check_solver_status():
     """Host-side check of every divide-and-conquer call issued since the last
     check (info != 0 -> the solver did not converge).  Syncs; call once per
@@ -373,14 +477,34 @@ def symeig_many(mats, clip=0.0, solver='auto'):
     if small:
         for i, r in zip(small, _jacobi_small([mats[i] for i in small], clip)):
             outs[i] = r
+    ts = []
+    if TWO_STAGE:
+        ts = [i for i in large if TWO_STAGE_MIN <= mats[i].shape[0] <= TWO_STAGE_MAX]
+        large = [i for i in large if i not in set(ts)]
+    cur = torch.cuda.current_stream(mats[0].device)
+    side = None
+    if ts:
+        # the two-stage group on its own stream, under the one-stage chains
+        side = _side_streams(mats[0].device, FUSED_STREAMS + 1)[-1]
+        side.wait_stream(cur)
+        sub = [mats[i] for i in ts]
+        res = _two_stage_group(sub, clip, side)
+        for A in sub:
+            A.record_stream(side)
+        for i, r in zip(ts, res):
+            outs[i] = r
     if large:
         sub = [mats[i] for i in large]
-        cur = torch.cuda.current_stream(sub[0].device)
         res = _large_fused(sub, clip, cur)
         for A in sub:
             A.record_stream(cur)
         for i, r in zip(large, res):
             outs[i] = r
+    if side is not None:
+        cur.wait_stream(side)
+        for i in ts:
+            outs[i][0].record_stream(cur)
+            outs[i][1].record_stream(cur)
     return outs
 
 

@@ -1156,6 +1156,45 @@ class KFAC(optim.Optimizer):
             b += size(layer.preconditioned_gradient)
         return b
 
+    def comm_summary(self):
+        """How this rank's K-FAC communication is laid out (JSON-able): the
+        backend and world it saw, how the K-FAC world communicator and the
+        inverse / gradient sub-groups were built (ncclCommSplit via
+        dist.split_group, or new_group), the factor all-reduce buckets and the
+        eigendata / gradient arena sizes, and the collectives issued so far.
+        Reference: kfac/comm.py:53-64 (CommGroup -> dist.new_group),
+        kfac/preconditioner.py:525-553 (one collective per layer and factor)."""
+        import torch.distributed as dist
+        be = comm.backend
+        out = {'backend': dist.get_backend() if (dist.is_available() and dist.is_initialized())
+               else 'none',
+               'world_size': be.size() if be is not None else 1,
+               'kfac_world': None, 'groups': [], 'factor_allreduce': None,
+               'eig_arena_bytes': None, 'grad_arena_bytes': None,
+               'collectives': be.counters() if be is not None else {}}
+        for rec in comm.build_log:
+            if rec['what'] == 'kfac_world':
+                out['kfac_world'] = {'size': len(rec['ranks']), 'built_by': rec['method']}
+            else:
+                out['groups'].append({'built_by': rec['method'], 'ranks': rec['ranks']})
+        far = self._factor_allreduce
+        if far is not None and far.buckets:
+            sizes = []
+            for dtype, st, en, _ in far.buckets:
+                esize = torch.tensor([], dtype=dtype).element_size()
+                sizes.append((en - st) * esize)
+            out['factor_allreduce'] = {'buckets': len(sizes), 'bucket_bytes': sizes,
+                                       'bucket_cap_mb': self.bucket_cap_mb,
+                                       'triu_packed': far.symmetric}
+        if self.plan is not None:
+            p = self.plan
+            out['grad_arena_bytes'] = p.grad_arena.numel() * 4
+            out['grad_group_size'] = p.grad_group.size if p.grad_group is not None else 1
+            if p.eig_arena is not None:
+                out['eig_arena_bytes'] = p.eig_arena.numel() * p.eig_arena.element_size()
+                out['eig_group_size'] = len(p.eig_ranks)
+        return out
+
     # ------------------------------------------------------------ assignment
     def _assign_workers(self):
         """LPT-balance inverse work over ranks and lay out the execution plan."""

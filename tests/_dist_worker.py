@@ -76,6 +76,56 @@ def kfac_strategy(rank, world, port, out_dir, cfg):
     dist.destroy_process_group()
 
 
+def kfac_split_strategy(rank, world, port, out_dir, cfg):
+    """The ncclCommSplit path (comm._can_split / dist.split_group) on gloo:
+    split_group is replaced by a recorder that builds the same groups with
+    new_group, so the construction sequence of every rank can be compared
+    and the strategies still checked against world 1."""
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    os.environ['RANK'] = str(rank)
+    os.environ['WORLD_SIZE'] = str(world)
+    os.environ['LOCAL_RANK'] = str(rank)
+    torch.set_num_threads(1)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from distributed_kfac_pytorch_amd import comm
+    calls = []
+
+    def fake_split_group(parent_pg=None, split_ranks=None, timeout=None, pg_options=None,
+                         group_desc=None):
+        parent = 'default' if parent_pg is None else (
+            'kfac_world' if parent_pg is getattr(comm.backend, 'kfac_world', None) else 'other')
+        calls.append({'parent': parent, 'split_ranks': [list(r) for r in split_ranks],
+                      'desc': group_desc})
+        mine = None
+        for ranks in split_ranks:           # collective: same order on every rank
+            g = dist.new_group(list(ranks))
+            if rank in ranks:
+                mine = g
+        return mine
+
+    dist.split_group = fake_split_group
+    comm._can_split = lambda: True
+    comm.reset_comm_backend()
+    comm.init_comm_backend()
+    import distributed_kfac_pytorch_amd as kfac
+    from tests._oracle_common import build_case, run_steps
+    model, data = build_case({'seed': 0, 'batch': 6, 'steps': cfg['steps']})
+    method = getattr(kfac.CommMethod, cfg['method'])
+    pre = kfac.KFAC(model, factor_update_freq=1, inv_update_freq=cfg.get('inv_freq', 2),
+                    lr=0.05, damping=0.003, comm_method=method,
+                    grad_worker_fraction=cfg.get('fraction', 0.25),
+                    distribute_layer_factors=False)
+    grads, factors = run_steps(model, pre, data, cfg['steps'])
+    summary = pre.comm_summary()
+    torch.save({'grads': grads, 'factors': factors, 'splits': calls,
+                'build_log': list(comm.build_log),
+                'groups': summary['groups'], 'kfac_world': summary['kfac_world']},
+               os.path.join(out_dir, 'rank{}.pt'.format(rank)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def deferred_factor_comm(rank, world, port, out_dir, cfg):
     """Different data per rank.  The factor all-reduce of a factor-only step
     must stay in flight after step() returns (no wait inside step()), be

@@ -116,6 +116,50 @@ def test_strategy_equivalence(tmp_path, world, cfg):
                                          for c in calls['grad']), calls
 
 
+SPLIT_CASES = [{'method': 'COMM_OPT'}, {'method': 'MEM_OPT'},
+               {'method': 'HYBRID_OPT', 'fraction': 0.25}]
+
+
+@pytest.mark.parametrize('cfg', SPLIT_CASES, ids=[c['method'] for c in SPLIT_CASES])
+def test_comm_split_path_world8(tmp_path, cfg):
+    """The RCCL ncclCommSplit construction (comm._can_split() true,
+    dist.split_group) rehearsed on gloo at world 8: every rank issues the
+    same split sequence (K-FAC world from the default group, then one split
+    of the K-FAC world per partition with more than one multi-rank group),
+    the partitions are the reference's (tests/worker_allocator.py goldens),
+    and the strategies still match world 1 (kfac/comm.py:53-64)."""
+    world = 8
+    cfg = dict(cfg, steps=3)
+    ref_grads, ref_factors = _single(cfg)
+    _spawn(_dist_worker.kfac_split_strategy, world, tmp_path, cfg)
+    res = [torch.load(os.path.join(str(tmp_path), 'rank{}.pt'.format(r)), weights_only=False)
+           for r in range(world)]
+    splits0 = res[0]['splits']
+    assert splits0[0] == {'parent': 'default', 'split_ranks': [list(range(world))],
+                          'desc': 'kfac_world'}, splits0
+    for r in range(world):
+        assert res[r]['splits'] == splits0, (r, res[r]['splits'], splits0)
+        assert res[r]['build_log'] == res[0]['build_log']
+        assert res[r]['kfac_world'] == {'size': world, 'built_by': 'split_group'}
+        for gs, rs in zip(res[r]['grads'], ref_grads):
+            for a, b in zip(gs, rs):
+                assert torch.allclose(a, b, rtol=1e-4, atol=1e-6), (r, (a - b).abs().max())
+        for gs, g0 in zip(res[r]['grads'], res[0]['grads']):
+            assert all(torch.equal(a, b) for a, b in zip(gs, g0)), r
+    subs = [c for c in splits0[1:]]
+    assert all(c['parent'] == 'kfac_world' and c['desc'] == 'kfac_sub' for c in subs), subs
+    got = [c['split_ranks'] for c in subs]
+    if cfg['method'] == 'HYBRID_OPT':
+        # grad_workers = 2: inverse groups of 2 contiguous ranks, gradient
+        # groups of 4 strided ranks (reference goldens, SURVEY.md 2.2)
+        assert [[0, 1], [2, 3], [4, 5], [6, 7]] in got, got
+        assert [[0, 2, 4, 6], [1, 3, 5, 7]] in got, got
+    else:
+        # COMM_OPT: inverse group = world, gradient groups singletons; MEM_OPT:
+        # the reverse -- no partition has a multi-rank group below the world
+        assert got == [], got
+
+
 def test_distribute_layer_factors_without_prediv(tmp_path):
     """A and G of a layer on different ranks (reference default for COMM_OPT
     once prediv is off): still bit-identical."""
