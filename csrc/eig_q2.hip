@@ -51,19 +51,20 @@ __device__ __forceinline__ float wave_shr1(float v) {
                                                     0xF, 0xF, false));
 }
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+constexpr int QP = QR / 2;     // row pairs: one packed (v_pk_fma_f32) lane-pair per component
+
 struct Q2State {
-  float z[QR][16];
+  f2 z[QP][16];         // z[p][k] = (row 2p, row 2p + 1) at slot k
   fx4 vn[4];            // reflectors of the next sweep (prefetched)
-  float zin[QR];        // thread 0: Z[k][s] (prefetched)
+  float zc[QR];         // wave 0, lane l < 16: Z[k][base + l] of the current block of 16 sweeps
 };
 
 // one sweep s with PH = s mod 16 known at compile time
 template <int PH>
-__device__ __forceinline__ void q2_sweep(Q2State& S, int s, const Q2Mat& M, int t, int k0,
-                                         float (*sx)[QW][QR]) {
+__device__ __forceinline__ void q2_sweep(Q2State& S, int s, int t, __amdgpu_buffer_rsrc_t rsv,
+                                         int vof, int ldv4, float (*sx)[QW][QR]) {
   const int lane = t & 63, w = t >> 6;
-  const AS1 float* V2 = gptr(M.v2);
-  const AS1 float* Z = gptr(M.Z);
   float V[16];
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
@@ -73,17 +74,13 @@ __device__ __forceinline__ void q2_sweep(Q2State& S, int s, const Q2Mat& M, int 
   // prefetch sweep s - 1 (segment t; threads past the last segment read
   // nothing: their window holds only zero padding) and, for thread 0, Z[k][s]
   {
+    // buffer loads: the per-thread offset is fixed, the sweep's row offset
+    // uniform (threads past the last segment get an out-of-range offset:
+    // zeros, and their window holds only zero padding)
     const int sp = s > 0 ? s - 1 : 0;
-    const bool on = 16 * t < M.n;
-    const long long vo = on ? (long long)sp * M.ldv2 + 16 * t : 0;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) S.vn[c] = *(const AS1 fx4*)(V2 + vo + 4 * c);
-  }
-  float zin[QR];
-#pragma unroll
-  for (int r = 0; r < QR; ++r) {
-    const bool ok = t == 0 && k0 + r < M.n;
-    zin[r] = gld_if(Z, (long long)(k0 + r) * M.ldz + s, ok, 0.f);
+    for (int c = 0; c < 4; ++c)
+      S.vn[c] = __builtin_amdgcn_raw_buffer_load_b128(rsv, vof + 16 * c, sp * ldv4, 0);
   }
   const float tau = V[0];
   // slot k holds component with v index i = (k - PH - 1) mod 16
@@ -94,29 +91,36 @@ __device__ __forceinline__ void q2_sweep(Q2State& S, int s, const Q2Mat& M, int 
     vk[k] = (i == 0) ? 1.f : V[i];
   }
 #pragma unroll
-  for (int r = 0; r < QR; ++r) {
-    float d = 0.f;
+  for (int p = 0; p < QP; ++p) {
+    f2 d0 = {0.f, 0.f}, d1 = {0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < 16; ++k) d += vk[k] * S.z[r][k];
-    const float f = tau * d;
+    for (int k = 0; k < 16; k += 2) {
+      d0 = __builtin_elementwise_fma(S.z[p][k], (f2){vk[k], vk[k]}, d0);
+      d1 = __builtin_elementwise_fma(S.z[p][k + 1], (f2){vk[k + 1], vk[k + 1]}, d1);
+    }
+    const f2 f = -tau * (d0 + d1);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) S.z[r][k] -= f * vk[k];
+    for (int k = 0; k < 16; ++k) S.z[p][k] = __builtin_elementwise_fma(f, (f2){vk[k], vk[k]}, S.z[p][k]);
   }
   // slide the window down one component: slot PH leaves to thread t + 1,
   // arrives from thread t - 1
   float (*buf)[QR] = sx[s & 1];
 #pragma unroll
-  for (int r = 0; r < QR; ++r) {
-    const float out = S.z[r][PH];
-    if (lane == 63) buf[w][r] = out;
-    S.z[r][PH] = wave_shr1(out);
+  for (int p = 0; p < QP; ++p) {
+    const f2 out = S.z[p][PH];
+    if (lane == 63) { buf[w][2 * p] = out.x; buf[w][2 * p + 1] = out.y; }
+    S.z[p][PH] = (f2){wave_shr1(out.x), wave_shr1(out.y)};
   }
   // LDS-only barrier: __syncthreads() would also drain vmcnt, i.e. wait for
   // the next sweep's reflector prefetch issued above
   kfac_lds_barrier();
-  if (lane == 0) {
+  // thread 0 takes the untouched Z[k][s] (lane PH of wave 0's block copy)
 #pragma unroll
-    for (int r = 0; r < QR; ++r) S.z[r][PH] = (w == 0) ? zin[r] : buf[w - 1][r];
+  for (int p = 0; p < QP; ++p) {
+    const float z0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(S.zc[2 * p]), PH));
+    const float z1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(S.zc[2 * p + 1]), PH));
+    if (lane == 0)
+      S.z[p][PH] = (w == 0) ? (f2){z0, z1} : (f2){buf[w - 1][2 * p], buf[w - 1][2 * p + 1]};
   }
 }
 
@@ -136,25 +140,47 @@ __global__ __launch_bounds__(QT) void q2_kernel(const Q2Mat* __restrict__ mats,
   for (int k = 0; k < 16; ++k) {
     const int x = s0 + 1 + 16 * t + ((k - (s0 + 1)) & 15);
 #pragma unroll
-    for (int r = 0; r < QR; ++r) {
-      const bool ok = x < n && k0 + r < n && s0 >= 0;
-      S.z[r][k] = gld_if(Z, (long long)(k0 + r) * M.ldz + x, ok, 0.f);
+    for (int p = 0; p < QP; ++p) {
+      const int r = 2 * p;
+      const bool ok = x < n && s0 >= 0;
+      S.z[p][k] = (f2){gld_if(Z, (long long)(k0 + r) * M.ldz + x, ok && k0 + r < n, 0.f),
+                       gld_if(Z, (long long)(k0 + r + 1) * M.ldz + x, ok && k0 + r + 1 < n, 0.f)};
     }
   }
   if (s0 >= 0) {
-    const long long vo = (16 * t < n) ? (long long)s0 * M.ldv2 + 16 * t : 0;
+    const __amdgpu_buffer_rsrc_t rsv = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(M.v2), 0, (int)((long long)(n - 1) * M.ldv2 * 4), 0x00020000);
+    const int vof = (16 * t < n) ? 64 * t : 0x7ffffff0;
+    const int ldv4 = (int)M.ldv2 * 4;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) S.vn[c] = *(const AS1 fx4*)(gptr(M.v2) + vo + 4 * c);
+    for (int c = 0; c < 4; ++c)
+      S.vn[c] = __builtin_amdgcn_raw_buffer_load_b128(rsv, vof + 16 * c, s0 * ldv4, 0);
     // blocks of 16 sweeps (phase PH = s mod 16 static in each unrolled body),
     // sweeps outside [0, s0] skipped (uniform)
+    // wave 0, lane l < 16 keeps Z[k][base + l] of the current block (the
+    // components thread 0 takes in over the block's 16 sweeps), the next
+    // block's copy loaded one block ahead
+    const int lane = t & 63;
+    auto zblock = [&](int bs, float (&dst)[QR]) {
+#pragma unroll
+      for (int r = 0; r < QR; ++r) {
+        const bool ok = t < 16 && bs >= 0 && k0 + r < n;
+        dst[r] = gld_if(Z, (long long)(k0 + r) * M.ldz + bs + lane, ok, 0.f);
+      }
+    };
+    zblock(s0 & ~15, S.zc);
 #pragma unroll 1
     for (int base = s0 & ~15; base >= 0; base -= 16) {
+      float zn[QR];
+      zblock(base - 16, zn);
 #define Q2_STEP(PH)                                                   \
-      if (base + PH <= s0) q2_sweep<PH>(S, base + PH, M, t, k0, sx);
+      if (base + PH <= s0) q2_sweep<PH>(S, base + PH, t, rsv, vof, ldv4, sx);
       Q2_STEP(15) Q2_STEP(14) Q2_STEP(13) Q2_STEP(12) Q2_STEP(11) Q2_STEP(10) Q2_STEP(9)
       Q2_STEP(8) Q2_STEP(7) Q2_STEP(6) Q2_STEP(5) Q2_STEP(4) Q2_STEP(3) Q2_STEP(2)
       Q2_STEP(1) Q2_STEP(0)
 #undef Q2_STEP
+#pragma unroll
+      for (int r = 0; r < QR; ++r) S.zc[r] = zn[r];
     }
   }
   // after sweep 0 the window is components 16t .. 16t + 15 (slot k = component 16t + k);
@@ -168,8 +194,11 @@ __global__ __launch_bounds__(QT) void q2_kernel(const Q2Mat* __restrict__ mats,
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       fx4 a;
-      a.x = S.z[r][4 * c + 0]; a.y = S.z[r][4 * c + 1]; a.z = S.z[r][4 * c + 2];
-      a.w = S.z[r][4 * c + 3];
+      const int p = r >> 1;
+      a.x = (r & 1) ? S.z[p][4 * c + 0].y : S.z[p][4 * c + 0].x;
+      a.y = (r & 1) ? S.z[p][4 * c + 1].y : S.z[p][4 * c + 1].x;
+      a.z = (r & 1) ? S.z[p][4 * c + 2].y : S.z[p][4 * c + 2].x;
+      a.w = (r & 1) ? S.z[p][4 * c + 3].y : S.z[p][4 * c + 3].x;
       *(AS1 fx4*)(o + 4 * c) = a;
     }
   }

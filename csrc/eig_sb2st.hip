@@ -76,7 +76,9 @@ struct SbMat {
   int* prog;              // [groups] published block count of each group's last sweep
   int* err;               // bounded waits that timed out (0 when healthy)
   long long ldv2;
-  int n, dbg;             // dbg (timing experiments, KFAC_SB2ST_DBG): 1 = no polls, 2 = no publish wait
+  int n, dbg;             // dbg (timing experiments, KFAC_SB2ST_DBG): 1 = no polls, 2 = no publish wait,
+                          // 8 = per-workgroup start / end stamps, 16 = XCD-affine workgroup order
+  long long* ts;          // dbg & 8: [workgroup][2] s_memrealtime stamps (100 MHz)
 };
 struct SbWg { int mat, g; };
 
@@ -96,6 +98,11 @@ __device__ __forceinline__ float row_sum16(float v) {
 
 __device__ __forceinline__ float rdlane(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// value of lane (lane & 15) of row 0 for every lane (v lives on lanes 0..15)
+__device__ __forceinline__ float rdlane_row(float v, int li) {
+  return __shfl(v, li, 64);
 }
 
 __device__ __forceinline__ fx4 band_ld(__amdgpu_buffer_rsrc_t rs, int byte_off) {
@@ -123,7 +130,9 @@ __device__ __forceinline__ void wait_count(int* p, int need, int* err) {
 __global__ __launch_bounds__(64 * NW) void sb2st_kernel(const SbMat* __restrict__ mats,
                                                        const SbWg* __restrict__ wgs) {
   const SbWg W = wgs[blockIdx.x];
+  if (W.mat < 0) return;                         // XCD-affine order: padding slot
   const SbMat M = mats[W.mat];
+  if (M.ts && threadIdx.x == 0) M.ts[2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
   const int n = M.n, grp = W.g;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   extern __shared__ float lds[];                 // NW x NSLOT x SLOTF floats (+ padding)
@@ -239,64 +248,76 @@ __global__ __launch_bounds__(64 * NW) void sb2st_kernel(const SbMat* __restrict_
       const int L = min(SB, n - r0);            // >= 2
       float* S0 = my + (j % NSLOT) * SLOTF;
       float* S1 = my + ((j + 1) % NSLOT) * SLOTF;
+      // ---- every LDS operand of the task first (none depends on the
+      // reflector): element l of this lane's vector, branch-free
+      //   g0 (left, j >= 1): column c+1+li, row l     -> S0 + 16 + li + 35 l
+      //   g1 (diagonal, row li): l <= li -> S0 + 35 li + 31 + l
+      //                          l >  li -> S0 + 35 l + li + 31
+      //   g2 (below, row 16+li): column r0+l           -> S1 + 35 li + 15 + l
+      // inactive lanes (g0 at j = 0 or li = 15, g3) read and write a dummy word
+      const bool g0 = g == 0, g1 = g == 1, g2 = g == 2;
+      const bool act = (g0 && j > 0 && li < SB - 1) || g1 || g2;
+      float* P = g2 ? S1 : S0;
+      const int boff = g0 ? 16 + li : (g1 ? 35 * li + 31 : 35 * li + 15);
+      const int bstr = g0 ? 35 : 1;
+      float* dummy = lds + NW * NSLOT * SLOTF + w;      // one spare word per wave
+      float* addr[SB];
+#pragma unroll
+      for (int l = 0; l < SB; ++l) {
+        const int off = (g1 && l > li) ? 35 * l + li + 31 : boff + bstr * l;
+        addr[l] = act ? P + off : dummy;
+      }
+      float val[SB];
+#pragma unroll
+      for (int l = 0; l < SB; ++l) val[l] = *addr[l];
       // ---- reflector from column c (lanes 0..15: row i = lane)
       const int xo = (j == 0) ? 30 : 15;        // column c's offset in row i: xo - i
-      const int xa = 35 * (lane & 15) + xo;
-      const float xl = S0[xa];
+      float* xp = S0 + 35 * (lane & 15) + xo;
+      const float xl = *xp;
       const float x = (lane < L) ? xl : 0.f;
       const float alpha = rdlane(x, 0);
       const float sig = wave_sum((lane >= 1 && lane < L) ? x * x : 0.f);
       float tau = 0.f, beta = alpha, scal = 0.f;
       if (sig != 0.f) {
-        beta = -copysignf(sqrtf(alpha * alpha + sig), alpha);
-        tau = (beta - alpha) / beta;
-        scal = 1.f / (alpha - beta);
+        beta = -copysignf(__builtin_sqrtf(alpha * alpha + sig), alpha);
+        tau = (beta - alpha) * __builtin_amdgcn_rcpf(beta);
+        scal = __builtin_amdgcn_rcpf(alpha - beta);
       }
       const float v = lane == 0 ? 1.f : ((lane < L) ? x * scal : 0.f);
       if (lane < L) {
-        S0[xa] = lane == 0 ? beta : 0.f;
+        *xp = lane == 0 ? beta : 0.f;
         v2[(long long)s * M.ldv2 + SB * j + lane] = lane == 0 ? tau : v;
       }
       if (tau != 0.f) {
         float vl[SB];
 #pragma unroll
         for (int l = 0; l < SB; ++l) vl[l] = rdlane(v, l);
-        // ---- element l of this lane's vector:
-        //   g0 (left, j >= 1): column c+1+li, row l     -> S0 + 16 + li + 35 l
-        //   g1 (diagonal, row li): l <= li -> S0 + 35 li + 31 + l
-        //                          l >  li -> S0 + 35 l + li + 31
-        //   g2 (below, row 16+li): column r0+l           -> S1 + 35 li + 15 + l
-        const bool act = (g == 0 && j > 0 && li < SB - 1) || g == 1 || g == 2;
-        float* base;
-        int stride;
-        if (g == 0) { base = S0 + 16 + li; stride = 35; }
-        else if (g == 1) { base = S0 + 35 * li + 31; stride = 1; }
-        else { base = S1 + 35 * li + 15; stride = 1; }
-        if (!act) { base = S0; stride = 0; }
-        float val[SB];
-        float dot = 0.f;
+        float d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f;
 #pragma unroll
-        for (int l = 0; l < SB; ++l) {
-          const float* pa = (g == 1 && l > li) ? (S0 + 35 * l + li + 31) : (base + stride * l);
-          val[l] = *pa;
-          dot += val[l] * vl[l];
+        for (int l = 0; l < SB; l += 4) {
+          d0 += val[l] * vl[l]; d1 += val[l + 1] * vl[l + 1];
+          d2 += val[l + 2] * vl[l + 2]; d3 += val[l + 3] * vl[l + 3];
         }
+        const float dot = (d0 + d1) + (d2 + d3);
         // g1: w = tau D v - K v, K = tau / 2 v^T (tau D v)
+        // (the shuffle outside the select: a ?: arm is divergent code, and a
+        // bpermute from inactive source lanes reads zero)
+        const float vsh = rdlane_row(v, li);
+        const float vli = g1 ? vsh : 0.f;
         const float p = tau * dot;
-        const float kk = 0.5f * tau * row_sum16(vl[li] * p);
-        const float wv = p - kk * vl[li];
+        const float kk = 0.5f * tau * row_sum16(vli * p);
+        const float wv = p - kk * vli;
         float wl[SB];
 #pragma unroll
         for (int l = 0; l < SB; ++l) wl[l] = rdlane(wv, 16 + l);
         // update: g0 / g2 -= (tau dot) v[l]; g1 -= w v[l] + v[li] w[l] (lower only)
-        const float a1 = (g == 1) ? wv : p;
-        const float a2 = (g == 1) ? vl[li] : 0.f;
+        const float a1 = g1 ? wv : p;
+        const float a2 = g1 ? vli : 0.f;
 #pragma unroll
         for (int l = 0; l < SB; ++l) {
-          const bool st = act && !(g == 1 && l > li);
           const float nv = val[l] - (a1 * vl[l] + a2 * wl[l]);
-          float* pa = base + stride * l;
-          if (st) *pa = nv;
+          float* pa = (g1 && l > li) ? dummy : addr[l];
+          *pa = nv;
         }
       }
       // ---- outputs finished by this task
@@ -320,6 +341,7 @@ __global__ __launch_bounds__(64 * NW) void sb2st_kernel(const SbMat* __restrict_
   // a group whose last sweep has no task still releases its successor
   if (w == NW - 1 && J == 0 && lane == 0)
     __hip_atomic_store(mine, DONE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (M.ts && threadIdx.x == 0) M.ts[2 * blockIdx.x + 1] = (long long)__builtin_amdgcn_s_memrealtime();
 }
 
 __global__ __launch_bounds__(256) void sb2st_zero_kernel(int* p, int n) {
@@ -331,13 +353,18 @@ struct SbPlan {
   SbWg* d_wgs = nullptr;
   int* d_prog = nullptr;       // all matrices' group counters, then the error count
   int nprog = 0, nwg = 0;
+  long long* d_ts = nullptr;
   hipGraphExec_t exec = nullptr;
 };
+
+long long* g_last_ts = nullptr;
+int g_last_nwg = 0;
+std::vector<SbWg> g_last_wgs;
 
 // 37 KB of ring per workgroup, padded so that exactly one workgroup sits on a
 // CU (the sc1 hand-off's measured form)
 constexpr size_t LDS_BYTES = 96 * 1024;
-static_assert((size_t)NW * NSLOT * SLOTF * sizeof(float) <= LDS_BYTES, "ring exceeds LDS");
+static_assert((size_t)(NW * NSLOT * SLOTF + NW) * sizeof(float) <= LDS_BYTES, "ring exceeds LDS");
 
 int enqueue(const SbPlan& P, hipStream_t s) {
   hipLaunchKernelGGL(sb2st_zero_kernel, dim3(4), dim3(256), 0, s, P.d_prog, P.nprog + 1);
@@ -349,6 +376,20 @@ std::mutex g_mu;
 std::map<std::string, SbPlan> g_plans;
 
 }  // namespace
+
+// dbg & 8: copy the last plan's stamps out: per workgroup (mat, group, start, end)
+KFAC_API int kfac_sb2st_debug_stamps(long long* out, int max_wg) {
+  if (!g_last_ts) return 0;
+  const int nw = std::min(max_wg, g_last_nwg);
+  std::vector<long long> t(2 * (size_t)g_last_nwg);
+  if (hipMemcpy(t.data(), g_last_ts, sizeof(long long) * t.size(), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  for (int b = 0; b < nw; ++b) {
+    out[4 * b] = g_last_wgs[b].mat; out[4 * b + 1] = g_last_wgs[b].g;
+    out[4 * b + 2] = t[2 * b]; out[4 * b + 3] = t[2 * b + 1];
+  }
+  return nw;
+}
 
 struct KfacSb2stRecord {
   const float* band_in; float* band; float* v2; float* d; float* e; long long ldv2; long long n;
@@ -408,10 +449,24 @@ KFAC_API int kfac_sb2st_batched(const KfacSb2stRecord* recs, int count, int use_
       std::vector<SbWg> wgs;
       int gmax = 0;
       for (int i = 0; i < count; ++i) gmax = std::max(gmax, ngrp[i]);
-      for (int g = 0; g < gmax; ++g)
-        for (int i = 0; i < count; ++i)
-          if (g < ngrp[i]) wgs.push_back(SbWg{i, g});
+      const int dbg = mats[0].dbg;
+      if ((dbg & 16) && count <= 8) {
+        // workgroup b runs on XCD b mod 8 (round-robin dispatch): matrix i's
+        // groups all on XCD i, padding slots exit at once
+        for (int g = 0; g < gmax; ++g)
+          for (int x = 0; x < 8; ++x)
+            wgs.push_back(x < count && g < ngrp[x] ? SbWg{x, g} : SbWg{-1, 0});
+      } else {
+        for (int g = 0; g < gmax; ++g)
+          for (int i = 0; i < count; ++i)
+            if (g < ngrp[i]) wgs.push_back(SbWg{i, g});
+      }
       P.nwg = (int)wgs.size();
+      if (dbg & 8) {
+        if ((err = (int)hipMalloc(&P.d_ts, sizeof(long long) * 2 * P.nwg)) != 0) return err;
+        for (auto& M : mats) M.ts = P.d_ts;
+        g_last_ts = P.d_ts; g_last_nwg = P.nwg; g_last_wgs = wgs;
+      }
       if ((err = (int)hipMalloc(&P.d_mats, sizeof(SbMat) * count)) != 0) return err;
       if ((err = (int)hipMemcpy(P.d_mats, mats.data(), sizeof(SbMat) * count,
                                 hipMemcpyHostToDevice)) != 0)

@@ -21,10 +21,10 @@
 //
 // Per panel, one launch each (all matrices of the batch in every launch):
 //   P  one 512-thread workgroup per matrix: the 16 x m panel in registers
-//      (10 columns per thread), Householder QR with two workgroup reductions
-//      per reflector (its norm; its dots with every other panel row, which are
-//      the trailing rows' update coefficients AND the new column of
-//      V^T V for T -- one pass), T (larft) built alongside; V rows -> Vr
+//      (10 columns per thread), Householder QR with ONE workgroup reduction
+//      per reflector (the dots of row c's tail with every panel row: its norm,
+//      the trailing rows' update coefficients and the new column of V^T V
+//      for T), T (larft) built alongside; V rows -> Vr
 //   Y  X = A22 V T, 16 rows per workgroup on v_mfma_f32_16x16x4_f32 (exact
 //      f32), 4 waves split K; per-workgroup partial M = V^T X
 //   N  N = T^T (sum of the partial M) -- one small workgroup per matrix
@@ -77,6 +77,8 @@ SyWs ws_layout(long long lda) {
 // matrix of this workgroup from a launch's ascending offsets (count + 1)
 // (the matrices are sorted by descending n, so the active ones of a panel are
 // a prefix: the active index is the matrix index)
+__device__ __forceinline__ bool r_ok(int r, int nr) { return r < nr; }
+
 __device__ __forceinline__ int find_mat(const int* __restrict__ offs, int count, int wg,
                                         int* local) {
   int lo = 0;
@@ -100,102 +102,116 @@ __global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   constexpr int NW = PT / 64;
   AS1 float* A = gptr(M.A);
   AS1 float* Vr = gptr(M.Vr);
-  __shared__ float red1[2][NW];
-  __shared__ float alph[2];
-  __shared__ float red16[NW][SB];
-  __shared__ float res16[SB];
+  __shared__ __attribute__((aligned(16))) float red16[2][NW][SB];
+  __shared__ __attribute__((aligned(16))) float colc[2][SB];
   __shared__ float sT[SB][SB + 1];
   for (int e = tid; e < SB * (SB + 1); e += PT) (&sT[0][0])[e] = 0.f;
 
-  float P[SB][PQ];
+  // buffer addressing (one voffset per thread, uniform row / column offsets):
+  // 64-bit per-element addresses, shared by the loads and the final stores,
+  // kept ~100 VGPRs live and spilled the panel
   const long long base = (long long)j0 * lda + j0 + SB;
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      M.A + base, 0, (int)(((long long)(nr - 1) * lda + m) * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsV = __builtin_amdgcn_make_buffer_rsrc(
+      M.Vr, 0, (int)((long long)SB * lda * 4), 0x00020000);
+  const int vo = tid * 4, ldi = (int)lda;
+  float P[SB][PQ];
 #pragma unroll
   for (int c = 0; c < SB; ++c)
 #pragma unroll
     for (int q = 0; q < PQ; ++q) {
       const int k = tid + PT * q;
       const bool ok = c < nr && k < m;
-      P[c][q] = gld_if(A, base + (long long)c * lda + k, ok, 0.f);
+      const float x = __uint_as_float(
+          __builtin_amdgcn_raw_buffer_load_b32(rsA, vo, (int)((c * lda + PT * q) * 4), 0));
+      P[c][q] = ok ? x : 0.f;
     }
+  __syncthreads();     // sT zeroed
 
   // fully unrolled over the panel rows: every P[c][q] index is static, so the
-  // panel stays in registers (a runtime row index puts it in scratch)
+  // panel stays in registers (a runtime row index puts it in scratch).
+  // ONE workgroup reduction (and one barrier) per reflector: the dots
+  // e_r = sum_{k > c} P[c][k] P[r][k] of row c's tail with every panel row,
+  // plus column c (thread c) through LDS, give
+  //   sig = e_c,  alpha = P[c][c],  and for r != c
+  //   d_r = sum_{k >= c} v[k] P[r][k] = P[r][c] + scal e_r
+  // -- the update coefficients (r > c) and V^T v for T (r < c), as before.
 #pragma clang loop unroll(full)
   for (int c = 0; c < SB; ++c) {
     if (c < kb) {                             // kb is uniform
-    // -- norm of row c beyond column c (one reduction) + alpha = P[c][c]
-    float part = 0.f;
+    const int b = c & 1;
+    float e[SB];
 #pragma unroll
-    for (int q = 0; q < PQ; ++q) {
-      const int k = tid + PT * q;
-      const float x = P[c][q];
-      part += (k > c) ? x * x : 0.f;
+    for (int r = 0; r < SB; ++r) {
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < PQ; ++q) {
+        const float x = (q == 0 && tid <= c) ? 0.f : P[c][q];   // k > c
+        s = __builtin_fmaf(x, P[r][q], s);
+      }
+      e[r] = r < nr ? s : 0.f;
     }
-    part = wave_sum(part);
-    if (lane == 0) red1[c & 1][wid] = part;
-    if (tid == c) alph[c & 1] = P[c][0];      // c < 16 <= PT: column c is thread c, q = 0
-    kfac_lds_barrier();      // LDS only: the Vr stores stay in flight
-    float sig = 0.f;
+    const float esum = kfac_butterfly16(e);   // lanes with (lane & 15) == x: wave sum of e[x]
+    if (lane < SB) red16[b][wid][lane] = esum;
+    if (tid == c) {                           // column c: thread c, q = 0
 #pragma unroll
-    for (int w = 0; w < NW; ++w) sig += red1[c & 1][w];
-    const float alpha = alph[c & 1];
+      for (int r = 0; r < SB; ++r) colc[b][r] = P[r][0];
+    }
+    kfac_lds_barrier();      // LDS only: the Vr stores stay in flight
+    // lane l (every wave) sums the 8 wave partials of e_{l & 15}; the row
+    // coefficients then go to scalar registers by readlane
+    float el = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) el += red16[b][w][lane & 15];
+    const float pl = colc[b][lane & 15];
+    const float sig = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(el), c));
+    const float alpha = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pl), c));
     float tau = 0.f, beta = alpha, scal = 0.f;
     if (sig != 0.f) {
       beta = -copysignf(sqrtf(alpha * alpha + sig), alpha);
       tau = (beta - alpha) / beta;
       scal = 1.f / (alpha - beta);
     }
+    // d_l = P[l][c] + scal e_l: update coefficient of row l > c, (V^T v)_l for l < c
+    const float dl = pl + scal * el;
     float v[PQ];
 #pragma unroll
     for (int q = 0; q < PQ; ++q) {
       const int k = tid + PT * q;
       v[q] = k < c ? 0.f : (k == c ? 1.f : P[c][q] * scal);
     }
-    // -- dots of v with every other panel row: r > c -> the update
-    // coefficient w_r, r < c -> (V^T v)_r for T (v is zero before column c,
-    // where rows r < c hold their R part)
-    float d[SB];
-#pragma unroll
-    for (int r = 0; r < SB; ++r) {
-      float s = 0.f;
-#pragma unroll
-      for (int q = 0; q < PQ; ++q) s += v[q] * P[r][q];
-      d[r] = (r != c && r < nr) ? s : 0.f;
-    }
-    const float dsum = kfac_butterfly16(d);    // lanes with (lane & 15) == x: wave sum of d[x]
-    if (lane < SB) red16[wid][lane] = dsum;
-    kfac_lds_barrier();
-    if (tid < SB) {
-      float s = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) s += red16[w][tid];
-      res16[tid] = s;
-    }
-    kfac_lds_barrier();
-    float wr[SB];
-#pragma unroll
-    for (int r = 0; r < SB; ++r) wr[r] = res16[r];
-    // -- update the rows below, finish row c (R before, beta, v after)
+    // -- update the rows below
 #pragma unroll
     for (int r = 0; r < SB; ++r) {
       if (r > c) {
-        const float f = tau * wr[r];
+        const float f = tau * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dl), r));
 #pragma unroll
-        for (int q = 0; q < PQ; ++q) P[r][q] -= f * v[q];
+        for (int q = 0; q < PQ; ++q) P[r][q] = __builtin_fmaf(-f, v[q], P[r][q]);
       }
     }
+    // -- finish row c (R before, beta, v after)
 #pragma unroll
     for (int q = 0; q < PQ; ++q) {
       const int k = tid + PT * q;
       P[c][q] = k == c ? beta : (k > c ? v[q] : P[c][q]);
-      if (k < lda) Vr[(long long)c * lda + k] = v[q];
+      if (k < ldi)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[q]), rsV, vo,
+                                              (int)((c * lda + PT * q) * 4), 0);
     }
-    // -- T column c (larft, forward columnwise): T[0:c, c] = -tau T[0:c, 0:c] (V^T v)
-    if (tid < c) {
+    // -- T column c (larft, forward columnwise): T[0:c, c] = -tau T[0:c, 0:c] (V^T v),
+    // (V^T v)_a = d_a for a < c; wave 0, lane a computes d_a (lane tid owns row
+    // tid of sT: written and read by the same lane)
+    if (wid == 0 && c > 0) {
       float s = 0.f;
 #pragma unroll
-      for (int a = 0; a < SB; ++a) s += (a >= tid && a < c) ? sT[tid][a] * wr[a] : 0.f;
-      sT[tid][c] = -tau * s;
+      for (int a = 0; a < SB; ++a) {
+        if (a < c) {
+          const float x = (r_ok(a, nr)) ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dl), a)) : 0.f;
+          s += (a >= lane) ? sT[lane & 15][a] * x : 0.f;
+        }
+      }
+      if (lane < c) sT[lane][c] = -tau * s;
     }
     if (tid == c) sT[c][c] = tau;
     if (tid == 0) M.tau[j0 + c] = tau;
@@ -207,7 +223,8 @@ __global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 #pragma unroll
     for (int q = 0; q < PQ; ++q) {
       const int k = tid + PT * q;
-      if (k < lda) Vr[(long long)c * lda + k] = 0.f;
+      if (k < ldi)
+        __builtin_amdgcn_raw_buffer_store_b32(0u, rsV, vo, (int)((c * lda + PT * q) * 4), 0);
     }
   }
 #pragma unroll
@@ -215,7 +232,9 @@ __global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 #pragma unroll
     for (int q = 0; q < PQ; ++q) {
       const int k = tid + PT * q;
-      if (c < nr && k < m) A[base + (long long)c * lda + k] = P[c][q];
+      if (c < nr && k < m)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(P[c][q]), rsA, vo,
+                                              (int)((c * lda + PT * q) * 4), 0);
     }
   __syncthreads();
   if (tid < SB * SB) M.T[tid] = sT[tid / SB][tid % SB];
@@ -250,7 +269,24 @@ __global__ __launch_bounds__(256) void sy2sb_yx_kernel(const SyMat* __restrict__
   const int chunk = ((mk / 16 + 3) / 4) * 16;
   const int kbeg = wid * chunk, kend = min(mk, kbeg + chunk);
   f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-  for (int k0 = kbeg; k0 < kend; k0 += 16) {
+  int k0 = kbeg;
+  // 4 k-steps per iteration: 8 float4 loads in flight before the MFMAs
+  for (; k0 + 64 <= kend; k0 += 64) {
+    fx4 a4[4], b4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a4[u] = *(const AS1 fx4*)(Arow + k0 + 16 * u + 4 * q);
+      b4[u] = *(const AS1 fx4*)(Vrow + k0 + 16 * u + 4 * q);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[u].x, b4[u].x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[u].y, b4[u].y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[u].z, b4[u].z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[u].w, b4[u].w, acc, 0, 0, 0);
+    }
+  }
+  for (; k0 < kend; k0 += 16) {
     const fx4 a4 = *(const AS1 fx4*)(Arow + k0 + 4 * q);
     const fx4 b4 = *(const AS1 fx4*)(Vrow + k0 + 4 * q);
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, b4.x, acc, 0, 0, 0);
@@ -330,6 +366,17 @@ __global__ __launch_bounds__(256) void sy2sb_upd_kernel(const SyMat* __restrict_
   const int nt = (m + UT - 1) / UT;
   const int I0 = (t / nt) * UT, J0 = (t % nt) * UT;
   const int tid = threadIdx.x;
+  const int ty = tid >> 4, tx = tid & 15;
+  // the tile's old values first: their latency hides under the V / Zm staging
+  AS1 float* A = gptr(M.A) + (long long)(j0 + SB) * lda + j0 + SB;
+  const int c0 = J0 + 4 * tx;
+  fx4 old[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int row = I0 + 4 * ty + a;
+    const fx4 z4 = {0.f, 0.f, 0.f, 0.f};
+    old[a] = (row < m && c0 + 3 < m) ? *(const AS1 fx4*)(A + (long long)row * lda + c0) : z4;
+  }
   __shared__ float sN[SB][SB + 1];
   __shared__ float sV[2][UT][SB + 1];
   __shared__ float sZ[2][UT][SB + 1];
@@ -357,7 +404,6 @@ __global__ __launch_bounds__(256) void sy2sb_upd_kernel(const SyMat* __restrict_
     sZ[h][rr][c] = z - 0.5f * s;
   }
   __syncthreads();
-  const int ty = tid >> 4, tx = tid & 15;
   float acc[4][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
@@ -378,18 +424,15 @@ __global__ __launch_bounds__(256) void sy2sb_upd_kernel(const SyMat* __restrict_
   }
   // tiles run past m up to a multiple of 64 (and past lda): only rows and
   // columns < m are read or written
-  AS1 float* A = gptr(M.A) + (long long)(j0 + SB) * lda + j0 + SB;
-  const int c0 = J0 + 4 * tx;
 #pragma unroll
   for (int a = 0; a < 4; ++a) {
     const int row = I0 + 4 * ty + a;
     if (row >= m) continue;
     AS1 float* pr = A + (long long)row * lda + c0;
     if (c0 + 3 < m) {
-      AS1 fx4* pa = (AS1 fx4*)pr;
-      fx4 x = *pa;
+      fx4 x = old[a];
       x.x -= acc[a][0]; x.y -= acc[a][1]; x.z -= acc[a][2]; x.w -= acc[a][3];
-      *pa = x;
+      *(AS1 fx4*)pr = x;
     } else {
 #pragma unroll
       for (int b = 0; b < 4; ++b)

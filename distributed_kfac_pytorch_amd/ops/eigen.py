@@ -8,7 +8,8 @@ the compact-WY back-transformation (csrc/eig_backtransform.hip) -- split
 over two streams by size (_fused_groups).  1x1 factors, and the opt-in
 solver='jacobi' for n <= SMALL_N, use the batched LDS Jacobi kernel
 (csrc/eig_jacobi.hip).  Factors above FUSED_MAX_N (a 16384^2 fp32 factor is
-1 GiB) are refused on the GPU.
+1 GiB; e.g. the 33k-vocabulary decoder of the wikitext-2 language model) fall
+back to torch.linalg.eigh on the device, with a one-time warning.
 CPU path: torch.linalg.eigh (the reference semantics, kfac/layers/utils.py:45-74).
 
 Results: ascending eigenvalues clipped at `clip` (reference default 0.0),
@@ -458,12 +459,12 @@ def symeig_many(mats, clip=0.0, solver='auto'):
                 d = torch.clamp(d, min=clip)
             outs.append((Q, d))
         return outs
-    nmax = max(A.shape[0] for A in mats)
-    if nmax > FUSED_MAX_N:
-        raise ValueError('factor of size {} exceeds the GPU eigensolver limit {} '
-                         '(csrc/eig_reduce.hip NMAX)'.format(nmax, FUSED_MAX_N))
     if solver not in ('auto', 'jacobi'):
         raise ValueError("solver must be 'auto' or 'jacobi', got {!r}".format(solver))
+    huge = [i for i, A in enumerate(mats) if A.shape[0] > FUSED_MAX_N]
+    if huge:
+        return _with_huge(mats, huge, clip, solver)
+    nmax = max(A.shape[0] for A in mats)
     _lib.check_pgemm_extent(nmax)
     # EVERY factor rides the fused ragged launch sequence (a small factor's
     # reduction columns run alongside the big ones', its divide and conquer is
@@ -505,6 +506,32 @@ def symeig_many(mats, clip=0.0, solver='auto'):
         for i in ts:
             outs[i][0].record_stream(cur)
             outs[i][1].record_stream(cur)
+    return outs
+
+
+_HUGE_WARNED = []
+
+
+def _with_huge(mats, huge, clip, solver):
+    """Factors above FUSED_MAX_N: torch.linalg.eigh on the device (the
+    reference's solver, kfac/layers/utils.py:45-74); the rest as usual."""
+    if not _HUGE_WARNED:
+        _HUGE_WARNED.append(1)
+        import warnings
+        warnings.warn('K-FAC: factor(s) of size {} exceed the native eigensolver limit {} '
+                      '(csrc/eig_reduce.hip NMAX); using torch.linalg.eigh for them (slow: '
+                      'consider skip_layers for that layer)'.format(
+                          sorted({mats[i].shape[0] for i in huge}), FUSED_MAX_N))
+    hs = set(huge)
+    rest = [i for i in range(len(mats)) if i not in hs]
+    outs = [None] * len(mats)
+    for i, r in zip(rest, symeig_many([mats[i] for i in rest], clip, solver)):
+        outs[i] = r
+    for i in huge:
+        d, Q = torch.linalg.eigh(mats[i].float())
+        if clip is not None:
+            d = torch.clamp(d, min=clip)
+        outs[i] = (Q.contiguous(), d)
     return outs
 
 

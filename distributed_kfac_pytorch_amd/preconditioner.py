@@ -288,6 +288,7 @@ class KFAC(optim.Optimizer):
         # compute_factor_in_hook on the GPU: gradient hooks of this step seen /
         # registered (the last one runs the grouped factor launches)
         self._hook_step = None
+        self._hook_flush_warned = False
         self._g_seen = 0
         self._g_expected = 0
         self.fused = None
@@ -542,6 +543,26 @@ class KFAC(optim.Optimizer):
             self._hook_step = st
             self._g_seen = self._g_expected = 0
 
+    def _flush_hook_factors(self):
+        """Grouped in-hook factors whose last gradient hook never came (a
+        hooked output the loss does not use, an output recomputed under
+        activation checkpointing): compute the saved factors now, in step(),
+        so no layer loses this step's update (the per-hook path and the
+        reference, kfac/base_preconditioner.py, only lose the factor of the
+        layer whose hook did not run)."""
+        if not (self._g_expected and self._hook_step == self.param_groups[0]['step']
+                and self._hook_factors_grouped()):
+            return
+        if not self._hook_flush_warned:
+            self._hook_flush_warned = True
+            warnings.warn('K-FAC: %d of %d hooked module outputs received no gradient in this '
+                          'backward; the grouped in-hook factor update runs in step() instead '
+                          '(every later such step too)' % (self._g_expected - self._g_seen,
+                                                           self._g_expected))
+        self._g_seen = self._g_expected = 0
+        with torch.autocast(device_type='cuda', enabled=False):
+            self.compute_factors(alpha=self.param_groups[0]['factor_decay'])
+
     # ----------------------------------------------- early A factors
     def _early_a_due(self):
         p = self.param_groups[0]
@@ -664,6 +685,8 @@ class KFAC(optim.Optimizer):
             if not self.compute_factor_in_hook:
                 with t('factors'):
                     self.compute_factors(alpha=p['factor_decay'])
+            else:
+                self._flush_hook_factors()
             with t('factor_comm'):
                 self.allreduce_factors()
         if self.comm_check and p['step'] % p['factor_update_freq'] == 0:
@@ -734,6 +757,8 @@ class KFAC(optim.Optimizer):
             return
         if not self.compute_factor_in_hook:
             self.compute_factors(alpha=p['factor_decay'])
+        else:
+            self._flush_hook_factors()
         self.allreduce_factors()
         self._factor_comm_step = p['step']
 

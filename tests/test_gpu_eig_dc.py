@@ -153,3 +153,42 @@ def test_fused_path_small_and_odd_sizes():
         orth = (Q64.t() @ Q64 - torch.eye(n, device=DEV, dtype=torch.float64)).abs().max().item()
         lam = ((d64 - ref.clamp(min=0)).abs().max() / an).item()
         assert res <= 2e-5 and orth <= 1e-4 and lam <= 1e-5, (n, res, orth, lam)
+
+
+def test_fused_path_at_limit_16384():
+    """FUSED_MAX_N itself (csrc/eig_reduce.hip NMAX): residual and
+    orthogonality in fp64, the eigenvalues through the trace and Frobenius
+    invariants (an fp64 eigvalsh at this size is a minute on its own)."""
+    n = eigen.FUSED_MAX_N
+    A64 = _kfac_factor(n, 91)
+    (Q, d), = eigen.symeig_many([A64.float()])
+    torch.cuda.synchronize()
+    eigen.check_solver_status()
+    Q64, d64 = Q.double(), d.double()
+    an = d64.abs().max().item()
+    res = ((A64 @ Q64 - Q64 * d64).norm() / (an * n ** 0.5)).item()
+    orth = (Q64.t() @ Q64 - torch.eye(n, device=DEV, dtype=torch.float64)).abs().max().item()
+    tr = abs(d64.sum().item() - A64.diagonal().sum().item()) / A64.diagonal().sum().item()
+    fro = abs((d64 * d64).sum().item() - (A64 * A64).sum().item()) / (A64 * A64).sum().item()
+    assert bool((d[1:] >= d[:-1]).all())
+    assert res <= 2e-5 and orth <= 1e-4 and tr <= 1e-5 and fro <= 1e-5, (res, orth, tr, fro)
+
+
+def test_beyond_limit_falls_back(monkeypatch):
+    """A factor above FUSED_MAX_N (the 33k-vocabulary decoder of the wikitext-2
+    LM) goes to torch.linalg.eigh with a warning instead of raising; the
+    others stay on the native path (limit lowered to keep the test small)."""
+    monkeypatch.setattr(eigen, 'FUSED_MAX_N', 256)
+    monkeypatch.setattr(eigen, '_HUGE_WARNED', [])
+    sizes = [64, 300, 200]
+    mats64 = [_kfac_factor(n, 60 + i) for i, n in enumerate(sizes)]
+    with pytest.warns(UserWarning, match='exceed the native eigensolver limit'):
+        outs = eigen.symeig_many([m.float() for m in mats64])
+    torch.cuda.synchronize()
+    for n, A64, (Q, d) in zip(sizes, mats64, outs):
+        assert Q.shape == (n, n) and d.shape == (n,)
+        Q64, d64 = Q.double(), d.double()
+        ref = torch.linalg.eigvalsh(A64)
+        an = ref.abs().max().item()
+        res = ((A64 @ Q64 - Q64 * d64).norm() / (an * n ** 0.5)).item()
+        assert res <= 2e-5 and ((d64 - ref.clamp(min=0)).abs().max() / an).item() <= 1e-5

@@ -214,3 +214,57 @@ def test_hook_factors_grouped_bitwise(graphed):
         assert torch.equal(a, b), (a - b).abs().max()
     for a, b in zip(p0, p1):
         assert torch.equal(a, b), (a - b).abs().max()
+
+
+def test_hook_factors_grouped_unused_output():
+    """Grouped in-hook factors with a hooked module whose output the loss does
+    not use (an aux head in the loss on the first step only): from then on its
+    gradient hook never runs, so the backward's 'last hook' never comes;
+    step() computes the saved factors instead (with one warning) and the
+    factors equal those of computing them in step()."""
+    import warnings
+    import distributed_kfac_pytorch_amd as kfac
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = torch.nn.Linear(32, 64)
+            self.b = torch.nn.Linear(64, 10)
+            self.aux = torch.nn.Linear(64, 5)
+
+        def forward(self, x):
+            h = torch.relu(self.a(x))
+            self.aux_out = self.aux(h)        # hooked, never reaches the loss
+            return self.b(h)
+
+    def run(hook):
+        torch.manual_seed(0)
+        m = Net().cuda()
+        pre = kfac.KFAC(m, factor_update_freq=1, inv_update_freq=2, damping=0.003,
+                        compute_factor_in_hook=hook)
+        g = torch.Generator(device='cuda').manual_seed(4)
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter('always')
+            for i in range(4):
+                x = torch.randn(16, 32, device='cuda', generator=g)
+                loss = F.cross_entropy(m(x), torch.zeros(16, dtype=torch.long, device='cuda'))
+                if i == 0:
+                    loss = loss + 0.1 * m.aux_out.square().mean()
+                loss.backward()
+                pre.step()
+        torch.cuda.synchronize()
+        msgs = [str(x.message) for x in w if 'received no gradient' in str(x.message)]
+        return {id(l.module): (l.state['A'], l.state['G']) for l in pre.layers}, pre, m, msgs
+
+    f0, _, m0, _ = run(False)
+    f1, pre, m1, msgs = run(True)
+    assert pre._hook_factors_grouped() and len(msgs) == 1, msgs
+    for l in pre.layers:
+        assert not l.a_inputs and not l.g_outputs
+    for (mod0, mod1) in zip((m0.a, m0.b, m0.aux), (m1.a, m1.b, m1.aux)):
+        A0, G0 = f0[id(mod0)]
+        A1, G1 = f1[id(mod1)]
+        assert torch.equal(A0, A1)
+        assert (G0 is None) == (G1 is None)
+        if G0 is not None:
+            assert torch.equal(G0, G1)
