@@ -37,11 +37,13 @@ Two modes:
                   (KFAC.prepare_factor_step), so the captured update holds no
                   collective.  With
                   `phased_update=True` (update == preconditioner.step() +
-                  optimizer.step()), a plain step that does communicate
-                  (MEM_OPT / HYBRID_OPT gradient all-gather) runs as two
-                  graphs -- KFAC.step_precondition, then KFAC.step_finish +
-                  optimizer.step() -- with KFAC.step_communicate eager between
-                  them; factor / inverse steps with collectives stay eager.
+                  optimizer.step()), a plain or factor step that does
+                  communicate (MEM_OPT / HYBRID_OPT gradient all-gather; a
+                  factor step's factor all-reduce is issued eagerly first, as
+                  above) runs as two graphs -- KFAC.step_precondition, then
+                  KFAC.step_finish + optimizer.step() -- with
+                  KFAC.step_communicate eager between them; only inverse
+                  steps with collectives (eigendata all-gather) stay eager.
 
 Step kinds follow the K-FAC schedule (`factor_update_freq`, `inv_update_freq`,
 reference kfac/preconditioner.py:494-514); the K-FAC step counter that a graph
