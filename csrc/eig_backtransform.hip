@@ -22,8 +22,10 @@
 // Q = H_0 H_1 ... H_{n-2} is applied as compact-WY blocks of BT reflectors,
 // last block first:  Z[j0:, :] -= V_k (T_k (V_k^T Z[j0:, :])).  Every GEMM is
 // the grouped MFMA kernel of csrc/precond_gemm.hip (exact f32 MFMA) over all
-// matrices of the size class; the long-K product V_k^T Z is split over K with
-// f32-atomic accumulation.  The whole sequence (~5 launches per block) is
+// matrices of the size class; the long-K product V_k^T Z is split over K
+// into per-chunk slabs summed in a fixed order by a small reduction kernel
+// (bitwise reproducible; round 3 accumulated the chunks with f32 atomics).
+// The whole sequence (~6 launches per block) is
 // captured once per buffer set into a hipGraph (no library GEMM, nothing on
 // the legacy stream).
 //
@@ -31,7 +33,8 @@
 // at j+1); Z column-major (row `col` of the row-major view = eigenvector
 // `col`); lda = ldz a multiple of 64 with zero padding past n, so every GEMM
 // operand is k-contiguous and zero-padded to the kernel's 64-wide k-steps.
-//   S1  W1t[col][c] = sum_{i>=j0} Z[col][i] V_k[c][i]     (split-K, atomic)
+//   S1  W1t_s[col][c] = sum_{i in chunk s} Z[col][i] V_k[c][i]   (split-K slabs)
+//   R   W1t = ((W1t_0 + W1t_1) + W1t_2) + ...                  (fixed order, in slab 0)
 //   S2  W2t[col][c] = sum_c' W1t[col][c'] T_k[c][c']
 //   S3  Z[col][j0+i] -= sum_c W2t[col][c] Vt_k[i][c]       (Vt_k = V_k^T copy)
 namespace {
@@ -48,6 +51,23 @@ const int g_bt_prec = [] {
 }();
 
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// split-K slabs per matrix (the most any block needs: K = lda - j0 <= lda)
+inline int nslab(int lda) { return cdiv(lda, KCH); }
+
+// R: slab 0 of every matrix <- the sum of its first `ns` slabs, in slab order
+__global__ __launch_bounds__(256) void slab_sum_kernel(float4* W1, long long slab4, int nsl,
+                                                       int ns) {
+  float4* base = W1 + (long long)blockIdx.y * nsl * slab4;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < slab4; i += (long long)gridDim.x * 256) {
+    float4 acc = base[i];
+    for (int s = 1; s < ns; ++s) {
+      const float4 x = base[(long long)s * slab4 + i];
+      acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+    }
+    base[i] = acc;
+  }
+}
 
 // Zero fill as a kernel (captured memset nodes misbehaved for multi-matrix
 // batches on ROCm 7.2).
@@ -133,7 +153,7 @@ struct BtArgs {
 
 // One recorded operation of the back-transformation.
 struct BtOp {
-  int kind;              // 0 pgemm, 1 split copy, 2 memset, 3 make_v, 4 larft
+  int kind;              // 0 pgemm, 1 split copy, 2 memset, 3 make_v, 4 larft, 5 slab sum (count = slabs)
   size_t off; int count; int tiles;    // table offset (bytes) / records / tiles
   void* ptr; size_t bytes;             // memset
 };
@@ -194,20 +214,22 @@ void build_plan(const BtArgs& a, BtPlan& plan, std::vector<unsigned char>& host)
     if (kb < BT) {   // partial block: stale columns >= kb must read as zero
       plan.ops.push_back(BtOp{2, 0, 0, 0, a.W2, (size_t)b * w1s * 4});
       plan.ops.push_back(BtOp{2, 0, 0, 0, a.Vt, (size_t)b * vts * 4});
+      plan.ops.push_back(BtOp{2, 0, 0, 0, a.W1, (size_t)b * nslab(a.lda) * w1s * 4});
     }
-    plan.ops.push_back(BtOp{2, 0, 0, 0, a.W1, (size_t)b * w1s * 4});
+    const int ns = cdiv(Kn, KCH), nsl = nslab(a.lda);
     for (int m = 0; m < b; ++m) {
       const float* Zm = a.Z + m * a.sZ;
       const float* Vk = a.A + m * a.sA + (long long)j0 * a.lda;
-      for (int k0 = 0; k0 < Kn; k0 += KCH) {
-        const int kc = Kn - k0 < KCH ? Kn - k0 : KCH;
-        recs.push_back(rec(Zm + j0 + k0, a.ldz, Vk + j0 + k0, a.lda, a.W1 + m * w1s, BT, n, kb, kc,
-                           EPI_ATOMIC));
+      for (int s = 0; s < ns; ++s) {
+        const int k0 = s * KCH, kc = Kn - k0 < KCH ? Kn - k0 : KCH;
+        recs.push_back(rec(Zm + j0 + k0, a.ldz, Vk + j0 + k0, a.lda,
+                           a.W1 + ((long long)m * nsl + s) * w1s, BT, n, kb, kc, EPI_STORE));
       }
     }
     add_pgemm(host, plan.ops, recs);
+    if (ns > 1) plan.ops.push_back(BtOp{5, 0, ns, 0, nullptr, 0});
     for (int m = 0; m < b; ++m)
-      recs.push_back(rec(a.W1 + m * w1s, BT, T + m * tstride + (long long)k * BT * BT, BT,
+      recs.push_back(rec(a.W1 + (long long)m * nsl * w1s, BT, T + m * tstride + (long long)k * BT * BT, BT,
                          a.W2 + m * w1s, BT, n, kb, BT, EPI_STORE));
     add_pgemm(host, plan.ops, recs);
     {  // Vt_k = V_k^T (rows j0.., kb columns)
@@ -247,6 +269,14 @@ int run_plan(const BtArgs& a, const BtPlan& plan, hipStream_t stream) {
         const long long n4 = (long long)(op.bytes / 16);
         const int grid = (int)((n4 + 255) / 256 < 2048 ? (n4 + 255) / 256 : 2048);
         hipLaunchKernelGGL(zero_kernel, dim3(grid), dim3(256), 0, stream, (float4*)op.ptr, n4);
+        err = (int)hipGetLastError();
+        break;
+      }
+      case 5: {
+        const long long slab4 = (long long)a.n * BT / 4;
+        const int grid = (int)((slab4 + 255) / 256 < 1024 ? (slab4 + 255) / 256 : 1024);
+        hipLaunchKernelGGL(slab_sum_kernel, dim3(grid, a.batch), dim3(256), 0, stream,
+                           (float4*)a.W1, slab4, nslab(a.lda), op.count);
         err = (int)hipGetLastError();
         break;
       }
@@ -303,7 +333,8 @@ BtPlan* plan_for(const BtArgs& a, int* err) {
 // A: the reduced matrices (reflectors in rows, made explicit in place),
 // Z: tridiagonal eigenvectors (column-major, ldz) -> eigenvectors of A.
 // lda == ldz, a multiple of 64 (zero padding past n).  Tbuf: 2 x batch x
-// nblk x BT x BT, W1, W2: batch x n x BT, Vt: batch x lda x BT.
+// nblk x BT x BT, W1: batch x kfac_backtransform_slabs(lda) x n x BT, W2: batch
+// x n x BT, Vt: batch x lda x BT.
 KFAC_API int kfac_tridiag_backtransform(float* A, int lda, long long strideA, const float* tau,
                                         float* Z, int ldz, long long strideZ, int n, int batch,
                                         float* Tbuf, float* W1, float* W2, float* Vt,
@@ -331,6 +362,8 @@ KFAC_API int kfac_band_backtransform(float* A, int lda, long long strideA, const
   if (use_graph && plan->exec) return (int)hipGraphLaunch(plan->exec, stream);
   return run_plan(a, *plan, stream);
 }
+
+KFAC_API int kfac_backtransform_slabs(int lda) { return nslab(lda); }
 
 KFAC_API int kfac_backtransform_prepare(float* A, int lda, long long strideA, const float* tau,
                                         float* Z, int ldz, long long strideZ, int n, int batch,

@@ -79,6 +79,7 @@ _SIGS = {
     'kfac_sy2sb_ws_floats': [c_ll],
     'kfac_sy2sb_nmax': [],
     'kfac_sb2st_batched': [ctypes.POINTER(Sb2stRecord), c_int, c_int, c_vp],
+    'kfac_backtransform_slabs': [c_int],
     'kfac_sb2st_debug_stamps': [ctypes.POINTER(ctypes.c_longlong), c_int],
     'kfac_q2_batched': [ctypes.POINTER(Q2Record), c_int, c_int, c_vp],
     'kfac_q2_nmax': [],

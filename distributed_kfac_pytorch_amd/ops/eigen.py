@@ -94,7 +94,8 @@ def _tri_buffers(dev, n, b, slot=0):
                     tau=torch.zeros(b, n, **f32),
                     info=torch.zeros(b, dtype=torch.int32, device=dev),
                     T=torch.zeros(2 * b * nblk * BT * BT, **f32),
-                    W1=torch.zeros(b * BT * n, **f32), W2=torch.zeros(b * BT * n, **f32),
+                    W1=torch.zeros(b * int(L.kfac_backtransform_slabs(lda)) * BT * n, **f32),
+                    W2=torch.zeros(b * BT * n, **f32),
                     Vt=torch.zeros(b * BT * lda, **f32))
         _TRI_BUFS[key] = bufs
     return bufs
@@ -364,7 +365,8 @@ def _ts_buffers(dev, n, b, slot=0):
                     w=torch.zeros(b, n, **f32), Z=torch.zeros(b, n, lda, **f32),
                     wsb=wsb, dcws=torch.zeros(b * wsb, dtype=torch.uint8, device=dev),
                     T=torch.zeros(2 * b * nblk * BT * BT, **f32),
-                    W1=torch.zeros(b * BT * n, **f32), W2=torch.zeros(b * BT * n, **f32),
+                    W1=torch.zeros(b * int(L.kfac_backtransform_slabs(lda)) * BT * n, **f32),
+                    W2=torch.zeros(b * BT * n, **f32),
                     Vt=torch.zeros(b * BT * lda, **f32))
         _TS_BUFS[key] = bufs
     return bufs

@@ -52,9 +52,9 @@ def run(args, dataset):
     if args.verbose:
         print(model)
     # --graphs: the bench's fast path (no eager DDP: a flat-arena all-reduce
-    # between graph replays); otherwise the reference's eager DDP loop
-    args.graphed = bool(getattr(args, 'graphs', 0)) and args.batches_per_allreduce == 1 and \
-        not args.fp16
+    # between graph replays), micro-batching and fp16 + GradScaler included;
+    # otherwise the reference's eager DDP loop
+    args.graphed = bool(getattr(args, 'graphs', 0))
     grad_sync = None
     if args.graphed and args.world_size > 1:
         from distributed_kfac_pytorch_amd.parallel import grad_sync as grad_sync_mod

@@ -14,6 +14,16 @@ at world size > 1 the gradient all-reduce is one flat-arena RCCL call between
 the forward/backward graph and the update graph (parallel/grad_sync.py), the
 K-FAC factor all-reduce is issued eagerly and joined at the next factor step.
 A batch of another shape (the last, ragged one) runs the same step eagerly.
+The fast path covers the reference's other two training modes too
+(examples/cnn_utils/engine.py:33-82 of the reference):
+  * `--batches-per-allreduce k`: the k micro-batches' forward/backward passes
+    are captured in the ONE forward/backward graph (gradients accumulate; the
+    graphed loop has no DDP, so the single all-reduce after it is the
+    reference's no_sync behaviour);
+  * `--fp16`: fp16 autocast + torch.amp.GradScaler, capturable because the
+    optimizer is the fused SGD (`_step_supports_amp_scaling`): scale, unscale
+    (device inf check), K-FAC step (device loss scale), the inf-skipping SGD
+    step and the scale update are all device work, no host read.
 """
 import contextlib
 import time
@@ -47,13 +57,17 @@ class GraphedTrainer(object):
         from distributed_kfac_pytorch_amd import graphs
         self.model, self.optimizer, self.pre = model, optimizer, preconditioner
         self.loss_func, self.args, self.grad_sync = loss_func, args, grad_sync
+        self.scaler = getattr(args, 'grad_scaler', None)
+        self.micro = max(1, int(getattr(args, 'batches_per_allreduce', 1)))
         self.x = self.y = None
         if grad_sync is not None:
+            # phased plain steps split the update at K-FAC's gradient
+            # all-gather and run opt.step() themselves: not with a scaler
             self.step = graphs.GraphedTrainStep(None, preconditioner, [optimizer],
                                                 enabled=args.cuda,
                                                 forward_backward=self._forward_backward,
                                                 communicate=grad_sync, update=self._update,
-                                                phased_update=True)
+                                                phased_update=self.scaler is None)
         else:
             self.step = graphs.GraphedTrainStep(self._train_step, preconditioner, [optimizer],
                                                 enabled=args.cuda)
@@ -63,16 +77,32 @@ class GraphedTrainer(object):
             self.grad_sync.zero_grad()
         else:
             self.optimizer.zero_grad(set_to_none=False)
-        with _autocast(self.args):
-            out = self.model(self.x)
-            loss = self.loss_func(out, self.y)
-        loss.backward()
-        return loss.detach(), out.detach()
+        k = self.micro
+        mb = self.x.shape[0] // k
+        losses, outs = [], []
+        for i in range(k):
+            xb, yb = (self.x, self.y) if k == 1 else \
+                (self.x[i * mb:(i + 1) * mb], self.y[i * mb:(i + 1) * mb])
+            with _autocast(self.args):
+                out = self.model(xb)
+                loss = self.loss_func(out, yb) / k
+            (self.scaler.scale(loss) if self.scaler is not None else loss).backward()
+            losses.append(loss.detach())
+            outs.append(out.detach())
+        if k == 1:
+            return losses[0], outs[0]
+        return torch.stack(losses).sum(), torch.cat(outs)
 
     def _update(self):
+        if self.scaler is not None:
+            self.scaler.unscale_(self.optimizer)     # K-FAC reads unscaled gradients
         if self.pre is not None:
             self.pre.step()
-        self.optimizer.step()
+        if self.scaler is not None:
+            self.scaler.step(self.optimizer)         # fused SGD: skips on device at inf
+            self.scaler.update()
+        else:
+            self.optimizer.step()
 
     def _train_step(self):
         res = self._forward_backward()
@@ -103,6 +133,8 @@ class GraphedTrainer(object):
                 dist.broadcast(b.data, src=0)
 
     def __call__(self, data, target):
+        if data.shape[0] % self.micro:
+            return self._eager(data, target)       # ragged batch: no equal micro-batches
         if self.x is None:
             self.x, self.y = data.clone(), target.clone()
         elif data.shape != self.x.shape or data.stride() != self.x.stride() or \

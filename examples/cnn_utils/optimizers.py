@@ -19,8 +19,12 @@ COMM = {'comm-opt': kfac.CommMethod.COMM_OPT, 'mem-opt': kfac.CommMethod.MEM_OPT
 
 def get_optimizer(model, args, batch_first=True):
     use_kfac = args.kfac_update_freq > 0
+    # fp16 + GradScaler on the GPU: the fused SGD takes the scaler's found_inf
+    # / scale as device tensors (no host read: capturable in the graphed
+    # loop; the eager loop uses the same optimizer so both train alike)
+    fused = getattr(args, 'grad_scaler', None) is not None
     optimizer = optim.SGD(model.parameters(), lr=args.base_lr, momentum=args.momentum,
-                          weight_decay=args.weight_decay)
+                          weight_decay=args.weight_decay, **({'fused': True} if fused else {}))
     preconditioner = None
     if use_kfac:
         if args.kfac_comm_method not in COMM:

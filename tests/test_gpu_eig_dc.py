@@ -192,3 +192,19 @@ def test_beyond_limit_falls_back(monkeypatch):
         an = ref.abs().max().item()
         res = ((A64 @ Q64 - Q64 * d64).norm() / (an * n ** 0.5)).item()
         assert res <= 2e-5 and ((d64 - ref.clamp(min=0)).abs().max() / an).item() <= 1e-5
+
+
+@pytest.mark.parametrize('n', [1152, 4608])
+def test_eigenvectors_bitwise_reproducible(n):
+    """The back-transformation's split-K GEMM sums its K-chunk slabs in a
+    fixed order (csrc/eig_backtransform.hip slab_sum_kernel): repeated solves
+    of the same factor give bitwise-equal eigenvectors (round 3's f32 atomics
+    did not)."""
+    A = _kfac_factor(n, 77).float()
+    outs = []
+    for _ in range(3):
+        (Q, d), = eigen.symeig_many([A])
+        outs.append((Q.clone(), d.clone()))
+    torch.cuda.synchronize()
+    for Q, d in outs[1:]:
+        assert torch.equal(Q, outs[0][0]) and torch.equal(d, outs[0][1])
