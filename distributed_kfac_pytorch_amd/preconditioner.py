@@ -283,6 +283,9 @@ class KFAC(optim.Optimizer):
         self._factor_stream = None
         self._early_a = None        # the A jobs in flight (keeps the activations alive)
         self._early_a_step = None
+        self._fwd_step = None       # forward passes per step (_count_forward)
+        self._fwd_calls = 0
+        self._prev_fwd_calls = None
         self._reverse_hooked = False
         self._segmented_capture = False   # set by graphs.GraphedTrainStep
         # compute_factor_in_hook on the GPU: gradient hooks of this step seen /
@@ -482,7 +485,28 @@ class KFAC(optim.Optimizer):
     def _no_autocast(self, t):
         return torch.autocast(device_type=t.device.type, enabled=False)
 
+    def _count_forward(self, module):
+        """Forward passes per step, counted at the first K-FAC layer's hook:
+        early_factors launches the A update from a step's FIRST backward,
+        which is the step() result only with one forward/backward per step
+        (several micro-batches apply the EMA from the last one)."""
+        if not self.layers or module is not self.layers[0].module:
+            return
+        st = self.param_groups[0]['step']
+        if self._fwd_step != st:
+            self._prev_fwd_calls = self._fwd_calls if self._fwd_step is not None else None
+            self._fwd_step, self._fwd_calls = st, 0
+        self._fwd_calls += 1
+        if self._fwd_calls > 1 and self._early_a_step == st:
+            # the pattern changed under an early launch: this step's A got
+            # the first micro-batch's EMA as well; stop launching early
+            warnings.warn('K-FAC early_factors: several forward passes in one step (micro-'
+                          'batching); early A-factor launches disabled')
+            self.early_factors = False
+
     def _forward_hook(self, module, input, output, reverse=False):
+        if torch.is_grad_enabled() and self.early_factors:
+            self._count_forward(module)
         if not (torch.is_grad_enabled() and self._factor_step()):
             return
         layer = self.hook_layers[module]
@@ -568,6 +592,9 @@ class KFAC(optim.Optimizer):
         p = self.param_groups[0]
         return (self.early_factors and self._early_a is None and self.grouped_factors
                 and self._early_a_step != p['step'] and not self.compute_factor_in_hook
+                # exactly one forward pass in the previous step and so far in
+                # this one (micro-batching: the early A would not be step()'s)
+                and self._prev_fwd_calls == 1 and self._fwd_calls == 1
                 and not self.accumulate_data and not self._reverse_hooked
                 and bool(self.layers) and self.layers[0].module.weight.is_cuda
                 # a segmented capture would fork in the forward/backward graph and
@@ -1255,7 +1282,15 @@ class KFAC(optim.Optimizer):
             # its graphs on plan_generation and KFAC's tail graph on buffer
             # pointers, so no graph older than that can replay again, and
             # work already enqueued on the old buffers is ordered before
-            # anything that reuses their memory on the same stream.
+            # anything that reuses their memory on the same stream.  Work on
+            # OTHER streams (a lagged inverse solve, the communicator's
+            # eigendata all-gather, the early-factor stream) is not: the
+            # host joins the solver thread and the device drains before the
+            # plan retired earlier is released (re-plans are rare).
+            if self._retired_plans:
+                self.wait_inverses()
+                if device.type == 'cuda':
+                    torch.cuda.synchronize(device)
             self._retired_plans = [(self.plan, self.fused)]
         self.plan = ExecutionPlan(self.layers, world, rank, a_locs, g_locs, allocator,
                                   self.use_eigen_decomp, self.precompute_outer_eigen,

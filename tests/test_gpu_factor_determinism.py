@@ -268,3 +268,42 @@ def test_hook_factors_grouped_unused_output():
         assert (G0 is None) == (G1 is None)
         if G0 is not None:
             assert torch.equal(G0, G1)
+
+
+def test_early_factors_micro_batching_equivalent():
+    """early_factors with two forward/backward passes per step (micro-batching,
+    accumulate_data=False): no early A launch (it would apply the first
+    micro-batch's EMA on top of step()'s), so the factors equal the
+    non-early run bitwise."""
+    import distributed_kfac_pytorch_amd as kfac
+    from distributed_kfac_pytorch_amd.models import resnet
+
+    def run(early):
+        torch.manual_seed(0)
+        m = resnet.resnet_tiny(num_classes=10).cuda().to(memory_format=torch.channels_last)
+        pre = kfac.KFAC(m, factor_update_freq=1, inv_update_freq=100, damping=0.003,
+                        use_eigen_decomp=False, early_factors=early)
+        g = torch.Generator(device='cuda').manual_seed(9)
+        for _ in range(4):
+            for _ in range(2):
+                x = torch.randn(8, 3, 32, 32, device='cuda', generator=g).contiguous(
+                    memory_format=torch.channels_last)
+                y = torch.randint(0, 10, (8,), device='cuda', generator=g)
+                with torch.autocast('cuda', dtype=torch.bfloat16):
+                    loss = F.cross_entropy(m(x), y) / 2
+                loss.backward()
+            pre.step()
+            m.zero_grad(set_to_none=False)
+        torch.cuda.synchronize()
+        return [l.state[w].clone() for l in pre.layers for w in ('A', 'G')], pre
+
+    prev = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        f0, _ = run(False)
+        f1, pre = run(True)
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = prev
+    assert pre._early_a_step is None       # never launched early
+    for a, b in zip(f0, f1):
+        assert torch.equal(a, b), (a - b).abs().max()
