@@ -556,10 +556,14 @@ class KFAC(optim.Optimizer):
     def _hook_factors_grouped(self):
         """compute_factor_in_hook on the GPU: save in the hooks, and run the
         grouped SYRK + EMA launches from the backward's last gradient hook
-        instead of ~3 launches per factor from every hook."""
+        instead of ~3 launches per factor from every hook.  With
+        accumulate_data (an LSTM: every gate Linear runs once per time step)
+        the last hook folds ALL of the backward's sources into one EMA per
+        factor -- the factors of computing them in step() after that
+        backward (reference accumulate semantics, kfac/layers/base.py:364-379),
+        instead of one EMA per time step."""
         return (self.compute_factor_in_hook and self.grouped_factors and bool(self.layers)
-                and self.layers[0].module.weight.is_cuda and not self.accumulate_data
-                and not self._reverse_hooked)
+                and self.layers[0].module.weight.is_cuda and not self._reverse_hooked)
 
     def _hook_counters(self):
         st = self.param_groups[0]['step']

@@ -307,3 +307,62 @@ def test_early_factors_micro_batching_equivalent():
     assert pre._early_a_step is None       # never launched early
     for a, b in zip(f0, f1):
         assert torch.equal(a, b), (a - b).abs().max()
+
+
+@pytest.mark.parametrize('graphed', [False, True])
+def test_lstm_lm_hook_factors_grouped_segmented_bitwise(graphed):
+    """The LSTM LM (accumulate_data=True, bptt 20) on the multi-rank
+    segmented-graph layout (forward/backward graph, eager communicate,
+    update graph) with the factors computed in the captured hooks: the
+    grouped in-hook path folds every time step's sources into one launch
+    sequence at the backward's last gradient hook, and the factors and the
+    trajectory are bitwise those of computing the factors in step()."""
+    import distributed_kfac_pytorch_amd as kfac
+    from distributed_kfac_pytorch_amd import graphs
+    from distributed_kfac_pytorch_amd.models import lstm_lm
+
+    def run(hook, use_graphs):
+        torch.manual_seed(0)
+        m = lstm_lm.LSTMModel(500, 64, 64, 2, dropout=0.0).cuda()
+        opt = torch.optim.SGD(m.parameters(), lr=0.5)
+        pre = kfac.KFAC(m, factor_update_freq=1, inv_update_freq=3, damping=0.003,
+                        accumulate_data=True, compute_factor_in_hook=hook,
+                        skip_layers=['embedding', 'decoder'], use_eigen_decomp=False)
+        g = torch.Generator(device='cuda').manual_seed(2)
+        xs = [torch.randint(0, 500, (20, 8), device='cuda', generator=g) for _ in range(6)]
+        ys = [torch.randint(0, 500, (20, 8), device='cuda', generator=g) for _ in range(6)]
+        x, y = torch.empty_like(xs[0]), torch.empty_like(ys[0])
+
+        def fb():
+            opt.zero_grad(set_to_none=False)
+            with torch.autocast('cuda', dtype=torch.bfloat16):
+                out, _ = m(x)
+                loss = F.cross_entropy(out.float().view(-1, 500), y.view(-1))
+            loss.backward()
+            return loss
+
+        def update():
+            pre.step()
+            opt.step()
+        step = graphs.GraphedTrainStep(None, pre, [opt], warmup=1, enabled=use_graphs,
+                                       forward_backward=fb, communicate=lambda: None,
+                                       update=update)
+        for i in range(6):
+            x.copy_(xs[i])
+            y.copy_(ys[i])
+            step()
+        torch.cuda.synchronize()
+        return ([l.state[w].clone() for l in pre.layers for w in ('A', 'G')],
+                [p.detach().clone() for p in m.parameters()], pre, step)
+
+    # baseline: eager, factors in step() (a replayed graph runs no Python
+    # hook, so the graphed layout needs the in-hook factors)
+    f0, p0, _, _ = run(False, False)
+    f1, p1, pre, step = run(True, graphed)
+    assert pre._hook_factors_grouped() and pre.accumulate_data
+    if graphed:
+        assert step.replays > 0
+    for a, b in zip(f0, f1):
+        assert torch.equal(a, b), (a - b).abs().max()
+    for a, b in zip(p0, p1):
+        assert torch.equal(a, b), (a - b).abs().max()
