@@ -52,6 +52,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 namespace {
@@ -60,7 +61,7 @@ constexpr int SB = 16;            // half-bandwidth
 constexpr int BW = 2 * SB;        // stored floats per band row
 constexpr int RS = 36;            // LDS row stride (16-B aligned rows; conflict-free strides)
 constexpr int NSLOT = 4;          // ring blocks per wave
-constexpr int NW = 4;             // waves (sweeps) per workgroup
+constexpr int NW4 = 4;            // waves (sweeps) per workgroup (default; 8 with KFAC_SB2ST_DBG & 32)
 constexpr int LAG = 3;            // ticks between consecutive sweeps
 constexpr int SLOTF = SB * RS;    // floats per ring block
 constexpr int SC1 = 16;           // buffer-op cache policy: sc1 (write-through / L1-bypass)
@@ -78,7 +79,9 @@ struct SbMat {
   long long ldv2;
   int n, dbg;             // dbg (timing experiments, KFAC_SB2ST_DBG): 1 = no polls, 2 = no publish wait,
                           // 8 = per-workgroup start / end stamps, 16 = XCD-affine workgroup order
-  long long* ts;          // dbg & 8: [workgroup][2] s_memrealtime stamps (100 MHz)
+  long long* ts;          // dbg & 8: [workgroup][2] s_memrealtime stamps (100 MHz); dbg & 128:
+                          // then 8 ticks x 8 phase stamps (s_memtime) of group 0's wave 1
+  int nwg;                // workgroups of the launch (stamp layout)
 };
 struct SbWg { int mat, g; };
 
@@ -127,16 +130,47 @@ __device__ __forceinline__ void wait_count(int* p, int need, int* err) {
   }
 }
 
-__global__ __launch_bounds__(64 * NW) void sb2st_kernel(const SbMat* __restrict__ mats,
-                                                       const SbWg* __restrict__ wgs) {
+// LDS layout of a workgroup (floats): the NW compute waves' rings, the IO
+// wave's staging ring for wave 0, the poll words, one dummy word per wave
+constexpr int NST = 8;            // staging slots (16 rows x 32 floats, lane-linear DMA image)
+constexpr int STF = SB * BW;      // floats per staging slot
+constexpr int PD = 4;             // IO wave: blocks loaded PD ticks ahead of wave 0's use
+template <int NW> constexpr int lds_floats() { return NW * NSLOT * SLOTF + NST * STF + 4 * 64 + NW + 1; }
+
+// LDS-DMA (buffer_load ... lds): each lane's `size` bytes land at base + lane * size
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, float* lds_base, int voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds_base, 16,
+                                           voff, 0, 0, SC1);
+}
+__device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t rs, int* lds_base, int voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds_base, 4,
+                                           voff, 0, 0, SC1);
+}
+
+// Waves 0 .. NW-1 run the sweeps (as before); wave NW is the IO wave: it
+// polls the predecessor group's published count and streams wave 0's band
+// blocks into LDS with LDS-DMA, PD ticks ahead, with COUNTED waits only (no
+// VGPR destinations, so no compiler-inserted vmcnt(0)): its tick issues
+// exactly three memory ops -- the poll DMA for tick t + 2 and the two 1-KB
+// DMAs of block t + PD -- and first waits vmcnt(3), i.e. for everything of
+// ticks <= t - 2 (block t + 2, wave 0's next copy, and the poll it reads now).
+// Round 3's register prefetch in wave 0 waited vmcnt(0) after every load
+// (register copies at the set merge) and its poll drained the queue: a
+// global round trip inside every other tick.
+template <int NW>
+__global__ __launch_bounds__(64 * (NW + 1)) void sb2st_kernel(const SbMat* __restrict__ mats,
+                                                             const SbWg* __restrict__ wgs) {
   const SbWg W = wgs[blockIdx.x];
   if (W.mat < 0) return;                         // XCD-affine order: padding slot
   const SbMat M = mats[W.mat];
   if (M.ts && threadIdx.x == 0) M.ts[2 * blockIdx.x] = (long long)__builtin_amdgcn_s_memrealtime();
   const int n = M.n, grp = W.g;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  extern __shared__ float lds[];                 // NW x NSLOT x SLOTF floats (+ padding)
-  float* my = lds + w * (NSLOT * SLOTF);
+  extern __shared__ float lds[];
+  float* stage = lds + NW * NSLOT * SLOTF;       // NST slots
+  int* polls = (int*)(stage + NST * STF);        // 4 x 64 words
+  float* dummy = (float*)(polls + 4 * 64) + w;   // one spare word per wave
+  float* my = lds + (w < NW ? w : 0) * (NSLOT * SLOTF);
   const float* prod = lds + ((w + NW - 1) % NW) * (NSLOT * SLOTF);
   AS1 float* v2 = gptr(M.v2);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -150,12 +184,14 @@ __global__ __launch_bounds__(64 * NW) void sb2st_kernel(const SbMat* __restrict_
     }
   }
   const int nsw = n - 2;                          // sweeps with tasks: 0 .. n - 3
-  const int s = grp * NW + w;
-  const int J = s < nsw ? sweep_tasks(n, s) : 0;
+  const int s0 = grp * NW;                        // wave 0's sweep
+  const int s = s0 + (w < NW ? w : 0);
+  const int J = (w < NW && s < nsw) ? sweep_tasks(n, s) : 0;
+  const int J0 = s0 < nsw ? sweep_tasks(n, s0) : 0;
   int T = 0;                                      // ticks of the group (uniform)
 #pragma unroll 1
   for (int ww = 0; ww < NW; ++ww) {
-    const int ss = grp * NW + ww;
+    const int ss = s0 + ww;
     const int jj = ss < nsw ? sweep_tasks(n, ss) : 0;
     if (jj > 0) T = max(T, LAG * ww + jj);
   }
@@ -164,35 +200,47 @@ __global__ __launch_bounds__(64 * NW) void sb2st_kernel(const SbMat* __restrict_
   const int g = lane >> 4, li = lane & 15;
   int* prev = grp > 0 ? M.prog + grp - 1 : nullptr;
   int* mine = M.prog + grp;
-  // producer blocks (previous group's last sweep s - 1 of wave 0) that block k
-  // of wave 0's sweep needs: rows s+1+16k .. min(s+16+16k, n-1)
+  const bool polling = prev && !(M.dbg & 1);
+  // producer blocks (previous group's last sweep s0 - 1) that block k of
+  // wave 0's sweep needs: rows s0+1+16k .. min(s0+16+16k, n-1)
   auto need_of = [&](int k) {
-    const int rlo = s + 1 + SB * k;
+    const int rlo = s0 + 1 + SB * k;
     if (rlo > n - 1) return 0;
-    const int rhi = min(s + SB + SB * k, n - 1);
-    return (rhi - s) / SB + 1;
+    const int rhi = min(s0 + SB + SB * k, n - 1);
+    return (rhi - s0) / SB + 1;
   };
-  fx4 R0[2], R1[2], R2[2], R3[2];
-  auto gload = [&](int k, fx4 (&dst)[2]) {
-    const int r = s + 1 + SB * k + ci;
-    const bool ok = r < n;
-    const int o = ok ? (r * BW + cq * 8) * 4 : 0;
-    const fx4 a = band_ld(rs, o);
-    const fx4 b = band_ld(rs, o + 16);
-    const fx4 z = {0.f, 0.f, 0.f, 0.f};
-    dst[0] = ok ? a : z;
-    dst[1] = ok ? b : z;
+  // IO wave: block k of wave 0's sweep (rows s0+1+16k ..: 2 KB contiguous in
+  // the band; rows n .. n+31 are zero, rows past them out of range -> zero)
+  auto dma_block = [&](int k) {
+    float* dst = stage + (k % NST) * STF;
+    const int vo = (s0 + 1 + SB * k) * BW * 4 + lane * 16;
+    dma16(rs, dst, vo);
+    dma16(rs, dst + 256, vo + 1024);
   };
-  auto lput = [&](int k, const fx4 (&src)[2]) {
-    float* dst = my + (k % NSLOT) * SLOTF + ci * RS + cq * 8;
-    *(fx4*)dst = src[0];
-    *(fx4*)(dst + 4) = src[1];
-  };
-  if (w == 0 && J > 0) {
-    if (prev && !(M.dbg & 1)) wait_count(prev, need_of(3), M.err);
-    gload(0, R0); gload(1, R1); gload(2, R2); gload(3, R3);
-    lput(0, R0);
+  const __amdgpu_buffer_rsrc_t rsp = __builtin_amdgcn_make_buffer_rsrc(
+      M.prog, 0, (grp + 1) * 4, 0x00020000);
+  const int poll_off = (grp > 0 ? grp - 1 : grp) * 4;
+  if (w == NW) {
+    if (J0 > 0) {
+      int c0 = 0;
+      if (polling) {
+        wait_count(prev, need_of(PD - 1), M.err);
+        c0 = __hip_atomic_load(prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      for (int k = 0; k < PD; ++k) dma_block(k);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) { polls[2 * 64] = c0; polls[3 * 64] = c0; }
+    }
   }
+  kfac_lds_barrier();
+  // wave 0 copies block k from the staging slot (rows of 32) into its ring
+  auto lput = [&](int k) {
+    const float* src = stage + (k % NST) * STF + ci * BW + cq * 8;
+    float* dst = my + (k % NSLOT) * SLOTF + ci * RS + cq * 8;
+    *(fx4*)dst = *(const fx4*)src;
+    *(fx4*)(dst + 4) = *(const fx4*)(src + 4);
+  };
+  if (w == 0 && J > 0) lput(0);
   // fill my block k from the previous wave's blocks k (rows 1..15) and
   // k + 1 (row 0); rows past n read as zero
   auto ring_fill = [&](int k) {
@@ -218,30 +266,39 @@ __global__ __launch_bounds__(64 * NW) void sb2st_kernel(const SbMat* __restrict_
 
 #pragma unroll 1
   for (int t = 0; t < T; ++t) {
+    if (w == NW) {
+      // ---- IO wave: ticks <= t - 2 landed (block t + 2, the poll of t - 2)
+      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      if (t + PD < J0 + 2) {
+        if (polling) {
+          const int c = polls[((t + 2) & 3) * 64];
+          const int need = need_of(t + PD);
+          if (c < need) wait_count(prev, need, M.err);   // slow path (drains the queue)
+        }
+      }
+      dma4(rsp, polls + (t & 3) * 64, poll_off);
+      dma_block(t + PD);
+      kfac_lds_barrier();
+      continue;
+    }
     const int j = t - LAG * w;
+    const bool stamp = (M.dbg & 128) && M.ts && grp == 0 && w == 1 && t >= 20 && t < 28;
+    long long* st = stamp ? M.ts + 2 * M.nwg + (t - 20) * 8 : nullptr;
+#define SB2ST_STAMP(ph)                                                     \
+    if (stamp && lane == 0) st[ph] = (long long)__builtin_amdgcn_s_memtime();
+    SB2ST_STAMP(0)
     if (w > 0 && J > 0 && j == -1) ring_fill(0);
     if (j >= 0 && j < J) {
       // ---- block j + 1 (the rows below this task's reflector)
-      if (w == 0) {
-        switch ((j + 1) & 3) {
-          case 0: lput(j + 1, R0); break;
-          case 1: lput(j + 1, R1); break;
-          case 2: lput(j + 1, R2); break;
-          default: lput(j + 1, R3); break;
-        }
-        if ((j & 1) == 0) {
-          // blocks j+4, j+5 into the sets of blocks j, j+1 (both in LDS now)
-          if (prev && !(M.dbg & 1)) wait_count(prev, need_of(j + 5), M.err);
-          if (j & 2) { gload(j + 4, R2); gload(j + 5, R3); }
-          else { gload(j + 4, R0); gload(j + 5, R1); }
-        }
-      } else {
-        ring_fill(j + 1);
-      }
+      if (w == 0) lput(j + 1);
+      else ring_fill(j + 1);
+      SB2ST_STAMP(1)
       if (w == NW - 1) {
-        // publish the blocks stored two tasks ago (their stores are the only
-        // memory ops this wave issued before the last ~4)
-        if (!(M.dbg & 2)) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        // publish the blocks stored two tasks ago: this wave's vector memory
+        // ops per task are the V2 store then the two band stores, so with
+        // the previous task's three still in flight (vmcnt(3)) every older
+        // band store has completed
+        if (!(M.dbg & 2)) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
         __hip_atomic_store(mine, j > 0 ? j - 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       const int r0 = s + 1 + SB * j;
@@ -260,7 +317,6 @@ __global__ __launch_bounds__(64 * NW) void sb2st_kernel(const SbMat* __restrict_
       float* P = g2 ? S1 : S0;
       const int boff = g0 ? 16 + li : (g1 ? 35 * li + 31 : 35 * li + 15);
       const int bstr = g0 ? 35 : 1;
-      float* dummy = lds + NW * NSLOT * SLOTF + w;      // one spare word per wave
       float* addr[SB];
 #pragma unroll
       for (int l = 0; l < SB; ++l) {
@@ -275,6 +331,8 @@ __global__ __launch_bounds__(64 * NW) void sb2st_kernel(const SbMat* __restrict_
       float* xp = S0 + 35 * (lane & 15) + xo;
       const float xl = *xp;
       const float x = (lane < L) ? xl : 0.f;
+      if (stamp) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+      SB2ST_STAMP(2)
       const float alpha = rdlane(x, 0);
       const float sig = wave_sum((lane >= 1 && lane < L) ? x * x : 0.f);
       float tau = 0.f, beta = alpha, scal = 0.f;
@@ -284,6 +342,7 @@ __global__ __launch_bounds__(64 * NW) void sb2st_kernel(const SbMat* __restrict_
         scal = __builtin_amdgcn_rcpf(alpha - beta);
       }
       const float v = lane == 0 ? 1.f : ((lane < L) ? x * scal : 0.f);
+      SB2ST_STAMP(3)
       if (lane < L) {
         *xp = lane == 0 ? beta : 0.f;
         v2[(long long)s * M.ldv2 + SB * j + lane] = lane == 0 ? tau : v;
@@ -307,6 +366,7 @@ __global__ __launch_bounds__(64 * NW) void sb2st_kernel(const SbMat* __restrict_
         const float p = tau * dot;
         const float kk = 0.5f * tau * row_sum16(vli * p);
         const float wv = p - kk * vli;
+        SB2ST_STAMP(4)
         float wl[SB];
 #pragma unroll
         for (int l = 0; l < SB; ++l) wl[l] = rdlane(wv, 16 + l);
@@ -320,6 +380,7 @@ __global__ __launch_bounds__(64 * NW) void sb2st_kernel(const SbMat* __restrict_
           *pa = nv;
         }
       }
+      SB2ST_STAMP(5)
       // ---- outputs finished by this task
       if (j == 0 && lane == 0) {
         M.d[s + 1] = S0[31];
@@ -336,8 +397,13 @@ __global__ __launch_bounds__(64 * NW) void sb2st_kernel(const SbMat* __restrict_
         }
       }
     }
+    if (stamp) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+    SB2ST_STAMP(6)
     kfac_lds_barrier();
+    SB2ST_STAMP(7)
+#undef SB2ST_STAMP
   }
+  if (w == NW) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA outlives the group
   // a group whose last sweep has no task still releases its successor
   if (w == NW - 1 && J == 0 && lane == 0)
     __hip_atomic_store(mine, DONE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -352,7 +418,7 @@ struct SbPlan {
   SbMat* d_mats = nullptr;
   SbWg* d_wgs = nullptr;
   int* d_prog = nullptr;       // all matrices' group counters, then the error count
-  int nprog = 0, nwg = 0;
+  int nprog = 0, nwg = 0, nw = NW4;
   long long* d_ts = nullptr;
   hipGraphExec_t exec = nullptr;
 };
@@ -364,11 +430,15 @@ std::vector<SbWg> g_last_wgs;
 // 37 KB of ring per workgroup, padded so that exactly one workgroup sits on a
 // CU (the sc1 hand-off's measured form)
 constexpr size_t LDS_BYTES = 96 * 1024;
-static_assert((size_t)(NW * NSLOT * SLOTF + NW) * sizeof(float) <= LDS_BYTES, "ring exceeds LDS");
+static_assert((size_t)lds_floats<8>() * sizeof(float) <= LDS_BYTES, "ring exceeds LDS");
 
 int enqueue(const SbPlan& P, hipStream_t s) {
   hipLaunchKernelGGL(sb2st_zero_kernel, dim3(4), dim3(256), 0, s, P.d_prog, P.nprog + 1);
-  hipLaunchKernelGGL(sb2st_kernel, dim3(P.nwg), dim3(64 * NW), LDS_BYTES, s, P.d_mats, P.d_wgs);
+  if (P.nw == 8)
+    hipLaunchKernelGGL(sb2st_kernel<8>, dim3(P.nwg), dim3(64 * 9), LDS_BYTES, s, P.d_mats, P.d_wgs);
+  else
+    hipLaunchKernelGGL(sb2st_kernel<NW4>, dim3(P.nwg), dim3(64 * (NW4 + 1)), LDS_BYTES, s,
+                       P.d_mats, P.d_wgs);
   return (int)hipGetLastError();
 }
 
@@ -381,7 +451,7 @@ std::map<std::string, SbPlan> g_plans;
 KFAC_API int kfac_sb2st_debug_stamps(long long* out, int max_wg) {
   if (!g_last_ts) return 0;
   const int nw = std::min(max_wg, g_last_nwg);
-  std::vector<long long> t(2 * (size_t)g_last_nwg);
+  std::vector<long long> t(2 * (size_t)g_last_nwg);  // (the phase stamps follow)
   if (hipMemcpy(t.data(), g_last_ts, sizeof(long long) * t.size(), hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
   for (int b = 0; b < nw; ++b) {
@@ -389,6 +459,13 @@ KFAC_API int kfac_sb2st_debug_stamps(long long* out, int max_wg) {
     out[4 * b + 2] = t[2 * b]; out[4 * b + 3] = t[2 * b + 1];
   }
   return nw;
+}
+
+// dbg & 128: the 64 phase stamps (8 ticks x 8 phases, s_memtime cycles)
+KFAC_API int kfac_sb2st_debug_phases(long long* out) {
+  if (!g_last_ts) return 0;
+  return (int)hipMemcpy(out, g_last_ts + 2 * g_last_nwg, sizeof(long long) * 64,
+                        hipMemcpyDeviceToHost);
 }
 
 struct KfacSb2stRecord {
@@ -405,8 +482,10 @@ KFAC_API int kfac_sb2st_batched(const KfacSb2stRecord* recs, int count, int use_
   if (count <= 0) return 0;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute((const void*)sb2st_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)LDS_BYTES) != hipSuccess)
+    if (hipFuncSetAttribute((const void*)sb2st_kernel<NW4>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES) != hipSuccess ||
+        hipFuncSetAttribute((const void*)sb2st_kernel<8>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES) != hipSuccess)
       return -7;
     attr = true;
   }
@@ -422,7 +501,8 @@ KFAC_API int kfac_sb2st_batched(const KfacSb2stRecord* recs, int count, int use_
     M.ldv2 = r.ldv2; M.n = (int)r.n;
     M.dbg = getenv("KFAC_SB2ST_DBG") ? atoi(getenv("KFAC_SB2ST_DBG")) : 0;
     const int nsw = (int)r.n - 2;
-    ngrp[i] = nsw > 0 ? (nsw + NW - 1) / NW : 1;
+    const int nw = (M.dbg & 32) ? 8 : NW4;
+    ngrp[i] = nsw > 0 ? (nsw + nw - 1) / nw : 1;
     nprog += ngrp[i];
   }
   hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
@@ -435,6 +515,7 @@ KFAC_API int kfac_sb2st_batched(const KfacSb2stRecord* recs, int count, int use_
     auto it = g_plans.find(key);
     if (it == g_plans.end()) {
       SbPlan P;
+      P.nw = (mats[0].dbg & 32) ? 8 : NW4;
       int err;
       if ((err = (int)hipMalloc(&P.d_prog, sizeof(int) * (nprog + 1))) != 0) return err;
       P.nprog = nprog;
@@ -463,8 +544,8 @@ KFAC_API int kfac_sb2st_batched(const KfacSb2stRecord* recs, int count, int use_
       }
       P.nwg = (int)wgs.size();
       if (dbg & 8) {
-        if ((err = (int)hipMalloc(&P.d_ts, sizeof(long long) * 2 * P.nwg)) != 0) return err;
-        for (auto& M : mats) M.ts = P.d_ts;
+        if ((err = (int)hipMalloc(&P.d_ts, sizeof(long long) * (2 * P.nwg + 64))) != 0) return err;
+        for (auto& M : mats) { M.ts = P.d_ts; M.nwg = P.nwg; }
         g_last_ts = P.d_ts; g_last_nwg = P.nwg; g_last_wgs = wgs;
       }
       if ((err = (int)hipMalloc(&P.d_mats, sizeof(SbMat) * count)) != 0) return err;

@@ -70,6 +70,7 @@ Eager steps and replays run on one side stream, joined to the caller's
 stream by events; the device is synchronised once after each eager
 (inverse-update) step, which also drains the eigensolver's worker streams.
 """
+import gc
 import warnings
 
 import torch
@@ -364,6 +365,12 @@ class GraphedTrainStep(object):
             self.pre.wait_inverses()   # no solver-thread library calls during a capture
         torch.cuda.synchronize()
         g = _lib.new_graph()
+        # no Python garbage collection inside the capture: a collected cycle
+        # holding a HIP event or graph destroys it mid-capture (an illegal
+        # call under global capture mode -> abort from the destructor; seen
+        # with the LSTM LM's many per-time-step objects)
+        gc_on = gc.isenabled()
+        gc.disable()
         try:
             # a private memory pool per graph: segments and kinds replay in
             # any order, so one graph's outputs must never alias another's
@@ -373,12 +380,16 @@ class GraphedTrainStep(object):
             # memset nodes (MIOpen's zeroed workspaces) -> fill kernels
             _lib.finalize_graph(g)
         except Exception as e:  # pragma: no cover - depends on the HIP runtime
+            if gc_on:
+                gc.enable()
             warnings.warn('hipGraph capture of the training step failed ({}); running '
                           'eagerly from now on'.format(e))
             self.enabled = False
             if self.pre is not None:
                 self.pre.param_groups[0]['step'] = step0
             return fn()
+        if gc_on:
+            gc.enable()
         if self.pre is not None:
             # capture recorded the work without running it; a captured
             # preconditioner.step() advanced the step counter: rewind

@@ -81,6 +81,7 @@ _SIGS = {
     'kfac_sb2st_batched': [ctypes.POINTER(Sb2stRecord), c_int, c_int, c_vp],
     'kfac_backtransform_slabs': [c_int],
     'kfac_sb2st_debug_stamps': [ctypes.POINTER(ctypes.c_longlong), c_int],
+    'kfac_sb2st_debug_phases': [ctypes.POINTER(ctypes.c_longlong)],
     'kfac_q2_batched': [ctypes.POINTER(Q2Record), c_int, c_int, c_vp],
     'kfac_q2_nmax': [],
     'kfac_band_backtransform': [c_vp, c_int, c_ll, c_vp, c_vp, c_int, c_ll, c_int, c_int,

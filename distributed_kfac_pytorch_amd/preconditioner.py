@@ -29,6 +29,7 @@ world > 1; #4 HYBRID validation uses max(1, round(W*f)); #7 group averaging;
 """
 import enum
 import functools
+import gc
 import warnings
 
 import torch
@@ -875,16 +876,22 @@ class KFAC(optim.Optimizer):
             self._precondition_and_apply()
             return
         self.wait_inverses()   # no solver thread may run library calls during a capture
+        gc_on = gc.isenabled()
+        gc.disable()     # no collected HIP object destroyed mid-capture (graphs.py)
         try:
             g = _lib.new_graph()
             # the captured ops read .grad; run them on a clean copy of the
             # current grads after capture (capture itself does not execute)
             with torch.cuda.graph(g):
                 self._graph_scale = self._precondition_and_apply()
+            if gc_on:
+                gc.enable()
             _lib.finalize_graph(g)
             self._graph = g
             self._graph.replay()
         except Exception as e:  # pragma: no cover - depends on the HIP runtime
+            if gc_on:
+                gc.enable()
             warnings.warn('hipGraph capture of the K-FAC step failed ({}); running eagerly'
                           .format(e))
             self.use_hip_graphs = False

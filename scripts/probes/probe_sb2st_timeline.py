@@ -90,6 +90,17 @@ def main():
                          span, life[len(life) // 2], life[-1], lags[len(lags) // 2],
                          lags[len(lags) // 10], lags[9 * len(lags) // 10]))
         print(line, flush=True)
+        if d & 128:
+            ph = (ctypes.c_longlong * 64)()
+            L.kfac_sb2st_debug_phases(ph)
+            names = ['fill', 'loads', 'house', 'dot', 'update', 'outputs', 'barrier']
+            for t in range(8):
+                row = [ph[8 * t + k] for k in range(8)]
+                if row[0] == 0:
+                    continue
+                dl = ['%s %d' % (names[k], row[k + 1] - row[k]) for k in range(7)
+                      if row[k + 1] and row[k]]
+                print('  tick %d cycles: total %d | %s' % (20 + t, row[7] - row[0], ', '.join(dl)))
 
 
 if __name__ == '__main__':

@@ -344,13 +344,19 @@ def test_lstm_lm_hook_factors_grouped_segmented_bitwise(graphed):
         def update():
             pre.step()
             opt.step()
-        step = graphs.GraphedTrainStep(None, pre, [opt], warmup=1, enabled=use_graphs,
-                                       forward_backward=fb, communicate=lambda: None,
-                                       update=update)
+        step = None
+        if hook:
+            step = graphs.GraphedTrainStep(None, pre, [opt], warmup=1, enabled=use_graphs,
+                                           forward_backward=fb, communicate=lambda: None,
+                                           update=update)
         for i in range(6):
             x.copy_(xs[i])
             y.copy_(ys[i])
-            step()
+            if step is not None:
+                step()
+            else:            # the plain eager loop, factors in step()
+                fb()
+                update()
         torch.cuda.synchronize()
         return ([l.state[w].clone() for l in pre.layers for w in ('A', 'G')],
                 [p.detach().clone() for p in m.parameters()], pre, step)
