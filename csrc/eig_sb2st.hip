@@ -282,10 +282,18 @@ __global__ __launch_bounds__(64 * (NW + 1)) void sb2st_kernel(const SbMat* __res
       continue;
     }
     const int j = t - LAG * w;
+#ifdef SB2ST_PHASE_STAMPS
+    // (compile-time only: the stamps' SMEM / flat ops share lgkmcnt with the
+    // LDS reads and make every LDS wait a full drain)
     const bool stamp = (M.dbg & 128) && M.ts && grp == 0 && w == 1 && t >= 20 && t < 28;
+#define SB2ST_IF if (stamp)
+#else
+    constexpr bool stamp = false;
+#define SB2ST_IF if constexpr (false)
+#endif
     long long* st = stamp ? M.ts + 2 * M.nwg + (t - 20) * 8 : nullptr;
 #define SB2ST_STAMP(ph)                                                     \
-    if (stamp && lane == 0) st[ph] = (long long)__builtin_amdgcn_s_memtime();
+    SB2ST_IF { if (lane == 0) st[ph] = (long long)__builtin_amdgcn_s_memtime(); }
     SB2ST_STAMP(0)
     if (w > 0 && J > 0 && j == -1) ring_fill(0);
     if (j >= 0 && j < J) {
@@ -323,18 +331,24 @@ __global__ __launch_bounds__(64 * (NW + 1)) void sb2st_kernel(const SbMat* __res
         const int off = (g1 && l > li) ? 35 * l + li + 31 : boff + bstr * l;
         addr[l] = act ? P + off : dummy;
       }
+      // ---- reflector column c first (lanes 0..15: row i = lane): the
+      // reflector math then runs while the 16 operand reads are in flight
+      const int xo = (j == 0) ? 30 : 15;        // column c's offset in row i: xo - i
+      float* xp = S0 + 35 * (lane & 15) + xo;
+      // (asm read + counted wait: the compiler's own wait for a value read
+      // before the 16 operand reads is lgkmcnt(0), i.e. all 17)
+      float xl;
+      asm volatile("ds_read_b32 %0, %1" : "=v"(xl) : "v"((unsigned)(size_t)xp) : "memory");
       float val[SB];
 #pragma unroll
       for (int l = 0; l < SB; ++l) val[l] = *addr[l];
-      // ---- reflector from column c (lanes 0..15: row i = lane)
-      const int xo = (j == 0) ? 30 : 15;        // column c's offset in row i: xo - i
-      float* xp = S0 + 35 * (lane & 15) + xo;
-      const float xl = *xp;
+      asm volatile("s_waitcnt lgkmcnt(16)" : "+v"(xl) :: "memory");
       const float x = (lane < L) ? xl : 0.f;
-      if (stamp) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+      SB2ST_IF { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
       SB2ST_STAMP(2)
       const float alpha = rdlane(x, 0);
-      const float sig = wave_sum((lane >= 1 && lane < L) ? x * x : 0.f);
+      // x lives on lanes 0..15: a 16-lane (DPP row) sum, read from lane 0
+      const float sig = rdlane(row_sum16((lane >= 1 && lane < L) ? x * x : 0.f), 0);
       float tau = 0.f, beta = alpha, scal = 0.f;
       if (sig != 0.f) {
         beta = -copysignf(__builtin_sqrtf(alpha * alpha + sig), alpha);
@@ -359,9 +373,8 @@ __global__ __launch_bounds__(64 * (NW + 1)) void sb2st_kernel(const SbMat* __res
         }
         const float dot = (d0 + d1) + (d2 + d3);
         // g1: w = tau D v - K v, K = tau / 2 v^T (tau D v)
-        // (the shuffle outside the select: a ?: arm is divergent code, and a
-        // bpermute from inactive source lanes reads zero)
-        const float vsh = rdlane_row(v, li);
+        // (the exchange outside the select: a ?: arm is divergent code)
+        const float vsh = __shfl_xor(v, 16, 64);   // lane 16 + li <- lane li (v_permlane16_swap)
         const float vli = g1 ? vsh : 0.f;
         const float p = tau * dot;
         const float kk = 0.5f * tau * row_sum16(vli * p);
@@ -397,11 +410,12 @@ __global__ __launch_bounds__(64 * (NW + 1)) void sb2st_kernel(const SbMat* __res
         }
       }
     }
-    if (stamp) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+    SB2ST_IF { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
     SB2ST_STAMP(6)
     kfac_lds_barrier();
     SB2ST_STAMP(7)
 #undef SB2ST_STAMP
+#undef SB2ST_IF
   }
   if (w == NW) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA outlives the group
   // a group whose last sweep has no task still releases its successor

@@ -356,8 +356,12 @@ def _ts_buffers(dev, n, b, slot=0):
         f32 = dict(dtype=torch.float32, device=dev)
         nblk = (n + BT - 1) // BT
         wsb = int(L.kfac_dc_ws_bytes(n))
+        # stage 1's Y launch reads whole 16-row blocks of A22, up to 15 rows
+        # past n (n == lda for 4608): 16 spare zero rows after the last matrix
+        a_full = torch.zeros(b * lda * lda + 16 * lda, **f32)
         bufs = dict(lda=lda, ldv2=ldv2, sA=lda * lda,
-                    A=torch.zeros(b, lda, lda, **f32), tau=torch.zeros(b, n, **f32),  # larft: stride n
+                    A=a_full[:b * lda * lda].view(b, lda, lda), A_full=a_full,
+                    tau=torch.zeros(b, n, **f32),  # larft: stride n
                     band=torch.zeros(b, (n + 2 * SB2) * 2 * SB2, **f32),
                     syws=torch.zeros(b, int(L.kfac_sy2sb_ws_floats(lda)), **f32),
                     v2=torch.zeros(b, max(n - 1, 1), ldv2, **f32),
