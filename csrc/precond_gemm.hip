@@ -186,7 +186,7 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   // zeroed by a select, so every load of a k-step issues back to back
   // per-thread 32-bit byte offsets of its chunks (operands < 4 GiB, checked
   // on the host); the k-step advances the uniform base pointer
-  u32x4n ra[QA], rb[QB];
+  u32x4n ra[2][QA], rb[2][QB];   // two k-steps of loads in flight (set = k-step parity)
   unsigned offa[QA], offb[QB];
   bool oka[QA], okb[QB];
 #pragma unroll
@@ -206,23 +206,22 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
     offb[q] = ((unsigned)(okb[q] ? n0 + row : n0) * (unsigned)ldb + kof) * ESZ;
   }
   const u32x4n z4 = {0u, 0u, 0u, 0u};
-  auto load = [&](int k0) {
+  auto load = [&](int k0, auto setc) {
+    constexpr int SET = decltype(setc)::value;
     const long long kb = (long long)k0 * ESZ;
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
       const int plane = PLANE_CT ? NT * q / (BM * CPR) : (tid + NT * q) / (BM * CPR);
       const AS1 unsigned char* base = (X6 ? (plane == 0 ? Ah : (plane == 1 ? Al : A2))
                                           : (plane ? Al : Ah)) + kb;
-      const u32x4n v = *(const AS1 u32x4n*)(base + offa[q]);
-      ra[q] = oka[q] ? v : z4;
+      ra[SET][q] = *(const AS1 u32x4n*)(base + offa[q]);   // rows past M: zeroed at the store
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
       const int plane = PLANE_CT ? NT * q / (BN * CPR) : (tid + NT * q) / (BN * CPR);
       const AS1 unsigned char* base = (X6 ? (plane == 0 ? Bh : (plane == 1 ? Bl : B2))
                                           : (plane ? Bl : Bh)) + kb;
-      const u32x4n v = *(const AS1 u32x4n*)(base + offb[q]);
-      rb[q] = okb[q] ? v : z4;
+      rb[SET][q] = *(const AS1 u32x4n*)(base + offb[q]);
     }
   };
   // LDS image: [A planes | B planes] rows of LDB16 bf16 (X3 / X6) or [A | B] rows of LDF32 f32
@@ -244,16 +243,22 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
     *(u32x2n*)(dst + plane_stride) = pm;
     *(u32x2n*)(dst + 2 * plane_stride) = pl;
   };
-  auto store = [&](unsigned char* img) {
+  // rows past the problem are zeroed HERE, not at the load: a select on a
+  // loaded value consumes it, so the compiler waited for the next k-step's
+  // loads right after issuing them -- before this k-step's MFMAs (the global
+  // latency of every k-step exposed)
+  auto store = [&](unsigned char* img, auto setc) {
+    constexpr int SET = decltype(setc)::value;
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
       const int c = tid + NT * q;
       const int plane = c / (BM * CPR);
       int row, kof;
       chunk_rc(c, BM, row, kof);
-      if (X6F) store_split((uint16_t*)img + row * LDB16 + x6f_off(row, kof), (long long)BM * LDB16, ra[q]);
-      else if (SPL) *(u32x4n*)((uint16_t*)img + (plane * BM + row) * LDB16 + kof) = ra[q];
-      else *(u32x4n*)((float*)img + row * LDF32 + kof) = (row & 16) ? ra[q].zwxy : ra[q];
+      const u32x4n v = oka[q] ? ra[SET][q] : z4;
+      if (X6F) store_split((uint16_t*)img + row * LDB16 + x6f_off(row, kof), (long long)BM * LDB16, v);
+      else if (SPL) *(u32x4n*)((uint16_t*)img + (plane * BM + row) * LDB16 + kof) = v;
+      else *(u32x4n*)((float*)img + row * LDF32 + kof) = (row & 16) ? v.zwxy : v;
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
@@ -261,10 +266,11 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
       const int plane = c / (BN * CPR);
       int row, kof;
       chunk_rc(c, BN, row, kof);
+      const u32x4n v = okb[q] ? rb[SET][q] : z4;
       if (X6F) store_split((uint16_t*)img + (PL * BM + row) * LDB16 + x6f_off(row, kof),
-                           (long long)BN * LDB16, rb[q]);
-      else if (SPL) *(u32x4n*)((uint16_t*)img + (PL * BM + plane * BN + row) * LDB16 + kof) = rb[q];
-      else *(u32x4n*)((float*)img + (BM + row) * LDF32 + kof) = (row & 16) ? rb[q].zwxy : rb[q];
+                           (long long)BN * LDB16, v);
+      else if (SPL) *(u32x4n*)((uint16_t*)img + (PL * BM + plane * BN + row) * LDB16 + kof) = v;
+      else *(u32x4n*)((float*)img + (BM + row) * LDF32 + kof) = (row & 16) ? v.zwxy : v;
     }
   };
 
@@ -277,20 +283,9 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int arow0 = wr * (BM / WM), brow0 = wc * (BN / WN);
-  load(0);
-  if constexpr (DBUF) {
-    store(smem);
-    __syncthreads();
-  }
-  for (int ks = 0; ks < ksteps; ++ks) {
-    unsigned char* cur = smem;
-    if constexpr (DBUF) {
-      cur = smem + (ks & 1) * LDS_BYTES;
-    } else {
-      store(smem);
-      __syncthreads();
-    }
-    if (ks + 1 < ksteps) load((ks + 1) * TK);   // global loads in flight under the MFMAs
+  using S0_ = std::integral_constant<int, 0>;
+  using S1_ = std::integral_constant<int, 1>;
+  auto mma = [&](const unsigned char* cur, unsigned char* nxt) {
     if constexpr (X3) {
       const uint16_t* sAh = (const uint16_t*)cur;
       const uint16_t* sAl = sAh + BM * LDB16;
@@ -381,11 +376,43 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
       }
     }
-    if constexpr (DBUF) {
-      // the idle image was last read in iteration ks-1, before its barrier
-      if (ks + 1 < ksteps) store(smem + ((ks + 1) & 1) * LDS_BYTES);
-    }
+  };
+  load(0, S0_());
+  if constexpr (DBUF) {
+    store(smem, S0_());
     __syncthreads();
+    for (int ks = 0; ks < ksteps; ++ks) {
+      const unsigned char* cur = smem + (ks & 1) * LDS_BYTES;
+      // the idle image was last read in iteration ks-1, before its barrier
+      unsigned char* nxt = (ks + 1 < ksteps) ? smem + ((ks + 1) & 1) * LDS_BYTES : nullptr;
+      if (ks + 1 < ksteps) load((ks + 1) * TK, S0_());   // global loads in flight under the MFMAs
+      mma(cur, nullptr);
+      if (nxt != nullptr) store(nxt, S0_());
+      __syncthreads();
+    }
+  } else {
+    // two k-steps of global loads in flight: set (ks & 1) is stored while
+    // the other set's loads are still arriving, so a k-step's loads have two
+    // k-steps of MFMAs to land (one k-step, ~1.3 us, did not cover an L2
+    // miss: SQ_WAIT_INST_ANY 47 % of wave cycles, profiles/r4_pmc_pgemm_*)
+    // The loads are issued unconditionally (past the last k-step they
+    // re-read k-step 0): the same number of loads on every path lets the
+    // compiler wait vmcnt(8) for one set instead of vmcnt(0) for both.
+    auto kclamp = [&](int k) { return k < ksteps ? k * TK : 0; };
+    load(kclamp(1), S1_());
+    for (int ks = 0; ks < ksteps; ks += 2) {
+      store(smem, S0_());
+      __syncthreads();
+      load(kclamp(ks + 2), S0_());
+      mma(smem, nullptr);
+      __syncthreads();
+      if (ks + 1 >= ksteps) break;
+      store(smem, S1_());
+      __syncthreads();
+      load(kclamp(ks + 3), S1_());
+      mma(smem, nullptr);
+      __syncthreads();
+    }
   }
 
   // ---- epilogue (C/D map of 32x32 MFMA: row = (r&3) + 8*(r>>2) + 4*lh, col = lr).

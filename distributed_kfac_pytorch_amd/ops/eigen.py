@@ -342,6 +342,10 @@ def _fused_group(mats, clip, stream, use_graph, slot=0):
 TWO_STAGE = bool(int(os.environ.get('KFAC_EIG_TWO_STAGE', '0')))
 TWO_STAGE_MIN = int(os.environ.get('KFAC_EIG_TWO_STAGE_MIN', '1024'))
 TWO_STAGE_MAX = 5120     # csrc/eig_sy2sb.hip NMAX2, csrc/eig_q2.hip 16 x QT
+# at most this many eligible factors (largest first) take the two-stage path
+# (0 = all): the two paths run concurrently on two streams, so moving only
+# part of the largest size class shortens the one-stage critical path
+TWO_STAGE_COUNT = int(os.environ.get('KFAC_EIG_TWO_STAGE_COUNT', '0'))
 SB2 = 16                 # band half-bandwidth
 _TS_BUFS = {}
 
@@ -487,6 +491,8 @@ def symeig_many(mats, clip=0.0, solver='auto'):
     ts = []
     if TWO_STAGE:
         ts = [i for i in large if TWO_STAGE_MIN <= mats[i].shape[0] <= TWO_STAGE_MAX]
+        if TWO_STAGE_COUNT > 0:
+            ts = sorted(ts, key=lambda i: -mats[i].shape[0])[:TWO_STAGE_COUNT]
         large = [i for i in large if i not in set(ts)]
     cur = torch.cuda.current_stream(mats[0].device)
     side = None

@@ -56,13 +56,16 @@ for s in "$@"; do
       find /tmp/prof_probe -name "*stats*.csv" -exec cp {} gpurun_out/prof_probe/ \;
       head -25 gpurun_out/prof_probe/*kernel_stats.csv | cut -c1-200 ;;
     pmc)
-      rm -rf /tmp/pmc_pass
-      timeout -s KILL 150 rocprofv3 --kernel-trace --pmc $PMC -d /tmp/pmc_pass -o run \
-        --output-format csv -- $PMC_CMD > gpurun_out/pmc.log 2>&1 || {
-          echo "[gpu_run] pmc failed"; tail -5 gpurun_out/pmc.log; exit 1; }
-      f=$(find /tmp/pmc_pass -name "*counter_collection.csv" | head -1)
-      python3 scripts/pmc_summary.py "$f" > gpurun_out/pmc_summary.txt
-      cat gpurun_out/pmc_summary.txt ;;
+      # PMC="<counters>" PMC_CMD="<program>" [PMC_FILTER=<kernel regex>] [PMC_NAME=<name>]
+      name=${PMC_NAME:-pmc}
+      filt=()
+      [ -n "$PMC_FILTER" ] && filt=(--kernel-include-regex "$PMC_FILTER")
+      rm -rf /tmp/pmc_$name
+      timeout -s KILL 150 rocprofv3 --pmc $PMC "${filt[@]}" -d /tmp/pmc_$name -o run \
+        --output-format csv -- $PMC_CMD > gpurun_out/$name.log 2>&1 || {
+          echo "[gpu_run] pmc failed"; tail -5 gpurun_out/$name.log; exit 1; }
+      python3 scripts/pmc_summary.py /tmp/pmc_$name gpurun_out/${name}_summary.csv
+      cat gpurun_out/${name}_summary.csv | cut -c1-200 ;;
     rehearse) N=${N:-2} step rehearse 600 bash scripts/gpu_rehearse_multirank.sh ;;
     serialized)
       AMD_SERIALIZE_KERNEL=3 AMD_SERIALIZE_COPY=3 step serialized 900 python -u -m pytest -x -q \

@@ -119,8 +119,11 @@ def resnet50(dev):
     import probe_eig_resnet50 as pr
     ns = pr.sizes()
     mats = [factor(n, dev, i) for i, n in enumerate(ns)]
-    for flag in (0, 1):
+    variants = [(0, 0)] + [(1, c) for c in
+                           [int(x) for x in os.environ.get('TS_COUNTS', '0').split(',')]]
+    for flag, cnt in variants:
         eigen.TWO_STAGE = bool(flag)
+        eigen.TWO_STAGE_COUNT = cnt
         for rep in range(4):
             torch.cuda.synchronize()
             t = time.perf_counter()
@@ -132,8 +135,8 @@ def resnet50(dev):
             Ad = A.double()
             sc = float(d.abs().max())
             worst = max(worst, float((Ad @ Q.double() - Q.double() * d.double()).abs().max()) / sc)
-        print('resnet50 set (%d factors) two_stage=%d: %.1f ms, worst resid (first 12) %.1e' %
-              (len(mats), flag, el, worst), flush=True)
+        print('resnet50 set (%d factors) two_stage=%d count=%d: %.1f ms, worst resid (first 12) '
+              '%.1e' % (len(mats), flag, cnt, el, worst), flush=True)
 
 
 def main():
