@@ -342,7 +342,7 @@ __global__ __launch_bounds__(64 * (NW + 1)) void sb2st_kernel(const SbMat* __res
       float val[SB];
 #pragma unroll
       for (int l = 0; l < SB; ++l) val[l] = *addr[l];
-      asm volatile("s_waitcnt lgkmcnt(16)" : "+v"(xl) :: "memory");
+      asm volatile("s_waitcnt lgkmcnt(15)" : "+v"(xl) :: "memory");   // (4-bit field: x and the first operand)
       const float x = (lane < L) ? xl : 0.f;
       SB2ST_IF { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
       SB2ST_STAMP(2)

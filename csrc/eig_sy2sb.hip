@@ -47,12 +47,11 @@ constexpr int PQ = 10;             // panel columns per thread: m <= PT * PQ
 constexpr int NMAX2 = PT * PQ;       // largest n of the two-stage path (5120; Q2 holds 16 components per thread)
 constexpr int UT = 64;             // update tile
 constexpr int MAXM2 = 64;          // matrices per launch sequence
-constexpr int KS = 4;              // Y stage: K split over workgroups (4x the workgroups of 16-row blocks)
 
 struct SyMat {
   float* A; float* tau; float* band;
   float* Vr;   // SB x lda: reflector rows of the current panel (v[0] = 1 explicit, 0 before)
-  float* X;    // KS x lda x SB: partial Y = A22 V of each K quarter
+  float* X;    // lda x SB
   float* Mp;   // (lda / 16) x 256 partial V^T X
   float* T;    // 16 x 16
   float* N;    // 16 x 16
@@ -67,8 +66,8 @@ SyWs ws_layout(long long lda) {
   SyWs L;
   long long o = 0;
   L.Vr = o; o += a64(SB * lda);
-  L.X = o; o += a64(KS * lda * SB);            // KS partial Y slabs
-  L.Mp = o; o += a64((lda / 16 + 1) * KS * 256);
+  L.X = o; o += a64(lda * SB);
+  L.Mp = o; o += a64((lda / 16 + 1) * 256);
   L.T = o; o += 256;
   L.N = o; o += 256;
   L.total = o;
@@ -242,11 +241,8 @@ __global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 }
 
 // ------------------------------------------------------------------- Y
-// Partial Y = A22 V over one K quarter for 16 rows of A22 per workgroup
-// (exact f32 MFMA 16x16x4; the 4 waves split the quarter again), and its
-// partial V^T Y.  K is split over KS workgroups so that a panel launches
-// KS x m / 16 workgroups (m / 16 alone left most of the 256 CUs idle and each
-// one latency-bound on its row stream); X = Y T is formed by the U stage.
+// X = A22 V T for 16 rows of A22 per workgroup (exact f32 MFMA 16x16x4; the
+// 4 waves take quarters of K), and this block's partial M = V^T X.
 // v_mfma_f32_16x16x4_f32: lane l supplies A[l % 16][l / 16] and
 // B[l / 16][l % 16] and holds D[4 (l / 16) + t][l % 16], t = 0..3.  Each lane
 // loads 4 consecutive k of its row (a float4) and feeds them to 4 MFMAs: the
@@ -255,23 +251,23 @@ __global__ __launch_bounds__(PT) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 __global__ __launch_bounds__(256) void sy2sb_yx_kernel(const SyMat* __restrict__ mats,
                                                        const int* __restrict__ offs, int count,
                                                        int p) {
-  int idx;
-  const SyMat M = mats[find_mat(offs, count, blockIdx.x, &idx)];
-  const int blk = idx / KS, ks = idx % KS;
+  int blk;
+  const SyMat M = mats[find_mat(offs, count, blockIdx.x, &blk)];
   const int n = M.n;
   const long long lda = M.lda;
   const int j0 = p * SB, m = n - j0 - SB;
-  const int nkb = (m + 15) / 16;                  // 16-wide k blocks
+  const int mk = (m + 15) / 16 * 16;
   const int row0 = blk * 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int i = lane & 15, q = lane >> 4;
   __shared__ float sY[4][16][17];
   __shared__ float sYt[16][17];
+  __shared__ float sX[16][17];
+  __shared__ float sTT[16][17];
   const AS1 float* Arow = gptr(M.A) + (long long)(j0 + SB + row0 + i) * lda + j0 + SB;
   const AS1 float* Vrow = gptr(M.Vr) + (long long)i * lda;
-  const int kper = (nkb + KS - 1) / KS, kb0 = ks * kper, kb1 = min(nkb, kb0 + kper);
-  const int wper = (max(kb1 - kb0, 0) + 3) / 4;
-  const int kbeg = (kb0 + wid * wper) * 16, kend = min(kb1, kb0 + (wid + 1) * wper) * 16;
+  const int chunk = ((mk / 16 + 3) / 4) * 16;
+  const int kbeg = wid * chunk, kend = min(mk, kbeg + chunk);
   f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
   int k0 = kbeg;
   // 4 k-steps per iteration: 8 float4 loads in flight before the MFMAs
@@ -300,34 +296,38 @@ __global__ __launch_bounds__(256) void sy2sb_yx_kernel(const SyMat* __restrict__
   }
 #pragma unroll
   for (int t = 0; t < 4; ++t) sY[wid][4 * q + t][i] = acc[t];
+  sTT[tid / 16][tid % 16] = M.T[tid];
   __syncthreads();
   const int r = tid / 16, c = tid % 16;
-  const float y = (sY[0][r][c] + sY[1][r][c]) + (sY[2][r][c] + sY[3][r][c]);
-  sYt[r][c] = y;
-  gptr(M.X)[((long long)ks * lda + row0 + r) * SB + c] = y;
+  sYt[r][c] = sY[0][r][c] + sY[1][r][c] + sY[2][r][c] + sY[3][r][c];
   __syncthreads();
-  // partial (V^T Y)[c][c'] = sum_r V[row0 + r][c] Y[r][c'] (V[k][c] = Vr[c][k])
-  const int cc = tid / 16, c2 = tid % 16;
-  float sacc = 0.f;
+  float x = 0.f;
 #pragma unroll
-  for (int rr = 0; rr < 16; ++rr) sacc += gptr(M.Vr)[(long long)cc * lda + row0 + rr] * sYt[rr][c2];
-  gptr(M.Mp)[(long long)idx * 256 + tid] = sacc;
+  for (int a = 0; a < SB; ++a) x += sYt[r][a] * sTT[a][c];
+  sX[r][c] = x;
+  gptr(M.X)[(long long)(row0 + r) * SB + c] = x;
+  __syncthreads();
+  // partial M[c][c'] = sum_r V[row0 + r][c] X[r][c'] (V[k][c] = Vr[c][k])
+  const int cc = tid / 16, c2 = tid % 16;
+  float s = 0.f;
+#pragma unroll
+  for (int rr = 0; rr < 16; ++rr) s += gptr(M.Vr)[(long long)cc * lda + row0 + rr] * sX[rr][c2];
+  gptr(M.Mp)[(long long)blk * 256 + tid] = s;
 }
 
 // ------------------------------------------------------------------- N
-// N = T^T (V^T Y) T (= T^T V^T X with X = Y T).  1024 threads: quarter `part`
-// of the partials of entry `e`, 8 loads in flight per thread, then a
-// fixed-order combine: deterministic.
+// 1024 threads: quarter `part` of the partials of entry `e`, 8 loads in
+// flight per thread (a serial 288-long sum took 34 us), then a fixed-order
+// combine: deterministic.
 __global__ __launch_bounds__(1024) void sy2sb_n_kernel(const SyMat* __restrict__ mats,
                                                        const int* __restrict__ act, int p) {
   const SyMat M = mats[act[blockIdx.x]];
   const int m = M.n - p * SB - SB;
   if (m < 1) return;
-  const int nblk = (m + 15) / 16 * KS, tid = threadIdx.x;
+  const int nblk = (m + 15) / 16, tid = threadIdx.x;
   const int e = tid & 255, part = tid >> 8;
   __shared__ float sP[4][256];
   __shared__ float sM[16][17];
-  __shared__ float sTM[16][17];
   const AS1 float* Mp = gptr(M.Mp);
   float acc[8];
 #pragma unroll
@@ -343,18 +343,11 @@ __global__ __launch_bounds__(1024) void sy2sb_n_kernel(const SyMat* __restrict__
   __syncthreads();
   if (tid < 256) sM[tid / 16][tid % 16] = (sP[0][tid] + sP[1][tid]) + (sP[2][tid] + sP[3][tid]);
   __syncthreads();
-  const int c = (tid & 255) / 16, c2 = tid % 16;
   if (tid < 256) {
+    const int c = tid / 16, c2 = tid % 16;
     float nn = 0.f;
 #pragma unroll
     for (int a = 0; a < SB; ++a) nn += M.T[a * SB + c] * sM[a][c2];
-    sTM[c][c2] = nn;
-  }
-  __syncthreads();
-  if (tid < 256) {
-    float nn = 0.f;
-#pragma unroll
-    for (int b = 0; b < SB; ++b) nn += sTM[c][b] * M.T[b * SB + c2];
     M.N[tid] = nn;
   }
 }
@@ -385,12 +378,9 @@ __global__ __launch_bounds__(256) void sy2sb_upd_kernel(const SyMat* __restrict_
     old[a] = (row < m && c0 + 3 < m) ? *(const AS1 fx4*)(A + (long long)row * lda + c0) : z4;
   }
   __shared__ float sN[SB][SB + 1];
-  __shared__ float sT[SB][SB + 1];
   __shared__ float sV[2][UT][SB + 1];
-  __shared__ float sY[2][UT][SB + 1];
   __shared__ float sZ[2][UT][SB + 1];
   sN[tid / 16][tid % 16] = M.N[tid];
-  sT[tid / 16][tid % 16] = M.T[tid];
   const AS1 float* Vr = gptr(M.Vr);
   const AS1 float* X = gptr(M.X);
   // V rows of I and J (V[k][c] = Vr[c][k]); 2 x 64 x 16 values, 8 per thread
@@ -401,30 +391,17 @@ __global__ __launch_bounds__(256) void sy2sb_upd_kernel(const SyMat* __restrict_
     const int row = (h ? J0 : I0) + rr;
     sV[h][rr][c] = gld_if(Vr, (long long)c * lda + row, row < m, 0.f);   // rows past m: 0
   }
-  // Y rows: the KS partial slabs summed in slab order
+  __syncthreads();
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int idx = tid + 256 * e;
     const int h = idx >> 10, rem = idx & 1023, rr = rem >> 4, c = rem & 15;
     const int row = (h ? J0 : I0) + rr;
-    float y = 0.f;
+    const float z = gld_if(X, (long long)row * SB + c, row < m, 0.f);
+    float s = 0.f;
 #pragma unroll
-    for (int k = 0; k < KS; ++k) y += gld_if(X, ((long long)k * lda + row) * SB + c, row < m, 0.f);
-    sY[h][rr][c] = y;
-  }
-  __syncthreads();
-  // Zm = X - V N / 2 with X = Y T
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int idx = tid + 256 * e;
-    const int h = idx >> 10, rem = idx & 1023, rr = rem >> 4, c = rem & 15;
-    float x = 0.f, s = 0.f;
-#pragma unroll
-    for (int a = 0; a < SB; ++a) {
-      x += sY[h][rr][a] * sT[a][c];
-      s += sV[h][rr][a] * sN[a][c];
-    }
-    sZ[h][rr][c] = x - 0.5f * s;
+    for (int a = 0; a < SB; ++a) s += sV[h][rr][a] * sN[a][c];
+    sZ[h][rr][c] = z - 0.5f * s;
   }
   __syncthreads();
   float acc[4][4];
@@ -560,7 +537,7 @@ SyPlan* plan_for(const KfacSy2sbRecord* recs, int count, bool capture, int* err)
         if (m < 1) continue;
         act[na] = i;
         oy[na] = accy; ou[na] = accu;
-        accy += (m + 15) / 16 * KS;
+        accy += (m + 15) / 16;
         const int nt = (m + UT - 1) / UT;
         accu += nt * nt;
         ++na;

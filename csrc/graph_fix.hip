@@ -117,3 +117,50 @@ KFAC_API int kfac_graph_fix_memsets(void* graph, int replace, long long* stats) 
   (void)hipGetLastError();
   return e;
 }
+
+// Cross-graph signalling: an event recorded with hipEventRecordExternal while
+// a stream is being captured becomes an external event-record node of that
+// graph, and hipStreamWaitEvent(..., hipEventWaitExternal) an external wait
+// node of another graph, so two graphs replayed on two streams can hand off
+// in the MIDDLE of the first one (torch refuses external events on ROCm).
+KFAC_API void* kfac_event_create() {
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+  return (void*)e;
+}
+KFAC_API int kfac_event_destroy(void* e) { return (int)hipEventDestroy((hipEvent_t)e); }
+// During a capture the node is added by hand after the stream's current
+// capture dependencies (hipEventRecordWithFlags(.., hipEventRecordExternal)
+// returns hipErrorInvalidValue under capture on this ROCm); outside a
+// capture these are the plain record / wait.
+namespace {
+int add_capture_node(hipStream_t s, void* e, bool record, bool* captured) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  hipGraph_t g = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t ndeps = 0;
+  hipError_t r = hipStreamGetCaptureInfo_v2(s, &st, &id, &g, &deps, &ndeps);
+  if (r != hipSuccess) return (int)r;
+  *captured = st == hipStreamCaptureStatusActive;
+  if (!*captured) return 0;
+  hipGraphNode_t node = nullptr;
+  r = record ? hipGraphAddEventRecordNode(&node, g, deps, ndeps, (hipEvent_t)e)
+             : hipGraphAddEventWaitNode(&node, g, deps, ndeps, (hipEvent_t)e);
+  if (r != hipSuccess) return (int)r;
+  return (int)hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies);
+}
+}  // namespace
+
+KFAC_API int kfac_event_record_external(void* e, hipStream_t s) {
+  bool cap = false;
+  const int r = add_capture_node(s, e, true, &cap);
+  if (r || cap) return r;
+  return (int)hipEventRecord((hipEvent_t)e, s);
+}
+KFAC_API int kfac_stream_wait_external(hipStream_t s, void* e) {
+  bool cap = false;
+  const int r = add_capture_node(s, e, false, &cap);
+  if (r || cap) return r;
+  return (int)hipStreamWaitEvent(s, (hipEvent_t)e, 0);
+}

@@ -80,6 +80,10 @@ _SIGS = {
     'kfac_sy2sb_nmax': [],
     'kfac_sb2st_batched': [ctypes.POINTER(Sb2stRecord), c_int, c_int, c_vp],
     'kfac_backtransform_slabs': [c_int],
+    'kfac_event_create': [],
+    'kfac_event_destroy': [c_vp],
+    'kfac_event_record_external': [c_vp, c_vp],
+    'kfac_stream_wait_external': [c_vp, c_vp],
     'kfac_sb2st_debug_stamps': [ctypes.POINTER(ctypes.c_longlong), c_int],
     'kfac_sb2st_debug_phases': [ctypes.POINTER(ctypes.c_longlong)],
     'kfac_q2_batched': [ctypes.POINTER(Q2Record), c_int, c_int, c_vp],
@@ -153,7 +157,7 @@ _RESTYPES = {'kfac_dc_ws_bytes': c_ll, 'kfac_sy2sb_ws_floats': c_ll,
              'kfac_reduce_ws_floats': c_ll, 'kfac_syrk_splits': c_ll,
              'kfac_chol_ws_bytes': c_ll, 'kfac_chol_info_offset': c_ll,
              'kfac_syrk_problem_set_part': None, 'kfac_syrk_problem_set_dscale': None,
-             'kfac_bn_ws_floats': c_ll}
+             'kfac_bn_ws_floats': c_ll, 'kfac_event_create': c_vp}
 
 
 def _load():
@@ -268,3 +272,33 @@ def workspace(device, numel, dtype=torch.float32, tag='main'):
         buf = torch.empty(max(numel, 1), dtype=dtype, device=device)
         _ws[key] = buf
     return buf[:numel]
+
+
+class ExternalEvent(object):
+    """A HIP event usable ACROSS captured graphs: record() during a capture
+    becomes an external event-record node of that graph, wait() during
+    another capture an external wait node, so graph B replayed on a second
+    stream starts when graph A passes the record point (torch.cuda.Event
+    refuses `external=True` on ROCm)."""
+
+    def __init__(self):
+        self.handle = lib().kfac_event_create()
+        if not self.handle:
+            raise RuntimeError('hipEventCreateWithFlags failed')
+
+    def record(self, stream=None):
+        s = stream if stream is not None else torch.cuda.current_stream()
+        check(lib().kfac_event_record_external(c_vp(self.handle), c_vp(s.cuda_stream)),
+              'kfac_event_record_external')
+
+    def wait(self, stream=None):
+        s = stream if stream is not None else torch.cuda.current_stream()
+        check(lib().kfac_stream_wait_external(c_vp(s.cuda_stream), c_vp(self.handle)),
+              'kfac_stream_wait_external')
+
+    def __del__(self):
+        try:
+            if self.handle and _lib is not None:
+                _lib.kfac_event_destroy(c_vp(self.handle))
+        except Exception:  # pragma: no cover - interpreter shutdown
+            pass

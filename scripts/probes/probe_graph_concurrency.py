@@ -7,7 +7,13 @@ graph serialise.)
 """
 import time
 
+import os
+import sys
+
 import torch
+
+sys.path.insert(0, os.getcwd())
+from distributed_kfac_pytorch_amd.ops import _lib  # noqa: E402
 
 
 def work(x, n):
@@ -19,10 +25,12 @@ def work(x, n):
 def main():
     dev = torch.device('cuda')
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
-    a = torch.randn(8 << 20, device=dev)
-    b = torch.randn(8 << 20, device=dev)
-    ev_mid = torch.cuda.Event(external=True)
-    ev_done = torch.cuda.Event(external=True)
+    # small tensors: latency-bound kernels that leave most CUs idle (a
+    # bandwidth-bound chain fills the GPU alone and cannot show overlap)
+    a = torch.randn(1 << 14, device=dev)
+    b = torch.randn(1 << 14, device=dev)
+    ev_mid = _lib.ExternalEvent()
+    ev_done = _lib.ExternalEvent()
     # warm up
     for st in (s1, s2):
         with torch.cuda.stream(st):
@@ -34,9 +42,12 @@ def main():
         ev_mid.record()
         za = work(ya, 40)
     with torch.cuda.graph(gb, stream=s2):
-        torch.cuda.current_stream().wait_event(ev_mid)
+        ev_mid.wait()
         yb = work(b, 80)
         ev_done.record()
+    gb2 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gb2, stream=s2):
+        yb2 = work(b, 80)
     torch.cuda.synchronize()
 
     def timed(fn, reps=5):
@@ -64,8 +75,24 @@ def main():
             ga.replay()
         with torch.cuda.stream(s2):
             gb.replay()
-        s1.wait_event(ev_done)
+        ev_done.wait(s1)
 
+    def both_nogate():
+        with torch.cuda.stream(s1):
+            ga.replay()
+        with torch.cuda.stream(s2):
+            gb2.replay()
+        s1.wait_stream(s2)
+
+    def eager_both():
+        with torch.cuda.stream(s1):
+            work(a, 80)
+        with torch.cuda.stream(s2):
+            work(b, 80)
+        s1.wait_stream(s2)
+
+    print('A || B without the gate %.2f ms; the same kernels eagerly on two streams %.2f ms' % (
+        timed(both_nogate), timed(eager_both)), flush=True)
     ta = timed(only_a)
     tseq = timed(only_b_after_a)
     tcon = timed(both)
