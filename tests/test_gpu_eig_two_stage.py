@@ -1,0 +1,66 @@
+"""The opt-in two-stage symmetric eigensolver (ops/eigen.py two_stage_eigh:
+csrc/eig_sy2sb.hip dense -> band, csrc/eig_sb2st.hip bulge chasing,
+csrc/eig_dc.hip divide and conquer, csrc/eig_q2.hip + the shift-16 compact-WY
+back-transformations) against fp64 torch references; fp64 model of the same
+operation order: scripts/models/two_stage_model.py.  Reference semantics:
+kfac/layers/utils.py:45-74 (ascending eigenvalues, eigenvectors in columns)."""
+import pytest
+import torch
+
+from distributed_kfac_pytorch_amd.ops import eigen
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def _factor(n, seed):
+    """K-FAC-like: decayed identity + low-rank data (clustered small eigenvalues)."""
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    x = torch.randn(n, max(8, n // 3), device=DEV, dtype=torch.float64, generator=g)
+    return 0.3 * torch.eye(n, device=DEV, dtype=torch.float64) + x @ x.t() / x.shape[1]
+
+
+def _check(A64, Q, d, tol_res=2e-5, tol_orth=1e-4, tol_lam=1e-5):
+    n = A64.shape[0]
+    Q64, d64 = Q.double(), d.double()
+    ref = torch.linalg.eigvalsh(A64)
+    an = ref.abs().max().item()
+    res = ((A64 @ Q64 - Q64 * d64).norm() / (an * n ** 0.5)).item()
+    orth = (Q64.t() @ Q64 - torch.eye(n, device=DEV, dtype=torch.float64)).abs().max().item()
+    lam = ((d64 - ref.clamp(min=0)).abs().max() / an).item()
+    assert bool((d[1:] >= d[:-1]).all()), 'eigenvalues not ascending'
+    assert res <= tol_res and orth <= tol_orth and lam <= tol_lam, (n, res, orth, lam)
+
+
+@pytest.mark.parametrize('sizes', [[33], [200, 200], [1000, 577, 64], [2304]])
+def test_two_stage_matches_fp64(sizes):
+    mats64 = [_factor(n, 11 + i) for i, n in enumerate(sizes)]
+    for use_graph in (False, True):
+        outs = eigen.two_stage_eigh([m.float() for m in mats64], use_graph=use_graph)
+        torch.cuda.synchronize()
+        for A64, (Q, d) in zip(mats64, outs):
+            _check(A64, Q, d)
+
+
+def test_two_stage_4608():
+    """ResNet-50's largest factor size."""
+    A64 = _factor(4608, 5)
+    (Q, d), = eigen.two_stage_eigh([A64.float()])
+    torch.cuda.synchronize()
+    _check(A64, Q, d)
+
+
+def test_two_stage_routing(monkeypatch):
+    """symeig_many with KFAC_EIG_TWO_STAGE routing: the largest eligible
+    factor on the two-stage path (side stream), the rest one-stage, results in
+    the caller's order."""
+    monkeypatch.setattr(eigen, 'TWO_STAGE', True)
+    monkeypatch.setattr(eigen, 'TWO_STAGE_MIN', 256)
+    monkeypatch.setattr(eigen, 'TWO_STAGE_COUNT', 1)
+    sizes = [300, 64, 1000, 500]
+    mats64 = [_factor(n, 31 + i) for i, n in enumerate(sizes)]
+    outs = eigen.symeig_many([m.float() for m in mats64])
+    torch.cuda.synchronize()
+    for A64, (Q, d) in zip(mats64, outs):
+        assert Q.shape == A64.shape
+        _check(A64, Q, d)
