@@ -506,18 +506,30 @@ __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int 
       rtab[(k & 1) * VB + (j ^ ((j >> 3) & 7))] = e;
     }
   };
+  // every row-table read first (one LDS wait), then branch-free integer
+  // address selects, then the loads back to back (a pointer ?: per load
+  // compiled to a divergent branch with an LDS read and a full lgkmcnt wait
+  // inside it: eight serial LDS round trips per k-step before the loads)
   auto load_step = [&](int k, u32x4_t (&dst)[RG][8]) {
     const int4* rt = rtab + (k & 1) * VB;
+    int4 ev[RG][8];
+#pragma unroll
+    for (int g = 0; g < RG; ++g)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) ev[g][q] = rt[g * 64 + rg * 8 + (q ^ rg)];
+    const unsigned long long xb = (unsigned long long)(size_t)(x + coff);
+    const unsigned long long pz = (unsigned long long)(size_t)zeros;
+    const unsigned long long pa = (unsigned long long)(size_t)alt;
 #pragma unroll
     for (int g = 0; g < RG; ++g) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const int4 e = rt[g * 64 + rg * 8 + (q ^ rg)];
+        const int4 e = ev[g][q];
         const long long off = ((long long)e.y << 32) | (unsigned)e.x;
         const bool in = ((unsigned)(e.z + di) < (unsigned)p.H) & ((unsigned)(e.w + dj) < (unsigned)p.W);
-        const AS1 u32x4_t* src = in ? (const AS1 u32x4_t*)(x + off + coff)
-                                    : (e.z != ROW_NONE ? alt : zeros);
-        dst[g][q] = *src;
+        const unsigned long long pin = xb + (unsigned long long)(off * 2);
+        const unsigned long long pout = (e.z != ROW_NONE) ? pa : pz;
+        dst[g][q] = *(const AS1 u32x4_t*)(size_t)(in ? pin : pout);
       }
     }
   };
