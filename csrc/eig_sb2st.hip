@@ -203,10 +203,12 @@ __global__ __launch_bounds__(64 * (NW + 1)) void sb2st_kernel(const SbMat* __res
   const bool polling = prev && !(M.dbg & 1);
   // producer blocks (previous group's last sweep s0 - 1) that block k of
   // wave 0's sweep needs: rows s0+1+16k .. min(s0+16+16k, n-1)
+  // (a block past the band's end still needs every producer block up to the
+  // last row: returning 0 there let the prologue, which asks for block PD-1,
+  // skip the wait on small matrices and read stale rows)
   auto need_of = [&](int k) {
-    const int rlo = s0 + 1 + SB * k;
-    if (rlo > n - 1) return 0;
     const int rhi = min(s0 + SB + SB * k, n - 1);
+    if (rhi < s0 + 1) return 0;
     return (rhi - s0) / SB + 1;
   };
   // IO wave: block k of wave 0's sweep (rows s0+1+16k ..: 2 KB contiguous in
