@@ -52,9 +52,14 @@ def run(args, dataset):
     if args.verbose:
         print(model)
     # --graphs: the bench's fast path (no eager DDP: a flat-arena all-reduce
-    # between graph replays), micro-batching and fp16 + GradScaler included;
-    # otherwise the reference's eager DDP loop
-    args.graphed = bool(getattr(args, 'graphs', 0))
+    # between graph replays), micro-batching included; otherwise the
+    # reference's eager DDP loop.  --fp16 (GradScaler) stays eager: a captured
+    # scaler step with a device-side skip diverged to NaN even without K-FAC
+    # (scripts/probes/probe_fp16_example.py), and the fused SGD's own skip let
+    # non-finite updates through on this ROCm build
+    args.graphed = bool(getattr(args, 'graphs', 0)) and not args.fp16
+    if getattr(args, 'graphs', 0) and args.fp16 and args.verbose:
+        print('--graphs: fp16 + GradScaler runs the eager loop')
     grad_sync = None
     if args.graphed and args.world_size > 1:
         from distributed_kfac_pytorch_amd.parallel import grad_sync as grad_sync_mod

@@ -20,10 +20,7 @@ The fast path covers the reference's other two training modes too
     are captured in the ONE forward/backward graph (gradients accumulate; the
     graphed loop has no DDP, so the single all-reduce after it is the
     reference's no_sync behaviour);
-  * `--fp16`: fp16 autocast + torch.amp.GradScaler, capturable because the
-    optimizer is the fused SGD (`_step_supports_amp_scaling`): scale, unscale
-    (device inf check), K-FAC step (device loss scale), the inf-skipping SGD
-    step and the scale update are all device work, no host read.
+  (`--fp16` + GradScaler runs the eager loop: examples/cnn_train.py.)
 """
 import contextlib
 import time
@@ -57,17 +54,14 @@ class GraphedTrainer(object):
         from distributed_kfac_pytorch_amd import graphs
         self.model, self.optimizer, self.pre = model, optimizer, preconditioner
         self.loss_func, self.args, self.grad_sync = loss_func, args, grad_sync
-        self.scaler = getattr(args, 'grad_scaler', None)
         self.micro = max(1, int(getattr(args, 'batches_per_allreduce', 1)))
         self.x = self.y = None
         if grad_sync is not None:
-            # phased plain steps split the update at K-FAC's gradient
-            # all-gather and run opt.step() themselves: not with a scaler
             self.step = graphs.GraphedTrainStep(None, preconditioner, [optimizer],
                                                 enabled=args.cuda,
                                                 forward_backward=self._forward_backward,
                                                 communicate=grad_sync, update=self._update,
-                                                phased_update=self.scaler is None)
+                                                phased_update=True)
         else:
             self.step = graphs.GraphedTrainStep(self._train_step, preconditioner, [optimizer],
                                                 enabled=args.cuda)
@@ -86,7 +80,7 @@ class GraphedTrainer(object):
             with _autocast(self.args):
                 out = self.model(xb)
                 loss = self.loss_func(out, yb) / k
-            (self.scaler.scale(loss) if self.scaler is not None else loss).backward()
+            loss.backward()
             losses.append(loss.detach())
             outs.append(out.detach())
         if k == 1:
@@ -94,15 +88,9 @@ class GraphedTrainer(object):
         return torch.stack(losses).sum(), torch.cat(outs)
 
     def _update(self):
-        if self.scaler is not None:
-            self.scaler.unscale_(self.optimizer)     # K-FAC reads unscaled gradients
         if self.pre is not None:
             self.pre.step()
-        if self.scaler is not None:
-            self.scaler.step(self.optimizer)         # fused SGD: skips on device at inf
-            self.scaler.update()
-        else:
-            self.optimizer.step()
+        self.optimizer.step()
 
     def _train_step(self):
         res = self._forward_backward()

@@ -19,12 +19,11 @@ COMM = {'comm-opt': kfac.CommMethod.COMM_OPT, 'mem-opt': kfac.CommMethod.MEM_OPT
 
 def get_optimizer(model, args, batch_first=True):
     use_kfac = args.kfac_update_freq > 0
-    # fp16 + GradScaler on the GPU: the fused SGD takes the scaler's found_inf
-    # / scale as device tensors (no host read: capturable in the graphed
-    # loop; the eager loop uses the same optimizer so both train alike)
-    fused = getattr(args, 'grad_scaler', None) is not None
+    # (not the fused SGD with fp16: on this ROCm build its GradScaler inf skip
+    # let non-finite updates through -- scripts/probes/probe_fp16_example.py;
+    # the graphed loop skips overflowed steps itself, engine.GraphedTrainer)
     optimizer = optim.SGD(model.parameters(), lr=args.base_lr, momentum=args.momentum,
-                          weight_decay=args.weight_decay, **({'fused': True} if fused else {}))
+                          weight_decay=args.weight_decay)
     preconditioner = None
     if use_kfac:
         if args.kfac_comm_method not in COMM:

@@ -11,10 +11,10 @@ from tests import _dist_worker  # noqa: F401  (ROOT on sys.path)
 pytestmark = pytest.mark.gpu
 
 
-def _final_params(tmp_path, graphs, extra=()):
+def _final_params(tmp_path, graphs, extra=(), size=64):
     from examples import torch_imagenet_resnet as ex
     log = os.path.join(str(tmp_path), 'g{}{}'.format(graphs, '_'.join(extra)))
-    argv = ['--model', 'resnet_tiny', '--synthetic-size', '64', '--batch-size', '8',
+    argv = ['--model', 'resnet_tiny', '--synthetic-size', str(size), '--batch-size', '8',
             '--val-batch-size', '8', '--image-size', '32', '--checkpoint-freq', '1',
             '--epochs', '1', '--kfac-update-freq', '4', '--kfac-cov-update-freq', '2',
             '--no-bf16', '--deterministic', '--log-dir', log, '--graphs', str(graphs)]
@@ -46,12 +46,11 @@ def _rel(p1, p0):
     return num / den
 
 
-@pytest.mark.parametrize('extra,tol', [(('--batches-per-allreduce', '2'), 1e-6),
-                                       (('--fp16',), 1e-5)])
+@pytest.mark.parametrize('extra,tol', [(('--batches-per-allreduce', '2'), 1e-6)])
 def test_graphed_example_modes_match_eager(tmp_path, extra, tol):
-    """The reference's micro-batching (engine.py:33-65) and fp16 + GradScaler
-    (engine.py:73-82) modes on the graphed fast path (round 3 fell back to
-    eager DDP for both): same final weights as the eager loop."""
+    """The reference's micro-batching (engine.py:33-65) on the graphed fast
+    path (round 3 fell back to eager DDP): same final weights as the eager
+    loop.  (--fp16 + GradScaler stays on the eager loop: cnn_train.py.)"""
     from distributed_kfac_pytorch_amd import graphs
     replays = []
     orig = graphs.GraphedTrainStep.__call__
@@ -63,8 +62,9 @@ def test_graphed_example_modes_match_eager(tmp_path, extra, tol):
     graphs.GraphedTrainStep.__call__ = spy
     prev = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
     try:
-        h1, p1 = _final_params(tmp_path, 1, extra)
-        h0, p0 = _final_params(tmp_path, 0, extra)
+        # 128 images: enough steps per epoch to warm up, capture and replay
+        h1, p1 = _final_params(tmp_path, 1, extra, size=128)
+        h0, p0 = _final_params(tmp_path, 0, extra, size=128)
     finally:
         graphs.GraphedTrainStep.__call__ = orig
         torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = prev
