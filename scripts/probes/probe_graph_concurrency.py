@@ -48,6 +48,19 @@ def main():
     gb2 = torch.cuda.CUDAGraph()
     with torch.cuda.graph(gb2, stream=s2):
         yb2 = work(b, 80)
+    # ONE graph with a forked branch (fork onto s3, join) vs the same kernels
+    # in one linear capture
+    s3 = torch.cuda.Stream()
+    gf, gl = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gf, stream=s1):
+        s3.wait_stream(s1)
+        with torch.cuda.stream(s3):
+            yf2 = work(b, 80)
+        yf1 = work(a, 80)
+        s1.wait_stream(s3)
+    with torch.cuda.graph(gl, stream=s1):
+        yl2 = work(b, 80)
+        yl1 = work(a, 80)
     torch.cuda.synchronize()
 
     def timed(fn, reps=5):
@@ -91,6 +104,18 @@ def main():
             work(b, 80)
         s1.wait_stream(s2)
 
+    def forked():
+        with torch.cuda.stream(s1):
+            gf.replay()
+
+    def linear():
+        with torch.cuda.stream(s1):
+            gl.replay()
+
+    print('one graph, forked branch %.2f ms; one graph, linear %.2f ms  (env %s)' % (
+        timed(forked), timed(linear),
+        {k: v for k, v in os.environ.items() if k.startswith(('DEBUG_HIP', 'DEBUG_CLR'))}),
+        flush=True)
     print('A || B without the gate %.2f ms; the same kernels eagerly on two streams %.2f ms' % (
         timed(both_nogate), timed(eager_both)), flush=True)
     ta = timed(only_a)

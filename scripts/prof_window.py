@@ -100,6 +100,17 @@ def main():
         print('[%s]' % c)
         for n, d in names[c].most_common(4):
             print('   %9.2f ms  %s' % (d, n))
+    # every kernel: total, launches per step, mean duration
+    kt = collections.Counter()
+    kc = collections.Counter()
+    for r in win:
+        n = r['Kernel_Name'][:90]
+        kt[n] += (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e6
+        kc[n] += 1
+    print()
+    print('%9s %9s %8s  %s' % ('ms/step', 'calls/st', 'us/call', 'kernel'))
+    for n, d in kt.most_common(40):
+        print('%9.3f %9.1f %8.2f  %s' % (d / steps, kc[n] / steps, 1e3 * d / kc[n], n))
 
 
 if __name__ == '__main__':
