@@ -206,9 +206,25 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
     offb[q] = ((unsigned)(okb[q] ? n0 + row : n0) * (unsigned)ldb + kof) * ESZ;
   }
   const u32x4n z4 = {0u, 0u, 0u, 0u};
+  // X6F: buffer loads -- the per-thread byte offset stays in one VGPR and the
+  // k-step advances the scalar soffset: no 64-bit address rebuilt per load
+  // (operands < 4 GiB, checked on the host)
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned char*>((const unsigned char*)P.a_hi), 0, -1, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned char*>((const unsigned char*)P.b_hi), 0, -1, 0x00020000);
   auto load = [&](int k0, auto setc) {
     constexpr int SET = decltype(setc)::value;
     const long long kb = (long long)k0 * ESZ;
+    if constexpr (X6F) {
+#pragma unroll
+      for (int q = 0; q < QA; ++q)
+        ra[SET][q] = __builtin_amdgcn_raw_buffer_load_b128(rsA, (int)offa[q], (int)kb, 0);
+#pragma unroll
+      for (int q = 0; q < QB; ++q)
+        rb[SET][q] = __builtin_amdgcn_raw_buffer_load_b128(rsB, (int)offb[q], (int)kb, 0);
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
       const int plane = PLANE_CT ? NT * q / (BM * CPR) : (tid + NT * q) / (BM * CPR);
@@ -326,24 +342,27 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
 #pragma unroll
           for (int p = 0; p < 3; ++p) bp[p][j] = *(const bf16x8_t*)(sB0 + p * BN * LDB16 + off);
         }
+        bf16x8_t ap[3][MI];
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           const int row = arow0 + i * 32 + lr;
           const int off = row * LDB16 + (X6F ? x6f_off(row, kk * 16 + lh * 8) : kk * 16 + lh * 8);
-          bf16x8_t ap[3];
 #pragma unroll
-          for (int p = 0; p < 3; ++p) ap[p] = *(const bf16x8_t*)(sA0 + p * BM * LDB16 + off);
-          // smallest terms first: lo.hi, hi.lo, mid.mid, mid.hi, hi.mid, hi.hi
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[2], bp[0][j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[0], bp[2][j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[1], bp[1][j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[1], bp[0][j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[0], bp[1][j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[0], bp[0][j], acc[i][j], 0, 0, 0);
-          }
+          for (int p = 0; p < 3; ++p) ap[p][i] = *(const bf16x8_t*)(sA0 + p * BM * LDB16 + off);
         }
+        // smallest terms first: lo.hi, hi.lo, mid.mid, mid.hi, hi.mid, hi.hi;
+        // term-major over the MI x NJ accumulators: consecutive MFMAs are
+        // independent (a dependent chain waits out each MFMA's latency).  Per
+        // accumulator the order is unchanged.
+        constexpr int TA[6] = {2, 0, 1, 1, 0, 0}, TB[6] = {0, 2, 1, 0, 1, 0};
+#pragma unroll
+        for (int t = 0; t < 6; ++t)
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[TA[t]][i], bp[TB[t]][j],
+                                                                  acc[i][j], 0, 0, 0);
       }
     } else {
       // Fragments are read 8 bytes at a time: lane half lh covers k in
