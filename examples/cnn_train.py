@@ -52,14 +52,10 @@ def run(args, dataset):
     if args.verbose:
         print(model)
     # --graphs: the bench's fast path (no eager DDP: a flat-arena all-reduce
-    # between graph replays), micro-batching included; otherwise the
-    # reference's eager DDP loop.  --fp16 (GradScaler) stays eager: a captured
-    # scaler step with a device-side skip diverged to NaN even without K-FAC
-    # (scripts/probes/probe_fp16_example.py), and the fused SGD's own skip let
-    # non-finite updates through on this ROCm build
-    args.graphed = bool(getattr(args, 'graphs', 0)) and not args.fp16
-    if getattr(args, 'graphs', 0) and args.fp16 and args.verbose:
-        print('--graphs: fp16 + GradScaler runs the eager loop')
+    # between graph replays), micro-batching and fp16 + GradScaler included
+    # (amp.CapturableGradScaler: the overflow skip stays on the device);
+    # otherwise the reference's eager DDP loop
+    args.graphed = bool(getattr(args, 'graphs', 0))
     grad_sync = None
     if args.graphed and args.world_size > 1:
         from distributed_kfac_pytorch_amd.parallel import grad_sync as grad_sync_mod
@@ -70,7 +66,10 @@ def run(args, dataset):
     # LR scales with the number of workers and micro-batches (reference)
     args.base_lr = args.base_lr * args.world_size * args.batches_per_allreduce
     if args.fp16 and args.cuda:
-        args.grad_scaler = torch.amp.GradScaler('cuda')
+        # a GradScaler (the eager loop uses its standard API) whose unscale /
+        # step / update the graphed loop can capture
+        from distributed_kfac_pytorch_amd.amp import CapturableGradScaler
+        args.grad_scaler = CapturableGradScaler('cuda')
     optimizer, preconditioner, lr_schedules = optimizers.get_optimizer(model, args)
     loss_func = LabelSmoothLoss(args.label_smoothing) if args.label_smoothing > 0 \
         else torch.nn.CrossEntropyLoss()

@@ -61,8 +61,9 @@ def base_parser(desc, d):
                         '(graphs.GraphedTrainStep), the data-parallel gradient all-reduce as one '
                         'flat-arena RCCL call between graph replays (parallel/grad_sync.py) '
                         'instead of eager DDP, K-FAC factors computed inside the captured hooks; '
-                        'needs --batches-per-allreduce 1 and no --fp16 (falls back to eager '
-                        'otherwise)')
+                        'micro-batches (--batches-per-allreduce) are captured in the one '
+                        'forward/backward graph, --fp16 uses amp.CapturableGradScaler '
+                        '(overflow skip on the device)')
     p.add_argument('--deterministic', action='store_true',
                    help='deterministic MIOpen algorithms (cudnn.deterministic, no autotuning)')
     p.add_argument('--backend', default=None, help='torch.distributed backend (nccl = RCCL)')

@@ -20,7 +20,11 @@ The fast path covers the reference's other two training modes too
     are captured in the ONE forward/backward graph (gradients accumulate; the
     graphed loop has no DDP, so the single all-reduce after it is the
     reference's no_sync behaviour);
-  (`--fp16` + GradScaler runs the eager loop: examples/cnn_train.py.)
+  * `--fp16`: the loss is scaled by the GradScaler's device scale inside the
+    graph, and the update is unscale -> K-FAC -> SGD step -> scale update with
+    every overflow decision on the device (distributed_kfac_pytorch_amd/amp.py
+    CapturableGradScaler: op for op GradScaler + SGD, a skipped step selected
+    away with torch.where).
 """
 import contextlib
 import time
@@ -55,13 +59,18 @@ class GraphedTrainer(object):
         self.model, self.optimizer, self.pre = model, optimizer, preconditioner
         self.loss_func, self.args, self.grad_sync = loss_func, args, grad_sync
         self.micro = max(1, int(getattr(args, 'batches_per_allreduce', 1)))
+        self.scaler = getattr(args, 'grad_scaler', None)
+        if self.scaler is not None and not hasattr(self.scaler, 'step_graphable'):
+            raise TypeError('the graphed loop needs amp.CapturableGradScaler')
         self.x = self.y = None
         if grad_sync is not None:
+            # (a phased update would run optimizer.step() without the scaler:
+            # with fp16 a kind whose update communicates runs it eagerly)
             self.step = graphs.GraphedTrainStep(None, preconditioner, [optimizer],
                                                 enabled=args.cuda,
                                                 forward_backward=self._forward_backward,
                                                 communicate=grad_sync, update=self._update,
-                                                phased_update=True)
+                                                phased_update=self.scaler is None)
         else:
             self.step = graphs.GraphedTrainStep(self._train_step, preconditioner, [optimizer],
                                                 enabled=args.cuda)
@@ -80,7 +89,10 @@ class GraphedTrainer(object):
             with _autocast(self.args):
                 out = self.model(xb)
                 loss = self.loss_func(out, yb) / k
-            loss.backward()
+            if self.scaler is not None:
+                self.scaler.scale(loss).backward()
+            else:
+                loss.backward()
             losses.append(loss.detach())
             outs.append(out.detach())
         if k == 1:
@@ -88,9 +100,16 @@ class GraphedTrainer(object):
         return torch.stack(losses).sum(), torch.cat(outs)
 
     def _update(self):
+        sc = self.scaler
+        if sc is not None:
+            sc.unscale_graphable(self.optimizer)
         if self.pre is not None:
             self.pre.step()
-        self.optimizer.step()
+        if sc is not None:
+            sc.step_graphable(self.optimizer)
+            sc.update_graphable()
+        else:
+            self.optimizer.step()
 
     def _train_step(self):
         res = self._forward_backward()

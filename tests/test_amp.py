@@ -1,0 +1,69 @@
+"""CapturableGradScaler (distributed_kfac_pytorch_amd/amp.py) against
+torch.amp.GradScaler + torch.optim.SGD, bitwise, on the CPU: the same
+parameters, momentum buffers and loss scale after a sequence of steps that
+includes overflowed (skipped) ones.  Reference semantics: the fp16 +
+GradScaler loop of examples/cnn_utils/engine.py:73-82."""
+import pytest
+import torch
+
+from distributed_kfac_pytorch_amd.amp import CapturableGradScaler
+
+
+def _setup(nesterov, wd):
+    torch.manual_seed(0)
+    ps = [torch.randn(7, 5), torch.randn(5), torch.randn(3, 4, 2)]
+    pa = [p.clone().requires_grad_(True) for p in ps]
+    pb = [p.clone().requires_grad_(True) for p in ps]
+    kw = dict(lr=0.05, momentum=0.9, weight_decay=wd, nesterov=nesterov)
+    return pa, pb, torch.optim.SGD(pa, **kw), torch.optim.SGD(pb, **kw)
+
+
+@pytest.mark.parametrize('nesterov,wd', [(False, 1e-4), (True, 0.0), (False, 0.0)])
+def test_capturable_scaler_matches_gradscaler(nesterov, wd):
+    pa, pb, oa, ob = _setup(nesterov, wd)
+    kw = dict(init_scale=2.0 ** 10, growth_interval=2, growth_factor=2.0, backoff_factor=0.5)
+    sa = torch.amp.GradScaler('cpu', **kw)
+    sb = CapturableGradScaler('cpu', **kw)
+    one = torch.tensor(1.0)
+    sa.scale(one)
+    sb.scale(one)
+    g = torch.Generator().manual_seed(1)
+    skipped = 0
+    for step in range(9):
+        bad = step in (0, 4, 5)          # overflow on the first step too (no momentum yet)
+        scale = float(sa.get_scale())
+        assert scale == float(sb.get_scale())
+        for a, b in zip(pa, pb):
+            gt = torch.randn(a.shape, generator=g) * scale
+            if bad:
+                gt.view(-1)[0] = float('inf') if step != 5 else float('nan')
+            a.grad = gt.clone()
+            b.grad = gt.clone()
+        sa.unscale_(oa)
+        sa.step(oa)
+        sa.update()
+        sb.unscale_graphable(ob)
+        sb.step_graphable(ob)
+        sb.update_graphable()
+        skipped += bad
+        for a, b in zip(pa, pb):
+            assert torch.equal(a, b), step
+            ma = oa.state[a].get('momentum_buffer')
+            mb = ob.state[b].get('momentum_buffer')
+            if ma is not None:
+                assert torch.equal(ma, mb), step
+            else:
+                assert mb is None or not mb.any()
+        assert torch.equal(sa._scale, sb._scale) and torch.equal(sa._growth_tracker,
+                                                                  sb._growth_tracker)
+    assert skipped == 3
+    assert all(torch.isfinite(p).all() for p in pb)
+
+
+def test_capturable_scaler_rejects_other_optimizers():
+    p = torch.zeros(3, requires_grad=True)
+    p.grad = torch.ones(3)
+    s = CapturableGradScaler('cpu')
+    s.scale(torch.tensor(1.0))
+    with pytest.raises(TypeError):
+        s.step_graphable(torch.optim.Adam([p]))

@@ -46,11 +46,14 @@ def _rel(p1, p0):
     return num / den
 
 
-@pytest.mark.parametrize('extra,tol', [(('--batches-per-allreduce', '2'), 1e-6)])
+@pytest.mark.parametrize('extra,tol', [(('--batches-per-allreduce', '2'), 1e-6),
+                                       (('--fp16',), 1e-6),
+                                       (('--fp16', '--batches-per-allreduce', '2'), 1e-6)])
 def test_graphed_example_modes_match_eager(tmp_path, extra, tol):
-    """The reference's micro-batching (engine.py:33-65) on the graphed fast
-    path (round 3 fell back to eager DDP): same final weights as the eager
-    loop.  (--fp16 + GradScaler stays on the eager loop: cnn_train.py.)"""
+    """The reference's micro-batching (engine.py:33-65) and fp16 + GradScaler
+    (engine.py:73-82) on the graphed fast path (round 3 fell back to eager
+    DDP for both): same final weights as the eager loop (torch GradScaler
+    API there, amp.CapturableGradScaler's device-side skip when graphed)."""
     from distributed_kfac_pytorch_amd import graphs
     replays = []
     orig = graphs.GraphedTrainStep.__call__
