@@ -341,7 +341,9 @@ def _fused_group(mats, clip, stream, use_graph, slot=0):
 # the other streams.
 TWO_STAGE = bool(int(os.environ.get('KFAC_EIG_TWO_STAGE', '0')))
 TWO_STAGE_MIN = int(os.environ.get('KFAC_EIG_TWO_STAGE_MIN', '1024'))
-TWO_STAGE_MAX = 5120     # csrc/eig_sy2sb.hip NMAX2, csrc/eig_q2.hip 16 x QT
+# largest size csrc/eig_sy2sb.hip (NMAX2) and csrc/eig_q2.hip (16 x QT) take;
+# KFAC_EIG_TWO_STAGE_MAX lowers the eligible range (e.g. a middle size class)
+TWO_STAGE_MAX = min(5120, int(os.environ.get('KFAC_EIG_TWO_STAGE_MAX', '5120')))
 # at most this many eligible factors (largest first) take the two-stage path
 # (0 = all): the two paths run concurrently on two streams, so moving only
 # part of the largest size class shortens the one-stage critical path
