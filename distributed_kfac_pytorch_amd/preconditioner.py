@@ -487,16 +487,18 @@ class KFAC(optim.Optimizer):
         return torch.autocast(device_type=t.device.type, enabled=False)
 
     def _count_forward(self, module):
-        """Forward passes per step, counted at the first K-FAC layer's hook:
-        early_factors launches the A update from a step's FIRST backward,
-        which is the step() result only with one forward/backward per step
-        (several micro-batches apply the EMA from the last one)."""
+        """Forward passes per step, counted at the first K-FAC layer's hook
+        and closed by step() (_close_forward_count): early_factors launches the
+        A update from a step's FIRST backward, which is the step() result only
+        with one forward/backward per step (several micro-batches apply the
+        EMA from the last one).  Counting between step() calls, not per value
+        of the step counter, keeps callers that rewind the counter
+        (GraphedTrainStep.prepare, a bench restarting its window) from
+        looking like micro-batching."""
         if not self.layers or module is not self.layers[0].module:
             return
         st = self.param_groups[0]['step']
-        if self._fwd_step != st:
-            self._prev_fwd_calls = self._fwd_calls if self._fwd_step is not None else None
-            self._fwd_step, self._fwd_calls = st, 0
+        self._fwd_step = st
         self._fwd_calls += 1
         if self._fwd_calls > 1 and self._early_a_step == st:
             # the pattern changed under an early launch: this step's A got
@@ -504,6 +506,12 @@ class KFAC(optim.Optimizer):
             warnings.warn('K-FAC early_factors: several forward passes in one step (micro-'
                           'batching); early A-factor launches disabled')
             self.early_factors = False
+
+    def _close_forward_count(self):
+        """End of a step (step() / step_finish()): this step's forward count
+        becomes the previous one."""
+        self._prev_fwd_calls = self._fwd_calls
+        self._fwd_calls = 0
 
     def _forward_hook(self, module, input, output, reverse=False):
         if torch.is_grad_enabled() and self.early_factors:
@@ -759,6 +767,7 @@ class KFAC(optim.Optimizer):
                 scale = None if p['kl_clip'] is None else self._compute_grad_scale()
                 self.update_gradients(scale)
         p['step'] += 1
+        self._close_forward_count()
         return loss
 
     # ------------------------------------------------- phased plain steps
@@ -822,6 +831,7 @@ class KFAC(optim.Optimizer):
         scale = None if p['kl_clip'] is None else self._compute_grad_scale()
         self.update_gradients(scale)
         p['step'] += 1
+        self._close_forward_count()
 
     # ------------------------------------------------------------ hipGraphs
     def _precondition_and_apply(self):

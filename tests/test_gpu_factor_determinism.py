@@ -194,6 +194,49 @@ def test_early_factors_bitwise(graphed):
         assert torch.equal(a, b), (a - b).abs().max()
 
 
+def test_early_factors_survive_counter_rewinds():
+    """GraphedTrainStep.prepare() and a bench restarting its window rewind
+    the K-FAC step counter: with one forward per step() that is not micro-
+    batching, so early_factors stays on (forwards are counted between step()
+    calls, not per counter value) and the eager inverse step still launches
+    the A factors early."""
+    import warnings
+    import distributed_kfac_pytorch_amd as kfac
+    from distributed_kfac_pytorch_amd import graphs
+    from distributed_kfac_pytorch_amd.models import resnet
+    torch.manual_seed(0)
+    m = resnet.resnet_tiny(num_classes=10).cuda().to(memory_format=torch.channels_last)
+    opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9)
+    pre = kfac.KFAC(m, factor_update_freq=2, inv_update_freq=4, lr=0.05, damping=0.003,
+                    early_factors=True)
+    x = torch.randn(8, 3, 32, 32, device='cuda').contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device='cuda')
+
+    def step_fn():
+        opt.zero_grad(set_to_none=False)
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            loss = F.cross_entropy(m(x), y)
+        loss.backward()
+        pre.step()
+        opt.step()
+        return loss
+
+    step = graphs.GraphedTrainStep(step_fn, pre, [opt], warmup=1)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter('always')
+        for _ in range(3):
+            step()
+        step.prepare()
+        pre.param_groups[0]['step'] = 0
+        launched = pre._early_a_step
+        for _ in range(6):
+            step()
+        torch.cuda.synchronize()
+    assert not [x for x in w if 'several forward passes' in str(x.message)]
+    assert pre.early_factors
+    assert pre._early_a_step is not None and pre._early_a_step != launched
+
+
 @pytest.mark.parametrize('graphed', [False, True])
 def test_hook_factors_grouped_bitwise(graphed):
     """compute_factor_in_hook=True on the GPU (the multi-rank segmented-graph
