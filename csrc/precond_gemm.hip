@@ -36,6 +36,7 @@
 // QA/QG/QAt/QGt planes and Dt after each inverse update.
 #include "pgemm.h"
 
+#include <cstdlib>
 #include <type_traits>
 #include "devtable.h"
 
@@ -109,7 +110,11 @@ constexpr int TK = 32;
 // one computing while the other waits at its k-step barrier.
 // DBUF: two LDS images -- the next k-step is stored into the idle image
 // right after the MFMAs, one barrier per k-step instead of two.
-template <int PREC, int BM, int BN, int WM, int WN, int WPE = 1, bool DBUF = false>
+// XCD: tiles that share the larger operand's panel are given block indices
+// equal mod 8 -- the same XCD, so the panel is fetched into one L2 instead of
+// several (blocks are dealt round-robin over the 8 XCDs)
+template <int PREC, int BM, int BN, int WM, int WN, int WPE = 1, bool DBUF = false,
+          bool XCD = false>
 __global__ __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(WPE)))
 void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict__ kl) {
   constexpr bool X3 = (PREC == PREC_BF16X3), X6 = (PREC == PREC_BF16X6);
@@ -132,10 +137,12 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   constexpr int LDS_BYTES = IMG16 ? (PL * (BM + BN) * LDB16 * 2) : ((BM + BN) * LDF32 * 4);
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES * (DBUF ? 2 : 1)];
 
-  // Workgroups stay in hardware order (round-robin over the 8 XCDs).  An
-  // XCD-contiguous remap (guide T1) measured 2.11 -> 4.62 ms on the ResNet-50
-  // chain (profiles/r3_pgemm_xcd_remap.log): over a ragged grouped grid it
-  // hands one XCD all the tiles of the big-K problems.
+  // Workgroups keep the hardware dispatch order (round-robin over the 8
+  // XCDs).  An XCD-contiguous remap (guide T1) measured 2.11 -> 4.62 ms on the
+  // ResNet-50 chain (profiles/r3_pgemm_xcd_remap.log): over a ragged grouped
+  // grid it hands one XCD all the tiles of the big-K problems.  XCD (below)
+  // only permutes tiles WITHIN a problem, in groups of 8 panels, so every XCD
+  // still gets an equal share of every problem at the same time.
   const int pi = find_problem(table, count, blockIdx.x);
   const PGemm P = table[pi];                      // uniform: scalar registers
   const AS1 unsigned char* const Ah = (const AS1 unsigned char*)P.a_hi;
@@ -144,7 +151,28 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   const AS1 unsigned char* const Bl = (const AS1 unsigned char*)P.b_lo;
   const long long lda = P.lda, ldb = P.ldb;
   const int local = blockIdx.x - P.tile_begin;
-  const int tm = local / P.tiles_n, tn = local - tm * P.tiles_n;
+  int tm = local / P.tiles_n, tn = local - tm * P.tiles_n;
+  if constexpr (XCD) {
+    const int nt = (pi + 1 < count ? table[pi + 1].tile_begin : (int)gridDim.x) - P.tile_begin;
+    const int tiles_m = nt / P.tiles_n, tiles_n = P.tiles_n;
+    // group along the dimension with more panels; the remainder (fewer than
+    // 8 panels) keeps the row-major order
+    const bool by_a = tiles_m >= tiles_n;
+    const int np = by_a ? tiles_m : tiles_n, other = by_a ? tiles_n : tiles_m;
+    const int full = (np / 8) * 8 * other;
+    int pa, ob;
+    if (local < full) {
+      const int i = local >> 3;
+      pa = 8 * (i / other) + (local & 7);
+      ob = i % other;
+    } else {
+      const int r = local - full;
+      pa = (np / 8) * 8 + r / other;
+      ob = r % other;
+    }
+    tm = by_a ? pa : ob;
+    tn = by_a ? ob : pa;
+  }
   const int m0 = tm * BM, n0 = tn * BN;
   const int M = P.M, N = P.N;
   // device-sized problems (csrc/eig_dc.hip patches M / K at run time and
@@ -663,6 +691,13 @@ KFAC_API int kfac_split_record_size() { return (int)sizeof(SplitJob); }
 // build = tile 8, profiles/r2_pgemm_occupancy.log), 1 = 256 x 256 (8 waves),
 // 2 = 64 x 64 (4 waves), 3 = 128 x 128 (8 waves), 4 = 128 x 64 (4 waves);
 // the table (ops/precond_fused.py) holds the problems of that tile class.
+// XCD-grouped tile order for the default bf16x6 tile (ResNet-50 chain 2.023 ->
+// 2.002 ms, profiles/r4_pgemm_xcd.log); KFAC_PGEMM_XCD=0 restores row-major
+static const bool g_pgemm_xcd = [] {
+  const char* e = getenv("KFAC_PGEMM_XCD");
+  return !(e && e[0] == '0');
+}();
+
 KFAC_API int kfac_pgemm(int prec, int tile, const void* dev_table, int count, int total_tiles,
                         double* kl, hipStream_t stream) {
   if (count <= 0 || total_tiles <= 0) return 0;
@@ -707,6 +742,9 @@ KFAC_API int kfac_pgemm(int prec, int tile, const void* dev_table, int count, in
     else if (tile == 8)
       hipLaunchKernelGGL((pgemm_kernel<PREC_BF16X6F, 128, 128, 2, 2, 1>), g, dim3(256), 0, stream,
                          t, count, kl);
+    else if (g_pgemm_xcd)
+      hipLaunchKernelGGL((pgemm_kernel<PREC_BF16X6F, 128, 128, 2, 2, 2, false, true>), g, dim3(256),
+                         0, stream, t, count, kl);
     else
       hipLaunchKernelGGL((pgemm_kernel<PREC_BF16X6F, 128, 128, 2, 2, 2>), g, dim3(256), 0, stream,
                          t, count, kl);
