@@ -76,13 +76,16 @@ def reset_comm_backend():
 
 
 def _can_split():
-    """ncclCommSplit is available: RCCL/NCCL default group bound to a device
-    (init_process_group(device_id=...), parallel/launch.py) and a torch
-    with dist.split_group.  Identical on every rank."""
+    """ncclCommSplit is requested (KFAC_COMM_SPLIT=1) and available: RCCL/NCCL
+    default group bound to a device (init_process_group(device_id=...),
+    parallel/launch.py) and a torch with dist.split_group.  Identical on every
+    rank.  Off by default: the split path has run only on gloo with a
+    recorded split_group (tests/test_distributed.py); plain new_group
+    communicators are the path every torch / RCCL build exercises."""
     if not (_dist_ready() and hasattr(dist, 'split_group')):
         return False
-    if os.environ.get('KFAC_COMM_SPLIT', '1') == '0':
-        return False        # plain new_group communicators (debugging / old RCCL)
+    if os.environ.get('KFAC_COMM_SPLIT', '0') != '1':
+        return False
     if dist.get_backend() != 'nccl':
         return False
     pg = dist.distributed_c10d._get_default_group()
