@@ -383,7 +383,34 @@ __global__ __launch_bounds__(256) void red_fin_kernel(const RMat* __restrict__ m
 
 // ------------------------------------------------------------------- U
 // A[I][K] -= L_I R_K^T with L = [V | W], R = [W | V] (rows >= q+1, upper):
-// the panel's rank-2NB update, exact-f32 MFMA, 4 waves of 64 x 64.
+// the panel's rank-2NB update, 4 waves of 64 x 64.  X6 (default): the fp32
+// operands split into bf16 hi / mid / lo planes as the fragments are read from
+// LDS, six v_mfma_f32_32x32x16_bf16 products per term (every term above 2^-24
+// relative, the precision scheme of csrc/precond_gemm.hip's bf16x6): fp32-level
+// error at 2.7x fewer MFMA cycles than the exact-f32 32x32x2 MFMA path
+// (KFAC_REDUCE_UPD=f32), which held each update workgroup ~4 us.
+__device__ __forceinline__ void split3(float x, uint16_t& h, uint16_t& m, uint16_t& l) {
+  h = f32_to_bf16_bits(x);
+  const float r = x - bf16_bits_to_f32(h);
+  m = f32_to_bf16_bits(r);
+  l = f32_to_bf16_bits(r - bf16_bits_to_f32(m));
+}
+// 8 consecutive fp32 of an LDS row -> the three bf16x8 planes of one fragment
+__device__ __forceinline__ void frag3(const float* src, bf16x8_t& h8, bf16x8_t& m8, bf16x8_t& l8) {
+  typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+  u16x8 h, m, l;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    uint16_t a, b, c;
+    split3(src[e], a, b, c);
+    h[e] = a; m[e] = b; l[e] = c;
+  }
+  h8 = __builtin_bit_cast(bf16x8_t, h);
+  m8 = __builtin_bit_cast(bf16x8_t, m);
+  l8 = __builtin_bit_cast(bf16x8_t, l);
+}
+
+template <bool X6>
 __global__ __launch_bounds__(256) void red_upd_kernel(const RMat* __restrict__ mats,
                                                       const int* __restrict__ offs, int nact,
                                                       int q) {
@@ -447,19 +474,41 @@ __global__ __launch_bounds__(256) void red_upd_kernel(const RMat* __restrict__ m
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int x = 0; x < 16; ++x) acc[a][b][x] = 0.f;
+  if constexpr (X6) {
+#pragma unroll
+    for (int kc = 0; kc < 2 * NB / 16; ++kc) {      // k = 16 kc + 8 lh + (0..7)
+      const int k0 = 16 * kc + 8 * lh;
+      bf16x8_t ap[3][2], bp[3][2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) frag3(&sL[wr * 64 + a * 32 + l31][k0], ap[0][a], ap[1][a], ap[2][a]);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) frag3(&sR[wc * 64 + b * 32 + l31][k0], bp[0][b], bp[1][b], bp[2][b]);
+      // smallest terms first: lo.hi, hi.lo, mid.mid, mid.hi, hi.mid, hi.hi
+      constexpr int TA[6] = {2, 0, 1, 1, 0, 0}, TB[6] = {0, 2, 1, 0, 1, 0};
+#pragma unroll
+      for (int t = 0; t < 6; ++t)
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[TA[t]][a], bp[TB[t]][b],
+                                                                acc[a][b], 0, 0, 0);
+    }
+  } else {
 #pragma unroll 4
-  for (int kk = 0; kk < NB; ++kk) {                 // k = 2 kk + lh over 2 NB
-    const int k = 2 * kk + lh;
-    float av[2], bv[2];
+    for (int kk = 0; kk < NB; ++kk) {               // k = 2 kk + lh over 2 NB
+      const int k = 2 * kk + lh;
+      float av[2], bv[2];
 #pragma unroll
-    for (int a = 0; a < 2; ++a) av[a] = sL[wr * 64 + a * 32 + l31][k];
+      for (int a = 0; a < 2; ++a) av[a] = sL[wr * 64 + a * 32 + l31][k];
 #pragma unroll
-    for (int b = 0; b < 2; ++b) bv[b] = sR[wc * 64 + b * 32 + l31][k];
+      for (int b = 0; b < 2; ++b) bv[b] = sR[wc * 64 + b * 32 + l31][k];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+      for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
-        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[b], acc[a][b], 0, 0, 0);
+        for (int b = 0; b < 2; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[b], acc[a][b], 0, 0, 0);
+    }
   }
   // C/D map of 32x32: row = (x&3) + 8 (x>>2) + 4 lh, col = lane & 31
 #pragma unroll
@@ -722,6 +771,12 @@ void launch_fin(const RPlan& P, const int* of, int j, hipStream_t s) {
                      P.nact[0][j], j);
 }
 
+// panel-update MFMA precision: bf16x6 (default) or exact f32 (KFAC_REDUCE_UPD=f32)
+const bool g_upd_x6 = [] {
+  const char* e = getenv("KFAC_REDUCE_UPD");
+  return !(e && !strcmp(e, "f32"));
+}();
+
 int enqueue(const RPlan& P, hipStream_t stream) {
   const int nm = (int)P.n_sorted.size();
   const size_t kstride = (size_t)P.nmax * (nm + 1);
@@ -736,9 +791,14 @@ int enqueue(const RPlan& P, hipStream_t stream) {
       case 96: launch_fin<96>(P, of, j, stream); break;
       default: launch_fin<128>(P, of, j, stream); break;
     }
-    if (P.grid[1][j] > 0)
-      hipLaunchKernelGGL(red_upd_kernel, dim3(P.grid[1][j]), dim3(256), 0, stream, P.d_mats,
-                         of + kstride, P.nact[1][j], j);
+    if (P.grid[1][j] > 0) {
+      if (g_upd_x6)
+        hipLaunchKernelGGL(red_upd_kernel<true>, dim3(P.grid[1][j]), dim3(256), 0, stream,
+                           P.d_mats, of + kstride, P.nact[1][j], j);
+      else
+        hipLaunchKernelGGL(red_upd_kernel<false>, dim3(P.grid[1][j]), dim3(256), 0, stream,
+                           P.d_mats, of + kstride, P.nact[1][j], j);
+    }
     if (P.grid[2][j] > 0)
       hipLaunchKernelGGL(red_symv_kernel, dim3(P.grid[2][j]), dim3(256), 0, stream, P.d_mats,
                          of + 2 * kstride, P.nact[2][j], j);
