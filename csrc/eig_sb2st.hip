@@ -82,6 +82,7 @@ struct SbMat {
   long long* ts;          // dbg & 8: [workgroup][2] s_memrealtime stamps (100 MHz); dbg & 128:
                           // then 8 ticks x 8 phase stamps (s_memtime) of group 0's wave 1
   int nwg;                // workgroups of the launch (stamp layout)
+  int* status;            // caller's int: the timed-out wait count after the launch (host check)
 };
 struct SbWg { int mat, g; };
 
@@ -434,7 +435,7 @@ struct SbPlan {
   SbMat* d_mats = nullptr;
   SbWg* d_wgs = nullptr;
   int* d_prog = nullptr;       // all matrices' group counters, then the error count
-  int nprog = 0, nwg = 0, nw = NW4;
+  int nprog = 0, nwg = 0, nw = NW4, count = 0;
   long long* d_ts = nullptr;
   hipGraphExec_t exec = nullptr;
 };
@@ -448,6 +449,15 @@ std::vector<SbWg> g_last_wgs;
 constexpr size_t LDS_BYTES = 96 * 1024;
 static_assert((size_t)lds_floats<8>() * sizeof(float) <= LDS_BYTES, "ring exceeds LDS");
 
+// after the pipeline: every matrix's status word = the launch's timed-out wait
+// count (a broken pipeline finishes with garbage d / e / v2; the host raises
+// on a nonzero status in eigen.check_solver_status)
+__global__ void sb2st_status_kernel(const SbMat* __restrict__ mats, int count) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count && mats[i].status != nullptr)
+    *mats[i].status = __hip_atomic_load(mats[i].err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 int enqueue(const SbPlan& P, hipStream_t s) {
   hipLaunchKernelGGL(sb2st_zero_kernel, dim3(4), dim3(256), 0, s, P.d_prog, P.nprog + 1);
   if (P.nw == 8)
@@ -455,6 +465,8 @@ int enqueue(const SbPlan& P, hipStream_t s) {
   else
     hipLaunchKernelGGL(sb2st_kernel<NW4>, dim3(P.nwg), dim3(64 * (NW4 + 1)), LDS_BYTES, s,
                        P.d_mats, P.d_wgs);
+  hipLaunchKernelGGL(sb2st_status_kernel, dim3((P.count + 63) / 64), dim3(64), 0, s, P.d_mats,
+                     P.count);
   return (int)hipGetLastError();
 }
 
@@ -486,6 +498,7 @@ KFAC_API int kfac_sb2st_debug_phases(long long* out) {
 
 struct KfacSb2stRecord {
   const float* band_in; float* band; float* v2; float* d; float* e; long long ldv2; long long n;
+  int* status;   // nullptr, or an int that receives the timed-out wait count
 };
 
 // Band -> tridiagonal for `count` matrices (n >= 2): band ((n+32) x 32, the
@@ -514,7 +527,7 @@ KFAC_API int kfac_sb2st_batched(const KfacSb2stRecord* recs, int count, int use_
     SbMat& M = mats[i];
     memset(&M, 0, sizeof(M));
     M.band = r.band; M.v2 = r.v2; M.d = r.d; M.e = r.e;
-    M.ldv2 = r.ldv2; M.n = (int)r.n;
+    M.ldv2 = r.ldv2; M.n = (int)r.n; M.status = r.status;
     M.dbg = getenv("KFAC_SB2ST_DBG") ? atoi(getenv("KFAC_SB2ST_DBG")) : 0;
     const int nsw = (int)r.n - 2;
     const int nw = (M.dbg & 32) ? 8 : NW4;
@@ -532,6 +545,7 @@ KFAC_API int kfac_sb2st_batched(const KfacSb2stRecord* recs, int count, int use_
     if (it == g_plans.end()) {
       SbPlan P;
       P.nw = (mats[0].dbg & 32) ? 8 : NW4;
+      P.count = count;
       int err;
       if ((err = (int)hipMalloc(&P.d_prog, sizeof(int) * (nprog + 1))) != 0) return err;
       P.nprog = nprog;

@@ -240,6 +240,21 @@ class GraphedTrainStep(object):
             for k in [k for k in d if k[2] and k[2][-1][-1] != gen]:
                 del d[k]
 
+    def _join_side_streams(self):
+        """After an eager step: order the current stream after every side
+        stream the step used (this trainer's update stream, K-FAC's factor /
+        fused-chain / eigensolver streams) with device-side event waits, so the
+        next replay cannot overtake them.  No host sync: a full
+        torch.cuda.synchronize() would also drain a deferred factor all-reduce
+        and a lagged inverse update that are meant to keep running."""
+        cur = torch.cuda.current_stream()
+        streams = [self.side] if self.side is not None else []
+        if self.pre is not None and hasattr(self.pre, 'side_streams'):
+            streams += self.pre.side_streams()
+        for s in streams:
+            if s is not None and s != cur:
+                cur.wait_stream(s)
+
     def __call__(self):
         self._purge_stale_plans()
         kind = self._kind()
@@ -259,21 +274,13 @@ class GraphedTrainStep(object):
             with torch.cuda.stream(self.side):
                 self.update()
             cur.wait_stream(self.side)
-            torch.cuda.synchronize()
+            self._join_side_streams()
             return loss
         if not self.enabled or kind == 'eager':
             self.eager_steps += 1
             out = self._eager()
             if self.enabled:
-                # drain every stream the eager step used (the eigensolver's
-                # worker streams are joined by events only) before the next
-                # replay; once per inv_update_freq steps.  A lagged inverse
-                # update in flight keeps running: only this step's streams.
-                if self.pre is not None and getattr(self.pre, 'inverses_in_flight', False):
-                    self.side.synchronize()
-                    torch.cuda.current_stream().synchronize()
-                else:
-                    torch.cuda.synchronize()
+                self._join_side_streams()
             return out
         if kind == 'factor':
             self._prepare_factor()

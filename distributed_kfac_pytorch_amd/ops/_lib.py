@@ -66,7 +66,7 @@ class Sy2sbRecord(ctypes.Structure):
 class Sb2stRecord(ctypes.Structure):
     # csrc/eig_sb2st.hip KfacSb2stRecord
     _fields_ = [('band_in', c_vp), ('band', c_vp), ('v2', c_vp), ('d', c_vp), ('e', c_vp),
-                ('ldv2', c_ll), ('n', c_ll)]
+                ('ldv2', c_ll), ('n', c_ll), ('status', c_vp)]
 
 
 class Q2Record(ctypes.Structure):
@@ -272,33 +272,3 @@ def workspace(device, numel, dtype=torch.float32, tag='main'):
         buf = torch.empty(max(numel, 1), dtype=dtype, device=device)
         _ws[key] = buf
     return buf[:numel]
-
-
-class ExternalEvent(object):
-    """A HIP event usable ACROSS captured graphs: record() during a capture
-    becomes an external event-record node of that graph, wait() during
-    another capture an external wait node, so graph B replayed on a second
-    stream starts when graph A passes the record point (torch.cuda.Event
-    refuses `external=True` on ROCm)."""
-
-    def __init__(self):
-        self.handle = lib().kfac_event_create()
-        if not self.handle:
-            raise RuntimeError('hipEventCreateWithFlags failed')
-
-    def record(self, stream=None):
-        s = stream if stream is not None else torch.cuda.current_stream()
-        check(lib().kfac_event_record_external(c_vp(self.handle), c_vp(s.cuda_stream)),
-              'kfac_event_record_external')
-
-    def wait(self, stream=None):
-        s = stream if stream is not None else torch.cuda.current_stream()
-        check(lib().kfac_stream_wait_external(c_vp(s.cuda_stream), c_vp(self.handle)),
-              'kfac_stream_wait_external')
-
-    def __del__(self):
-        try:
-            if self.handle and _lib is not None:
-                _lib.kfac_event_destroy(c_vp(self.handle))
-        except Exception:  # pragma: no cover - interpreter shutdown
-            pass

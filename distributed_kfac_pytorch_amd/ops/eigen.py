@@ -30,12 +30,16 @@ _streams = {}
 
 
 def _side_streams(device, k):
-    key = str(device)
-    pool = _streams.get(key)
-    if pool is None or len(pool) < k:
-        pool = [torch.cuda.Stream(device=device) for _ in range(k)]
-        _streams[key] = pool
+    pool = _streams.setdefault(str(device), [])
+    while len(pool) < k:     # grow only: a stream in the pool may still run work
+        pool.append(torch.cuda.Stream(device=device))
     return pool[:k]
+
+
+def side_streams(device):
+    """Every worker stream the eigensolver has used on `device` (a caller
+    that needs the device quiet joins these instead of a full device sync)."""
+    return list(_streams.get(str(device), []))
 
 
 def _jacobi_small(mats, clip, max_sweeps=30, tol=1e-7):
@@ -200,87 +204,28 @@ def _large_fused(mats, clip, stream, use_graph=True):
     on a side stream.  No library solver, no host round trip; each stage is
     a cached hipGraph.
 
-    Options measured on ResNet-50 (profiles/r2_eig_streams.log), both off by
-    default: FUSED_THREADS enqueues the side groups from worker threads (a
-    reduction graph holds one node per column, more packets than a HW queue
-    holds, so hipGraphLaunch blocks its host thread until the GPU has drained
-    most of it; from one thread the second group reaches its stream late) --
-    the chains then overlap, but each slows down as much as the overlap gains
-    (both bandwidth-heavy): 157 vs 156 ms.  FUSED_PRIORITY puts the largest
-    factors' chain on a high-priority stream: 162 vs 157 ms.
-    """
+    Measured and dropped (profiles/r2_eig_streams.log, r4_eig_groups.log):
+    enqueueing the side groups from worker threads (157 vs 156 ms) and the
+    largest factors' chain on a high-priority stream (162 vs 157 ms; 277 ms
+    in round 4)."""
     dev = mats[0].device
     groups = _fused_groups(mats)
     outs = [None] * len(mats)
     caller = stream
-    if FUSED_PRIORITY and len(groups) > 1:
-        # the largest factors' chain sets the critical path: its launches go
-        # to a high-priority queue, so the command processor dispatches them
-        # ahead of the smaller factors' chain, which has slack
-        stream = _priority_stream(dev)
     streams = [stream] + _side_streams(dev, len(groups) - 1)
-    for s in streams:
-        if s is not caller:
-            s.wait_stream(caller)
-
-    def run(slot):
-        g, st = groups[slot], streams[slot]
+    for s in streams[1:]:
+        s.wait_stream(caller)
+    for slot, (g, st) in enumerate(zip(groups, streams)):
         for i, r in zip(g, _fused_group([mats[i] for i in g], clip, st, use_graph, slot)):
             outs[i] = r
-
-    key = (str(dev), use_graph, tuple(tuple(mats[i].shape[0] for i in g) for g in groups))
-    if len(groups) > 1 and FUSED_THREADS and key in _FUSED_PLANNED:
-        pool = _thread_pool(len(groups) - 1)
-        didx = dev.index if dev.index is not None else torch.cuda.current_device()
-
-        def side(slot):
-            torch.cuda.set_device(didx)
-            run(slot)
-        futs = [pool.submit(side, slot) for slot in range(1, len(groups))]
-        try:
-            run(0)
-        finally:
-            for f in futs:
-                f.result()     # re-raises a worker's error
-    else:
-        # first call of a group layout: plans are built and captured (on
-        # private capture streams), serially
-        for slot in range(len(groups)):
-            run(slot)
-        _FUSED_PLANNED.add(key)
     del _INFOS[:-256]
-    for g, st in zip(groups, streams):
-        if st is caller:
-            continue
+    for g, st in zip(groups[1:], streams[1:]):
         caller.wait_stream(st)
         for i in g:
             mats[i].record_stream(st)
             outs[i][0].record_stream(caller)
             outs[i][1].record_stream(caller)
     return outs
-
-
-FUSED_THREADS = bool(int(os.environ.get('KFAC_EIG_FUSED_THREADS', '0')))
-FUSED_PRIORITY = bool(int(os.environ.get('KFAC_EIG_FUSED_PRIORITY', '0')))
-_prio = {}
-
-
-def _priority_stream(device):
-    key = str(device)
-    s = _prio.get(key)
-    if s is None:
-        lo, hi = torch.cuda.Stream.priority_range()
-        s = _prio[key] = torch.cuda.Stream(device=device, priority=hi)
-    return s
-_FUSED_PLANNED = set()
-_POOL = [None]
-
-
-def _thread_pool(k):
-    from concurrent.futures import ThreadPoolExecutor
-    if _POOL[0] is None or _POOL[0]._max_workers < k:
-        _POOL[0] = ThreadPoolExecutor(max_workers=max(k, 3), thread_name_prefix='kfac-eig')
-    return _POOL[0]
 
 
 def _fused_group(mats, clip, stream, use_graph, slot=0):
@@ -373,6 +318,7 @@ def _ts_buffers(dev, n, b, slot=0):
                     v2=torch.zeros(b, max(n - 1, 1), ldv2, **f32),
                     d=torch.zeros(b, n, **f32), e=torch.zeros(b, n, **f32),
                     w=torch.zeros(b, n, **f32), Z=torch.zeros(b, n, lda, **f32),
+                    sbstat=torch.zeros(b, dtype=torch.int32, device=dev),
                     wsb=wsb, dcws=torch.zeros(b * wsb, dtype=torch.uint8, device=dev),
                     T=torch.zeros(2 * b * nblk * BT * BT, **f32),
                     W1=torch.zeros(b * int(L.kfac_backtransform_slabs(lda)) * BT * n, **f32),
@@ -415,6 +361,7 @@ def _two_stage_group(mats, clip, stream, use_graph=True, slot=0):
                 q.band_in = q.band = B['band'][i].data_ptr()
                 q.v2, q.d, q.e = B['v2'][i].data_ptr(), B['d'][i].data_ptr(), B['e'][i].data_ptr()
                 q.ldv2, q.n = B['ldv2'], n
+                q.status = B['sbstat'][i].data_ptr()    # timed-out bulge-chasing waits
                 r3[k] = dcr[i]
                 z = r4[k]
                 z.Z, z.v2, z.ldz, z.ldv2, z.n = (B['Z'][i].data_ptr(), B['v2'][i].data_ptr(),
@@ -422,6 +369,10 @@ def _two_stage_group(mats, clip, stream, use_graph=True, slot=0):
                 k += 1
         _lib.check(L.kfac_sy2sb_batched(r1, total, int(use_graph), cs), 'kfac_sy2sb_batched')
         _lib.check(L.kfac_sb2st_batched(r2, total, int(use_graph), cs), 'kfac_sb2st_batched')
+        # a bounded wait that timed out leaves garbage d / e / v2: the count
+        # joins the solver status that check_solver_status() raises on
+        for _, _, B in bufs:
+            _INFOS.append(B['sbstat'].clone())
         _lib.check(L.kfac_dc_batched(r3, total, int(use_graph), cs), 'kfac_dc_batched')
         _lib.check(L.kfac_q2_batched(r4, total, int(use_graph), cs), 'kfac_q2_batched')
         for n, idx, B in bufs:
@@ -449,8 +400,10 @@ def two_stage_eigh(mats, clip=0.0, use_graph=True):
 
 def check_solver_status():
     """Host-side check of every divide-and-conquer call issued since the last
-    check (info != 0 -> the solver did not converge).  Syncs; call once per
-    inverse step, not in the hot path."""
+    check (info != 0 -> the solver did not converge) and of every bulge-chasing
+    launch of the two-stage path (nonzero = bounded waits that timed out, the
+    band reduction's output is garbage).  Syncs; call once per inverse step,
+    not in the hot path."""
     global _INFOS
     infos, _INFOS = _INFOS, []
     bad = [int(i.abs().max().item()) for i in infos if (i != 0).any().item()]

@@ -643,6 +643,25 @@ class KFAC(optim.Optimizer):
             layer.state['A'] = st
         self._early_a = items
 
+    def side_streams(self):
+        """The streams other than the current one that K-FAC's last step may
+        have left work on: the factor stream, the fused chain's side stream,
+        the eigensolver's workers, and the lagged-inverse stream unless a
+        lagged update is still in flight (that one runs on purpose).  Not the
+        deferred factor all-reduce, which is joined by join_factor_comm()."""
+        out = []
+        if self._factor_stream is not None:
+            out.append(self._factor_stream)
+        side = getattr(self.fused, '_side', None)
+        if side is not None:
+            out.append(side)
+        if self._inv_stream is not None and not self.inverses_in_flight:
+            out.append(self._inv_stream)
+        if self.layers and self.layers[0].module.weight.is_cuda:
+            from .ops import eigen as eigen_ops
+            out += eigen_ops.side_streams(self.layers[0].module.weight.device)
+        return out
+
     def join_early_factors(self):
         """Order the current stream after an early A-factor update in flight."""
         if self._early_a is not None:

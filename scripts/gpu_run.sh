@@ -36,6 +36,8 @@ step() {  # step <name> <limit_s> <command...>
 for s in "$@"; do
   case $s in
     tests) step tests 900 python -u -m pytest $TESTS -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    # the round-end driver's exact command (no timeout plugin flags, fresh MIOpen db)
+    driver) MIOPEN_USER_DB_PATH=/tmp/mdb_fresh_$$ step driver 900 python3 -m pytest tests/ -x -q -m gpu -p no:cacheprovider ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps $STEPS --warmup $WARMUP $BENCH_ARGS ;;
     bench-sgd) step bench_sgd 600 python bench.py --steps $STEPS --warmup $WARMUP --no-kfac $BENCH_ARGS ;;

@@ -38,17 +38,14 @@ def main():
         mats.append(x @ x.t() / x.shape[1] + 1e-3 * torch.eye(n, device=dev))
     print('factors', len(ns), 'sum n^3 %.3g' % sum(float(n) ** 3 for n in ns), flush=True)
     variants = [('default', {}), ('fs1', {'FS': 1}), ('fs3', {'FS': 3}),
-                ('threads', {'TH': True}), ('prio', {'PR': True}),
                 ('only_big', {'SEL': 'big'}), ('only_rest', {'SEL': 'rest'}),
                 ('only_big_fs1', {'SEL': 'big', 'FS': 1}), ('only_rest_fs1', {'SEL': 'rest', 'FS': 1})]
     if len(sys.argv) > 1:
         variants = [v for v in variants if v[0] in sys.argv[1:]]
     res = {}
-    base = dict(FS=eigen.FUSED_STREAMS, TH=eigen.FUSED_THREADS, PR=eigen.FUSED_PRIORITY)
+    base = dict(FS=eigen.FUSED_STREAMS)
     for name, cfg in variants:
         eigen.FUSED_STREAMS = cfg.get('FS', base['FS'])
-        eigen.FUSED_THREADS = cfg.get('TH', base['TH'])
-        eigen.FUSED_PRIORITY = cfg.get('PR', base['PR'])
         nmax = max(A.shape[0] for A in mats)
         sel = cfg.get('SEL')
         run_mats = mats if sel is None else [A for A in mats if (2 * A.shape[0] > nmax) == (sel == 'big')]

@@ -14,6 +14,8 @@ import torch
 
 sys.path.insert(0, os.getcwd())
 from distributed_kfac_pytorch_amd.ops import _lib  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from external_event import ExternalEvent  # noqa: E402
 
 
 def work(x, n):
@@ -29,8 +31,8 @@ def main():
     # bandwidth-bound chain fills the GPU alone and cannot show overlap)
     a = torch.randn(1 << 14, device=dev)
     b = torch.randn(1 << 14, device=dev)
-    ev_mid = _lib.ExternalEvent()
-    ev_done = _lib.ExternalEvent()
+    ev_mid = ExternalEvent()
+    ev_done = ExternalEvent()
     # warm up
     for st in (s1, s2):
         with torch.cuda.stream(st):

@@ -9,7 +9,7 @@ are kept; for every factor it reports, in fp64:
   * the mixing band of the old eigenbasis: U = Q100^T Q_ref(200); for each
     eigenvector above the noise floor, how far (in sorted index) its weight
     spreads (|U_ij| > 1e-2 / 1e-4),
-  * iterations of the warm-started refinement (ops/eig_warm.refine_reference)
+  * iterations of the warm-started refinement (scripts/probes/eig_warm.refine_reference)
     to reach the tolerance, per window size.
 
     python scripts/probes/probe_warm_eig.py [--fixed] [--steps 201] [--min-n 256]
@@ -23,9 +23,10 @@ import torch
 import torch.nn.functional as F
 
 sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import distributed_kfac_pytorch_amd as kfac  # noqa: E402
 from distributed_kfac_pytorch_amd.models import resnet  # noqa: E402
-from distributed_kfac_pytorch_amd.ops import eig_warm  # noqa: E402
+import eig_warm  # noqa: E402  (scripts/probes/eig_warm.py)
 
 
 def train(args, dev):
