@@ -84,6 +84,11 @@ class CapturableGradScaler(torch.amp.GradScaler):
             grads = [p.grad for p in params]
             lr, momentum = group['lr'], group['momentum']
             wd, damp, nesterov = group['weight_decay'], group['dampening'], group['nesterov']
+            if damp != 0 and momentum != 0:
+                # torch.optim.SGD's first step clones g into a fresh buffer and
+                # ignores dampening; a zero buffer here would give (1 - d) g
+                raise ValueError('step_graphable: dampening != 0 is not supported '
+                                 '(SGD applies it only after the first step)')
             if wd != 0:
                 grads = torch._foreach_add(grads, params, alpha=wd)
             bufs = None

@@ -27,6 +27,7 @@ world > 1; #4 HYBRID validation uses max(1, round(W*f)); #7 group averaging;
 #11 register_shared_module forwards every layer kwarg; #16 device KL scale;
 #17 unassigned ranks start as None.
 """
+import contextlib
 import enum
 import functools
 import gc
@@ -292,6 +293,7 @@ class KFAC(optim.Optimizer):
         # compute_factor_in_hook on the GPU: gradient hooks of this step seen /
         # registered (the last one runs the grouped factor launches)
         self._hook_step = None
+        self._defer_hook = False     # defer_hook_factors(): save only, compute later
         self._hook_flush_warned = False
         self._g_seen = 0
         self._g_expected = 0
@@ -513,6 +515,23 @@ class KFAC(optim.Optimizer):
         self._prev_fwd_calls = self._fwd_calls
         self._fwd_calls = 0
 
+    @contextlib.contextmanager
+    def defer_hook_factors(self):
+        """With compute_factor_in_hook: the forward / backward passes inside
+        this block only SAVE their hook data (the next pass overwrites it
+        unless accumulate_data), computing no factor.  A micro-batched step
+        runs all but its last micro-batch under it, so the factors come from
+        the last micro-batch with ONE running-average update per factor step
+        -- the reference's default (accumulate_data=False, factors in step(),
+        kfac/preconditioner.py:494-497, kfac/layers/base.py:364-379) -- not k
+        EMA updates, one per micro-batch.  Also captured correctly: the hooks
+        run (and read the flag) while a graph is being captured."""
+        prev, self._defer_hook = self._defer_hook, True
+        try:
+            yield
+        finally:
+            self._defer_hook = prev
+
     def _forward_hook(self, module, input, output, reverse=False):
         if torch.is_grad_enabled() and self.early_factors:
             self._count_forward(module)
@@ -520,6 +539,14 @@ class KFAC(optim.Optimizer):
             return
         layer = self.hook_layers[module]
         alpha = self.param_groups[0]['factor_decay']
+        if self._defer_hook and self.compute_factor_in_hook:
+            if reverse:
+                layer.save_grad_outputs(input)
+            else:
+                layer.save_inputs(input)
+            if isinstance(output, torch.Tensor) and output.requires_grad:
+                output.register_hook(functools.partial(self._grad_hook_deferred, module, reverse))
+            return
         grouped = self._hook_factors_grouped()
         if grouped:
             self._hook_counters()
@@ -535,6 +562,15 @@ class KFAC(optim.Optimizer):
             if grouped:
                 self._g_expected += 1
             output.register_hook(functools.partial(self._grad_hook, module, reverse))
+
+    def _grad_hook_deferred(self, module, reverse, grad):
+        if not self._factor_step():
+            return
+        layer = self.hook_layers[module]
+        if reverse:
+            layer.save_inputs((grad,))
+        else:
+            layer.save_grad_outputs((grad,))
 
     def _grad_hook(self, module, reverse, grad):
         if not self._factor_step():

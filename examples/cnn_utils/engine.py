@@ -75,24 +75,38 @@ class GraphedTrainer(object):
             self.step = graphs.GraphedTrainStep(self._train_step, preconditioner, [optimizer],
                                                 enabled=args.cuda)
 
-    def _forward_backward(self):
+    def _forward_backward(self, ragged=False):
         if self.grad_sync is not None:
             self.grad_sync.zero_grad()
         else:
             self.optimizer.zero_grad(set_to_none=False)
         k = self.micro
         mb = self.x.shape[0] // k
+        if ragged:
+            # a batch that does not split into k equal micro-batches (eager):
+            # micro-batches of args.batch_size and a shorter last one, like the
+            # reference's data[i:i + batch_size] loop (examples/cnn_utils/engine.py:33-48)
+            mb = int(getattr(self.args, 'batch_size', 0)) or -(-self.x.shape[0] // k)
+            k = -(-self.x.shape[0] // mb)
         losses, outs = [], []
+        # factors in the captured hooks (multi-rank): all but the last
+        # micro-batch only save hook data, so the factors come from the last
+        # micro-batch with one EMA update, as in the eager loop and the
+        # reference (KFAC.defer_hook_factors)
+        defer = self.pre is not None and getattr(self.pre, 'compute_factor_in_hook', False)
         for i in range(k):
             xb, yb = (self.x, self.y) if k == 1 else \
                 (self.x[i * mb:(i + 1) * mb], self.y[i * mb:(i + 1) * mb])
-            with _autocast(self.args):
-                out = self.model(xb)
-                loss = self.loss_func(out, yb) / k
-            if self.scaler is not None:
-                self.scaler.scale(loss).backward()
-            else:
-                loss.backward()
+            ctx = self.pre.defer_hook_factors() if (defer and i < k - 1) else \
+                contextlib.nullcontext()
+            with ctx:
+                with _autocast(self.args):
+                    out = self.model(xb)
+                    loss = self.loss_func(out, yb) / k
+                if self.scaler is not None:
+                    self.scaler.scale(loss).backward()
+                else:
+                    loss.backward()
             losses.append(loss.detach())
             outs.append(out.detach())
         if k == 1:
@@ -120,7 +134,7 @@ class GraphedTrainer(object):
         x, y = self.x, self.y
         self.x, self.y = data, target
         try:
-            loss, out = self._forward_backward()
+            loss, out = self._forward_backward(ragged=data.shape[0] % self.micro != 0)
             if self.grad_sync is not None:
                 self.grad_sync()
             self._update()

@@ -67,3 +67,16 @@ def test_capturable_scaler_rejects_other_optimizers():
     s.scale(torch.tensor(1.0))
     with pytest.raises(TypeError):
         s.step_graphable(torch.optim.Adam([p]))
+
+
+def test_step_graphable_rejects_dampening():
+    """SGD's first step clones the gradient into the momentum buffer and
+    skips dampening; the graphable step cannot: refuse it."""
+    p = torch.randn(3).requires_grad_(True)
+    opt = torch.optim.SGD([p], lr=0.1, momentum=0.9, dampening=0.5)
+    sc = CapturableGradScaler('cpu', init_scale=2.0)
+    sc.scale(torch.tensor(1.0))
+    p.grad = torch.ones(3)
+    sc.unscale_graphable(opt)
+    with pytest.raises(ValueError):
+        sc.step_graphable(opt)

@@ -90,6 +90,37 @@ def test_compute_factor_in_hook_bit_identical():
             assert torch.equal(x, y)
 
 
+def test_defer_hook_factors_micro_batches():
+    """Micro-batched steps with the factors in the hooks (the graphed
+    multi-rank examples' mode): deferring all but the last micro-batch gives
+    the factors of computing them in step() -- the last micro-batch, one EMA
+    update per factor step -- while without deferral every
+    micro-batch's pass applies its own EMA update."""
+    torch.manual_seed(0)
+    base = SmallNet()
+    x = torch.randn(8, 3, 8, 8)
+    y = torch.randint(0, 10, (8,))
+    states = {}
+    for mode in ('step', 'deferred', 'every'):
+        model = copy.deepcopy(base)
+        pre = kfac.KFAC(model, factor_update_freq=1, inv_update_freq=1,
+                        compute_factor_in_hook=(mode != 'step'))
+        for _ in range(2):
+            model.zero_grad()
+            for i in range(2):          # two micro-batches of 4
+                ctx = pre.defer_hook_factors() if (mode == 'deferred' and i == 0) else \
+                    warnings.catch_warnings()
+                with ctx:
+                    out = model(x[4 * i:4 * i + 4])
+                    (nn.functional.cross_entropy(out, y[4 * i:4 * i + 4]) / 2).backward()
+            pre.step()
+        states[mode] = [(l.state['A'].clone(), l.state['G'].clone()) for l in pre.layers]
+    for (a1, g1), (a2, g2) in zip(states['step'], states['deferred']):
+        assert torch.equal(a1, a2) and torch.equal(g1, g2)
+    assert any(not torch.equal(a1, a2) for (a1, _), (a2, _) in zip(states['step'],
+                                                                    states['every']))
+
+
 @pytest.mark.parametrize('kw', [dict(precompute_outer_eigen=False), dict(use_eigen_decomp=False),
                                 dict(kl_clip=None), dict(factor_dtype=torch.float64),
                                 dict(inv_dtype=torch.float64), dict(accumulate_data=True)])
