@@ -159,7 +159,8 @@ class FactorAllreduce(object):
 
 def broadcast_eigendata(plan):
     backend = comm.backend
-    if backend.size() == 1 or plan.eig_arena is None or len(plan.eig_ranks) <= 1:
+    if backend.size() == 1 or plan.eig_arena is None or len(plan.eig_ranks) <= 1 or \
+            plan.eig_empty:
         return
     s, e = plan.eig_slot_of(plan.rank)
     backend.sync(backend.allgather_into(plan.eig_arena, plan.eig_arena[s:e],

@@ -65,6 +65,7 @@ class ExecutionPlan(object):
         self._build_grad_arena()
         self.eig_arena = None
         self.eig_regions = {}
+        self.eig_empty = True
         if build_eig_arena:
             self._build_eig_arena()
 
@@ -107,6 +108,9 @@ class ExecutionPlan(object):
         # one equal, 64-element aligned slot per group rank (group-rank order =
         # sorted global ranks): the distribution is one in-place all-gather
         self.eig_slot = max(1, (max(sizes) + 63) // 64 * 64)
+        # a group that owns no factor (more groups than layers) has nothing to
+        # distribute: broadcast_eigendata issues no collective for it
+        self.eig_empty = max(sizes) == 0
         self.eig_arena = torch.zeros(len(self.eig_ranks) * self.eig_slot, dtype=self.inv_dtype,
                                      device=self.device)
         for gi, owner in enumerate(self.eig_ranks):

@@ -70,7 +70,8 @@ def kfac_strategy(rank, world, port, out_dir, cfg):
                     assignment_strategy=cfg.get('assign', 'compute'))
     calls = _count_collectives(pre)
     grads, factors = run_steps(model, pre, data, cfg['steps'])
-    torch.save({'grads': grads, 'factors': factors, 'calls': calls},
+    torch.save({'grads': grads, 'factors': factors, 'calls': calls,
+                'eig_empty': bool(pre.plan is not None and pre.plan.eig_empty)},
                os.path.join(out_dir, 'rank{}.pt'.format(rank)))
     dist.barrier()
     dist.destroy_process_group()
@@ -331,3 +332,45 @@ def example_graphs(rank, world, port, out_dir, cfg):
             '--graphs', str(cfg['graphs'])]
     hist = ex.main(argv)
     torch.save(hist, os.path.join(out_dir, 'rank{}_g{}.pt'.format(rank, cfg['graphs'])))
+
+
+def kfac_collective_counts(rank, world, port, out_dir, cfg):
+    """The K-FAC collectives each step kind issues on this rank, as bench.py
+    reports them (comm.kfac_collectives_per_step_kind: counter deltas of the
+    first step of each kind), plus the plan facts an independent expectation
+    needs (layer sizes, owners)."""
+    _init(rank, world, port)
+    import torch.nn as nn
+    import distributed_kfac_pytorch_amd as kfac
+    from distributed_kfac_pytorch_amd import comm
+    from tests._oracle_common import build_case
+    steps = 6
+    model, data = build_case({'seed': 0, 'batch': 6, 'steps': steps})
+    pre = kfac.KFAC(model, factor_update_freq=2, inv_update_freq=4, lr=0.05, damping=0.003,
+                    comm_method=getattr(kfac.CommMethod, cfg['method']),
+                    grad_worker_fraction=cfg.get('fraction', 0.25),
+                    precompute_outer_eigen=cfg.get('prediv', True))
+    opt = torch.optim.SGD(model.parameters(), lr=0.05, momentum=0.9)
+    by_kind = {}
+    for i in range(steps):
+        p = pre.param_groups[0]
+        kind = 'inverse' if p['step'] % p['inv_update_freq'] == 0 else \
+            'factor' if p['step'] % p['factor_update_freq'] == 0 else 'plain'
+        c0 = comm.backend.counters()
+        x, y = data[i]
+        opt.zero_grad()
+        nn.functional.cross_entropy(model(x), y).backward()
+        pre.step()
+        opt.step()
+        c1 = comm.backend.counters()
+        delta = {k: [v[0] - c0.get(k, (0, 0))[0], v[1] - c0.get(k, (0, 0))[1]]
+                 for k, v in c1.items() if v != c0.get(k)}
+        by_kind.setdefault(kind, []).append(delta)
+    pre.join_factor_comm()
+    layers = [{'nA': l.state['A'].shape[0], 'nG': l.state['G'].shape[0],
+               'grad_numel': int(torch.Size(l.grad_shape).numel())} for l in pre.layers]
+    torch.save({'by_kind': by_kind, 'layers': layers, 'a_locs': list(pre.plan.a_locs),
+                'g_locs': list(pre.plan.g_locs), 'summary': pre.comm_summary()},
+               os.path.join(out_dir, 'rank{}.pt'.format(rank)))
+    dist.barrier()
+    dist.destroy_process_group()

@@ -108,8 +108,10 @@ def test_strategy_equivalence(tmp_path, world, cfg):
         gw = max(1, int(round(world * {'COMM_OPT': 1.0, 'MEM_OPT': 0.0}.get(
             cfg['method'], cfg.get('fraction', 0.25)))))
         if cfg['method'] != 'MEM_OPT':
-            # inverse groups of gw ranks: one all-gather when gw > 1
-            assert calls['eig'] and all(c == (1 if gw > 1 else 0) for c in calls['eig']), calls
+            # inverse groups of gw ranks: one all-gather when gw > 1 (none for
+            # a group that owns no factor: more groups than layers)
+            want = 1 if (gw > 1 and not res['eig_empty']) else 0
+            assert calls['eig'] and all(c == want for c in calls['eig']), calls
         if cfg['method'] != 'COMM_OPT':
             # gradient groups of world / gw ranks
             assert calls['grad'] and all(c == (1 if gw < world else 0)
@@ -276,3 +278,68 @@ def test_example_graphs_path_world2(tmp_path):
     a, b = h1[0]['train'], h0[0]['train']
     assert abs(a['loss'] - b['loss']) <= 1e-5 * max(1.0, abs(b['loss'])), (a, b)
     assert abs(h1[0]['val']['loss'] - h0[0]['val']['loss']) <= 1e-4, (h1, h0)
+
+
+COUNT_CASES = [{'method': 'COMM_OPT'}, {'method': 'MEM_OPT'},
+               {'method': 'HYBRID_OPT', 'fraction': 0.25}]
+
+
+def _expected_collectives(world, method, fraction, layers, a_locs, g_locs, rank, prediv=True):
+    """What each step kind must issue on `rank`, derived from the reference's
+    group layout (kfac/utils.py:59-159: inverse groups = contiguous blocks of
+    gw ranks, gradient groups = stride gw) and the layer sizes alone:
+      factor steps   ONE SUM all-reduce of every factor's upper triangle, fp32
+                     (the triu-packed bucket, X1/X2; one bucket at 64 MB)
+      inverse steps  + ONE all-gather of the inverse group's eigendata arena:
+                     an equal 64-element-aligned slot per group rank, sized
+                     by the largest owner's QA + QG + dGdA (X3)
+      every step     (MEM_OPT / HYBRID) ONE all-gather of the gradient arena
+                     over the gradient group: an equal slot per block of gw
+                     ranks, sized by the largest block's gradients (X5)."""
+    gw = max(1, int(round(world * {'COMM_OPT': 1.0, 'MEM_OPT': 0.0}.get(method, fraction))))
+    tri = sum(L['nA'] * (L['nA'] + 1) // 2 + L['nG'] * (L['nG'] + 1) // 2 for L in layers)
+    factor = {'all_reduce': [1, 4 * tri]}
+    out = {'plain': {}, 'factor': dict(factor), 'inverse': dict(factor)}
+    inv_group = list(range(rank // gw * gw, rank // gw * gw + gw))
+    if method != 'MEM_OPT' and gw > 1:
+        owned = {o: 0 for o in inv_group}
+        for L, a, g in zip(layers, a_locs, g_locs):
+            items = [('A', L['nA'] ** 2), ('G', L['nG'] ** 2)]
+            items += [('A', L['nG'] * L['nA'])] if prediv else [('A', L['nA']), ('G', L['nG'])]
+            for f, n in items:
+                o = a if f == 'A' else g
+                if o in owned:
+                    owned[o] += n
+        slot = (max(owned.values()) + 63) // 64 * 64
+        if slot:      # a group that owns no factor issues nothing
+            out['inverse']['all_gather_into_tensor'] = [1, 4 * slot * gw]
+    if method != 'COMM_OPT' and gw < world:
+        nblocks = world // gw
+        sizes = [0] * nblocks
+        for L, a in zip(layers, a_locs):
+            sizes[a // gw] += L['grad_numel']
+        gbytes = 4 * nblocks * ((max(sizes) + 63) // 64 * 64)
+        for k in out:
+            # gradient and eigendata all-gathers share the counter key
+            prev = out[k].get('all_gather_into_tensor', [0, 0])
+            out[k]['all_gather_into_tensor'] = [prev[0] + 1, prev[1] + gbytes]
+    return out
+
+
+@pytest.mark.parametrize('cfg', COUNT_CASES, ids=[c['method'] for c in COUNT_CASES])
+def test_collectives_per_step_kind_world8(tmp_path, cfg):
+    """The exact K-FAC collective calls and bytes of each step kind at world
+    8 (one MI355X node's ranks), per rank, against an expectation built from
+    the reference's group layout and the layer sizes -- the numbers the
+    bench's comm.kfac_collectives_per_step_kind reports, so the first RCCL
+    scaling record can be checked against this test line for line."""
+    world = 8
+    _spawn(_dist_worker.kfac_collective_counts, world, tmp_path, cfg)
+    for r in range(world):
+        res = torch.load(os.path.join(str(tmp_path), 'rank{}.pt'.format(r)), weights_only=False)
+        exp = _expected_collectives(world, cfg['method'], cfg.get('fraction', 0.25),
+                                    res['layers'], res['a_locs'], res['g_locs'], r)
+        assert sorted(res['by_kind']) == ['factor', 'inverse', 'plain'], res['by_kind']
+        for kind, deltas in res['by_kind'].items():
+            for d in deltas:
+                assert d == exp[kind], (r, kind, d, exp[kind])
