@@ -11,7 +11,13 @@
 // (a register-split variant -- fp32 LDS image, planes split per MFMA
 // fragment -- measured 2.55 vs 2.28 ms on ResNet-50: 2.3x the VALU work,
 // profiles/r3_pgemm_mode_r.log; removed)
-enum { PREC_F32 = 0, PREC_BF16X3 = 1, PREC_BF16X6 = 2, PREC_BF16X6F = 3 };
+// PREC_BF16X6A / PREC_BF16X6B: the same products with ONE operand (A resp.
+// B) stored as its three bf16 planes -- the eigenvector operands of the
+// preconditioning chain, split once per inverse update -- and the other, the
+// per-step operand, fp32 and split while it is staged: half the per-k-step
+// split work of PREC_BF16X6F
+enum { PREC_F32 = 0, PREC_BF16X3 = 1, PREC_BF16X6 = 2, PREC_BF16X6F = 3, PREC_BF16X6A = 4,
+       PREC_BF16X6B = 5 };
 // EPI_SUB: C -= A B^T (f32); EPI_ATOMIC: C += A B^T with f32 atomics (split-K)
 enum { EPI_STORE = 0, EPI_HADAMARD = 1, EPI_HADAMARD_VEC = 2, EPI_FINAL = 3, EPI_SUB = 4,
        EPI_ATOMIC = 5 };

@@ -119,8 +119,11 @@ __global__ __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(WP
 void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict__ kl) {
   constexpr bool X3 = (PREC == PREC_BF16X3), X6 = (PREC == PREC_BF16X6);
   constexpr bool X6F = (PREC == PREC_BF16X6F);     // fp32 in memory, planes in LDS
+  constexpr bool X6A = (PREC == PREC_BF16X6A), X6B = (PREC == PREC_BF16X6B);
+  constexpr bool X6M = X6A || X6B;                // one operand planes, one fp32
   constexpr bool SPL = X3 || X6;                  // split-bf16 planes in memory
-  constexpr bool IMG16 = SPL || X6F;              // bf16 plane image in LDS
+  constexpr bool SWZ = X6F || X6M;                // 64-byte swizzled LDS rows
+  constexpr bool IMG16 = SPL || SWZ;              // bf16 plane image in LDS
   constexpr int NT = 64 * WM * WN;                // threads
   constexpr int MI = BM / WM / 32, NJ = BN / WN / 32;
   // 80-byte rows: conflict-free ds_read_b128 (guide: LDS banking).  X6F
@@ -130,10 +133,10 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   // 16-byte pieces XOR-swizzled by (row >> 2) & 3 -- writes (two rows = 32
   // banks) and the b128 fragment reads (16 rows = 16 disjoint 4-bank spans)
   // both conflict-free
-  constexpr int LDB16 = (PREC == PREC_BF16X6F) ? TK : TK + 8;
+  constexpr int LDB16 = SWZ ? TK : TK + 8;
   constexpr int LDF32 = TK + 4;   // 16-byte aligned chunk writes
   // one LDS array (guide: a second __shared__ object can de-pipeline loads)
-  constexpr int PL = (X6 || X6F) ? 3 : (X3 ? 2 : 1);   // planes
+  constexpr int PL = (X6 || SWZ) ? 3 : (X3 ? 2 : 1);   // planes
   constexpr int LDS_BYTES = IMG16 ? (PL * (BM + BN) * LDB16 * 2) : ((BM + BN) * LDF32 * 4);
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES * (DBUF ? 2 : 1)];
 
@@ -189,23 +192,25 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
 
   // ---- loader: 16-byte chunks.  bf16 planes: per operand 2 planes x rows x 4
   // chunks (8 elements); f32: rows x 8 chunks (4 elements)
-  constexpr int CPR = SPL ? TK / 8 : TK / 4;      // chunks per row and plane
-  constexpr int MPL = SPL ? PL : 1;               // planes in memory
-  constexpr int CA = MPL * BM * CPR, CB = MPL * BN * CPR;
+  // per operand: planes in memory (bf16, 8 elements per 16-byte chunk) or fp32
+  constexpr bool APL = SPL || X6A, BPL = SPL || X6B;
+  constexpr int CPRA = APL ? TK / 8 : TK / 4, CPRB = BPL ? TK / 8 : TK / 4;   // chunks per row and plane
+  constexpr int MPLA = APL ? PL : 1, MPLB = BPL ? PL : 1;                     // planes in memory
+  constexpr int ESZA = APL ? 2 : 4, ESZB = BPL ? 2 : 4;
+  constexpr int CA = MPLA * BM * CPRA, CB = MPLB * BN * CPRB;
   constexpr int QA = CA / NT, QB = CB / NT;
   static_assert(CA % NT == 0 && CB % NT == 0, "loader split");
   // a chunk round stays in one plane: the plane index is a compile-time
   // constant (a run-time one turns the 3-way pointer select into a scratch
   // lookup table)
-  constexpr bool PLANE_CT = (BM * CPR) % NT == 0 && (BN * CPR) % NT == 0;
-  static_assert(!X6 || PLANE_CT, "3-plane loader needs whole chunk rounds per plane");
-  constexpr int ESZ = SPL ? 2 : 4;
+  constexpr bool PLANE_CT = (BM * CPRA) % NT == 0 && (BN * CPRB) % NT == 0;
+  static_assert(!(X6 || X6M) || PLANE_CT, "3-plane loader needs whole chunk rounds per plane");
   // chunk c -> (row, k offset): chunks fastest, a wave's global loads read
   // whole 128-byte row segments
-  auto chunk_rc = [&](int c, int rows, int& row, int& kof) {
-    const int cc = c % (rows * CPR);
-    row = cc / CPR;
-    kof = (cc % CPR) * (16 / ESZ);
+  auto chunk_rc = [&](int c, int rows, int cpr, int esz, int& row, int& kof) {
+    const int cc = c % (rows * cpr);
+    row = cc / cpr;
+    kof = (cc % cpr) * (16 / esz);
   };
   // third plane (X6): one plane stride past the second
   const AS1 unsigned char* const A2 = Al + (Al - Ah);
@@ -217,21 +222,26 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   u32x4n ra[2][QA], rb[2][QB];   // two k-steps of loads in flight (set = k-step parity)
   unsigned offa[QA], offb[QB];
   bool oka[QA], okb[QB];
+  // X6A / X6B: byte stride between the planes of the plane operand
+  const unsigned pstride_a = X6A ? (unsigned)(Al - Ah) : 0u;
+  const unsigned pstride_b = X6B ? (unsigned)(Bl - Bh) : 0u;
 #pragma unroll
   for (int q = 0; q < QA; ++q) {
     const int c = tid + NT * q;
     int row, kof;
-    chunk_rc(c, BM, row, kof);
+    chunk_rc(c, BM, CPRA, ESZA, row, kof);
     oka[q] = m0 + row < M;
-    offa[q] = ((unsigned)(oka[q] ? m0 + row : m0) * (unsigned)lda + kof) * ESZ;
+    offa[q] = ((unsigned)(oka[q] ? m0 + row : m0) * (unsigned)lda + kof) * ESZA;
+    if (X6A) offa[q] += (unsigned)(c / (BM * CPRA)) * pstride_a;
   }
 #pragma unroll
   for (int q = 0; q < QB; ++q) {
     const int c = tid + NT * q;
     int row, kof;
-    chunk_rc(c, BN, row, kof);
+    chunk_rc(c, BN, CPRB, ESZB, row, kof);
     okb[q] = n0 + row < N;
-    offb[q] = ((unsigned)(okb[q] ? n0 + row : n0) * (unsigned)ldb + kof) * ESZ;
+    offb[q] = ((unsigned)(okb[q] ? n0 + row : n0) * (unsigned)ldb + kof) * ESZB;
+    if (X6B) offb[q] += (unsigned)(c / (BN * CPRB)) * pstride_b;
   }
   const u32x4n z4 = {0u, 0u, 0u, 0u};
   // X6F: buffer loads -- the per-thread byte offset stays in one VGPR and the
@@ -243,26 +253,28 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
       const_cast<unsigned char*>((const unsigned char*)P.b_hi), 0, -1, 0x00020000);
   auto load = [&](int k0, auto setc) {
     constexpr int SET = decltype(setc)::value;
-    const long long kb = (long long)k0 * ESZ;
-    if constexpr (X6F) {
+    if constexpr (SWZ) {
+      // the k-step in the scalar offset (bytes per element per operand)
 #pragma unroll
       for (int q = 0; q < QA; ++q)
-        ra[SET][q] = __builtin_amdgcn_raw_buffer_load_b128(rsA, (int)offa[q], (int)kb, 0);
+        ra[SET][q] = __builtin_amdgcn_raw_buffer_load_b128(rsA, (int)offa[q], k0 * ESZA, 0);
 #pragma unroll
       for (int q = 0; q < QB; ++q)
-        rb[SET][q] = __builtin_amdgcn_raw_buffer_load_b128(rsB, (int)offb[q], (int)kb, 0);
+        rb[SET][q] = __builtin_amdgcn_raw_buffer_load_b128(rsB, (int)offb[q], k0 * ESZB, 0);
       return;
     }
+    constexpr int ESZ = ESZA;   // X3 / X6 (both planes) or F32 (both fp32)
+    const long long kb = (long long)k0 * ESZ;
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
-      const int plane = PLANE_CT ? NT * q / (BM * CPR) : (tid + NT * q) / (BM * CPR);
+      const int plane = PLANE_CT ? NT * q / (BM * CPRA) : (tid + NT * q) / (BM * CPRA);
       const AS1 unsigned char* base = (X6 ? (plane == 0 ? Ah : (plane == 1 ? Al : A2))
                                           : (plane ? Al : Ah)) + kb;
       ra[SET][q] = *(const AS1 u32x4n*)(base + offa[q]);   // rows past M: zeroed at the store
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
-      const int plane = PLANE_CT ? NT * q / (BN * CPR) : (tid + NT * q) / (BN * CPR);
+      const int plane = PLANE_CT ? NT * q / (BN * CPRB) : (tid + NT * q) / (BN * CPRB);
       const AS1 unsigned char* base = (X6 ? (plane == 0 ? Bh : (plane == 1 ? Bl : B2))
                                           : (plane ? Bl : Bh)) + kb;
       rb[SET][q] = *(const AS1 u32x4n*)(base + offb[q]);
@@ -296,23 +308,25 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
       const int c = tid + NT * q;
-      const int plane = c / (BM * CPR);
+      const int plane = c / (BM * CPRA);
       int row, kof;
-      chunk_rc(c, BM, row, kof);
+      chunk_rc(c, BM, CPRA, ESZA, row, kof);
       const u32x4n v = oka[q] ? ra[SET][q] : z4;
-      if (X6F) store_split((uint16_t*)img + row * LDB16 + x6f_off(row, kof), (long long)BM * LDB16, v);
+      if (X6A) *(u32x4n*)((uint16_t*)img + (plane * BM + row) * LDB16 + x6f_off(row, kof)) = v;
+      else if (SWZ) store_split((uint16_t*)img + row * LDB16 + x6f_off(row, kof), (long long)BM * LDB16, v);
       else if (SPL) *(u32x4n*)((uint16_t*)img + (plane * BM + row) * LDB16 + kof) = v;
       else *(u32x4n*)((float*)img + row * LDF32 + kof) = (row & 16) ? v.zwxy : v;
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
       const int c = tid + NT * q;
-      const int plane = c / (BN * CPR);
+      const int plane = c / (BN * CPRB);
       int row, kof;
-      chunk_rc(c, BN, row, kof);
+      chunk_rc(c, BN, CPRB, ESZB, row, kof);
       const u32x4n v = okb[q] ? rb[SET][q] : z4;
-      if (X6F) store_split((uint16_t*)img + (PL * BM + row) * LDB16 + x6f_off(row, kof),
-                           (long long)BN * LDB16, v);
+      if (X6B) *(u32x4n*)((uint16_t*)img + (PL * BM + plane * BN + row) * LDB16 + x6f_off(row, kof)) = v;
+      else if (SWZ) store_split((uint16_t*)img + (PL * BM + row) * LDB16 + x6f_off(row, kof),
+                                (long long)BN * LDB16, v);
       else if (SPL) *(u32x4n*)((uint16_t*)img + (PL * BM + plane * BN + row) * LDB16 + kof) = v;
       else *(u32x4n*)((float*)img + (BM + row) * LDF32 + kof) = (row & 16) ? v.zwxy : v;
     }
@@ -357,7 +371,7 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
           }
         }
       }
-    } else if constexpr (X6 || X6F) {
+    } else if constexpr (X6 || SWZ) {
       const uint16_t* sA0 = (const uint16_t*)cur;
       const uint16_t* sB0 = sA0 + 3 * BM * LDB16;
 #pragma unroll
@@ -366,7 +380,7 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const int row = brow0 + j * 32 + lr;
-          const int off = row * LDB16 + (X6F ? x6f_off(row, kk * 16 + lh * 8) : kk * 16 + lh * 8);
+          const int off = row * LDB16 + (SWZ ? x6f_off(row, kk * 16 + lh * 8) : kk * 16 + lh * 8);
 #pragma unroll
           for (int p = 0; p < 3; ++p) bp[p][j] = *(const bf16x8_t*)(sB0 + p * BN * LDB16 + off);
         }
@@ -374,7 +388,7 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           const int row = arow0 + i * 32 + lr;
-          const int off = row * LDB16 + (X6F ? x6f_off(row, kk * 16 + lh * 8) : kk * 16 + lh * 8);
+          const int off = row * LDB16 + (SWZ ? x6f_off(row, kk * 16 + lh * 8) : kk * 16 + lh * 8);
 #pragma unroll
           for (int p = 0; p < 3; ++p) ap[p][i] = *(const bf16x8_t*)(sA0 + p * BM * LDB16 + off);
         }
@@ -748,6 +762,12 @@ KFAC_API int kfac_pgemm(int prec, int tile, const void* dev_table, int count, in
     else
       hipLaunchKernelGGL((pgemm_kernel<PREC_BF16X6F, 128, 128, 2, 2, 2>), g, dim3(256), 0, stream,
                          t, count, kl);
+  } else if (prec == PREC_BF16X6A) {
+    hipLaunchKernelGGL((pgemm_kernel<PREC_BF16X6A, 128, 128, 2, 2, 2, false, true>), g, dim3(256),
+                       0, stream, t, count, kl);
+  } else if (prec == PREC_BF16X6B) {
+    hipLaunchKernelGGL((pgemm_kernel<PREC_BF16X6B, 128, 128, 2, 2, 2, false, true>), g, dim3(256),
+                       0, stream, t, count, kl);
   } else if (prec == PREC_F32) {
     KFAC_PGEMM_LAUNCH(PREC_F32)
   } else {

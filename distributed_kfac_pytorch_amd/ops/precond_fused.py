@@ -19,10 +19,12 @@ Precision (`precision=`):
   'bf16x6'  operands as three bf16 planes (hi, mid, lo = the fp32
             significand), six bf16 MFMAs per product (every term above 2^-24
             relative), fp32 accumulation: fp32-level error at the bf16 rate.
-            The operands stay fp32 in memory and are split into the planes
-            while the kernel stages them into LDS (PREC_BF16X6F: 4 bytes per
-            element from L2 / HBM instead of 6, no plane copies);
-            KFAC_X6_PLANES=1 keeps the round-2 plane-stored operands.
+            The eigenvector operands are stored as planes (split once per
+            inverse update); the per-step operands stay fp32 and are split
+            while the kernel stages them into LDS (PREC_BF16X6A / _B): half
+            the k-loop split work of splitting both (PREC_BF16X6F,
+            KFAC_X6_MODE=fp32); KFAC_X6_MODE=planes keeps the round-2
+            all-planes kernel.  All three give bitwise-equal results.
   'fp32'    fp32 operands on the exact f32 MFMA (the reference's fp32 math).
 
 Static GEMM tables (all pointers are arena/buffer pointers that never move)
@@ -44,8 +46,17 @@ __all__ = ['FusedPreconditioner', 'PRECISIONS']
 PRECISIONS = {'fp32': 0, 'bf16x3': 1, 'bf16x6': 2}
 PLANES = {'fp32': 1, 'bf16x3': 2, 'bf16x6': 3}
 PREC_BF16X6F = 3   # csrc/pgemm.h: bf16x6 products on fp32 operands, planes split into LDS
-# KFAC_X6_PLANES=1: the round-2 kernel on plane-stored operands (A/B comparisons)
-X6_PLANES = os.environ.get('KFAC_X6_PLANES') == '1'
+PREC_BF16X6A, PREC_BF16X6B = 4, 5   # one operand (A / B) stored as planes, the other fp32
+# bf16x6 operand storage (same products, same order, bitwise-equal results):
+#   'mixed'  (default) the eigenvector operands QG^T, QA^T, QG, QA as three
+#            bf16 planes, split once per inverse update; the per-step operands
+#            (gathered gradient, intermediates) fp32, split while staged
+#   'fp32'   every operand fp32, split while staged (PREC_BF16X6F, round 3-4)
+#   'planes' every operand as planes (the round-2 kernel)
+# KFAC_X6_MODE selects; KFAC_X6_PLANES=1 is the old spelling of 'planes'
+X6_MODE = os.environ.get('KFAC_X6_MODE') or \
+    ('planes' if os.environ.get('KFAC_X6_PLANES') == '1' else 'mixed')
+X6_PLANES = X6_MODE == 'planes'
 X6_BIG = int(os.environ['KFAC_X6_BIG']) if os.environ.get('KFAC_X6_BIG') else None
 EPI_STORE, EPI_HADAMARD, EPI_HADAMARD_VEC, EPI_FINAL = 0, 1, 2, 3
 TILE = 128        # small tile class (csrc/precond_gemm.hip)
@@ -166,14 +177,15 @@ class _Operand(object):
 
 
 class _LayerBufs(object):
-    def __init__(self, layer, planes, device, inverse=False):
+    def __init__(self, layer, planes, device, inverse=False, q_planes=None):
         self.layer = layer
         nG, nA = layer.grad_shape
         self.nG, self.nA = nG, nA
+        qp = planes if q_planes is None else q_planes     # eigenvector operands
         # inverse path (use_eigen_decomp=False): QGt holds G_inv and QA holds
         # A_inv (both symmetric), V = (G_inv Grad) A_inv in two stages
-        self.QGt = _Operand(nG, nG, planes, device)
-        self.QA = _Operand(nA, nA, planes, device)
+        self.QGt = _Operand(nG, nG, qp, device)
+        self.QA = _Operand(nA, nA, qp, device)
         self.Gct = _Operand(nA, nG, planes, device)
         self.T1 = _Operand(nG, nA, planes, device)
         self.prediv = layer.prediv_eigenvalues and not inverse
@@ -181,8 +193,8 @@ class _LayerBufs(object):
             self.QG = self.QAt = self.T2t = self.T3 = None
             self.Dt = None
             return
-        self.QG = _Operand(nG, nG, planes, device)
-        self.QAt = _Operand(nA, nA, planes, device)
+        self.QG = _Operand(nG, nG, qp, device)
+        self.QAt = _Operand(nA, nA, qp, device)
         self.T2t = _Operand(nA, nG, planes, device)
         self.T3 = _Operand(nG, nA, planes, device)
         self.Dt = torch.zeros(nA, nG, dtype=torch.float32, device=device) if self.prediv else None
@@ -198,14 +210,27 @@ class FusedPreconditioner(object):
         self.prec = PRECISIONS[precision]
         self.x3 = precision == 'bf16x3'
         self.planes = PLANES[precision]
-        # precision of the stored operands (gather / split launches)
-        self.store_prec = self.prec
-        if precision == 'bf16x6' and not X6_PLANES:
+        # precision of the stored operands: the gathered gradient (gather
+        # launch) and the eigenvector operands (split launch)
+        self.store_prec = self.q_store_prec = self.prec
+        q_planes = None
+        # kernel precision per stage: S1-S3 multiply an eigenvector operand
+        # as A, S4 (and the inverse path's second stage) as B
+        self.stage_prec = None
+        if precision == 'bf16x6' and X6_MODE != 'planes':
             self.prec, self.store_prec, self.planes = PREC_BF16X6F, 0, 1
+            self.q_store_prec = 0
+            if X6_MODE == 'mixed':
+                q_planes = PLANES['bf16x6']
+                self.q_store_prec = PRECISIONS['bf16x6']
+                self.stage_prec = (PREC_BF16X6A, PREC_BF16X6A, PREC_BF16X6A, PREC_BF16X6B)
         self.device = self.layers[0].module.weight.device if self.layers else None
         # the damped-inverse path (K9): V = G_inv Grad A_inv, two grouped stages
         self.inverse = bool(self.layers) and not self.layers[0].use_eigen_decomp
-        self.bufs = [_LayerBufs(l, self.planes, self.device, self.inverse) for l in self.layers]
+        if self.inverse and self.stage_prec is not None:
+            self.stage_prec = (PREC_BF16X6A, PREC_BF16X6B)
+        self.bufs = [_LayerBufs(l, self.planes, self.device, self.inverse, q_planes)
+                     for l in self.layers]
         for b in self.bufs:
             _lib.check_pgemm_extent(max(b.nG, b.nA), 'layer')
         self._gather_sig = None
@@ -329,7 +354,7 @@ class FusedPreconditioner(object):
                 add(fjobs, D, _F32Dst(b.Dt), True)
         stream = _lib.stream(self.device)
         L = _lib.lib()
-        for lst, prec in ((jobs, self.store_prec), (fjobs, 0)):
+        for lst, prec in ((jobs, self.q_store_prec), (fjobs, 0)):
             if not lst:
                 continue
             tiles = 0
@@ -404,10 +429,11 @@ class FusedPreconditioner(object):
         final = len(self._stage_tables) - 1
         for i, launches in enumerate(self._stage_tables):
             slot = 1
+            prec = self.prec if self.stage_prec is None else self.stage_prec[i]
             for tile, table, count, tiles in launches:
                 kl = _lib.c_vp(self.kl_buf.data_ptr() + 8 * slot) if (with_kl and i == final) \
                     else None
-                _lib.check(L.kfac_pgemm(self.prec, tile, _lib.ptr(table), count, tiles, kl,
+                _lib.check(L.kfac_pgemm(prec, tile, _lib.ptr(table), count, tiles, kl,
                                         stream), 'kfac_pgemm')
                 slot += tiles
         if with_kl:

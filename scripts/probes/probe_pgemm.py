@@ -63,13 +63,14 @@ for cfg in [int(c) for c in os.environ.get('PGEMM_CFGS', '0,3,5,6,7').split(',')
 pf.TILE_CFG = int(os.environ['TILE_CFG']) if 'TILE_CFG' in os.environ else None
 fz._build_stage_tables()
 tot = timeit(lambda: fz.run(damping=0.001))
-print('%s: full chain %.3f ms  (%.1f GFLOP real, %.1f TFLOP/s)' % (prec, tot, sum(flops) / 1e9, sum(flops) / tot / 1e9))
+print('%s (operands %s): full chain %.3f ms  (%.1f GFLOP real, %.1f TFLOP/s)' % (prec, pf.X6_MODE, tot, sum(flops) / 1e9, sum(flops) / tot / 1e9))
 for i, launches in enumerate(fz._stage_tables):
     def stage(i=i, launches=launches):
         slot = 1
         for tile, table, count, tiles in launches:
             kl = _lib.c_vp(fz.kl_buf.data_ptr() + 8 * slot) if i == 3 else None
-            L.kfac_pgemm(fz.prec, tile, _lib.ptr(table), count, tiles, kl, stream)
+            prec_i = fz.prec if fz.stage_prec is None else fz.stage_prec[i]
+            L.kfac_pgemm(prec_i, tile, _lib.ptr(table), count, tiles, kl, stream)
             slot += tiles
     t = timeit(stage)
     desc = ' '.join('%s:%d' % ('big' if tl else 'small', n) for tl, _, _, n in launches)

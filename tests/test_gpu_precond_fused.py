@@ -127,26 +127,39 @@ def test_fused_kl_matches_reference_dot():
     assert vg.item() > 0
 
 
+@pytest.mark.parametrize('eigen', [False, True])
 @pytest.mark.parametrize('channels_last', [False, True])
-def test_bf16x6_fp32_operands_equal_plane_operands(channels_last, monkeypatch):
-    """The default bf16x6 kernel splits fp32 operands into the three bf16
-    planes while staging them into LDS (PREC_BF16X6F); KFAC_X6_PLANES=1 runs
-    the round-2 kernel on plane-stored operands.  Same split, same products in
-    the same order: the preconditioned gradients are bitwise equal.  Run on
-    the damped-inverse path: its inputs (deterministic SYRK factors, Cholesky
-    inverses) are bitwise reproducible run to run, while the eigensolver's
-    back-transformation sums split-K partials with f32 atomics."""
+def test_bf16x6_operand_storage_modes_bitwise(channels_last, eigen, monkeypatch):
+    """The three bf16x6 operand storages -- 'mixed' (eigenvector operands as
+    stored bf16 planes, per-step operands fp32 split while staged:
+    PREC_BF16X6A / _B, the default), 'fp32' (every operand split while staged,
+    PREC_BF16X6F) and 'planes' (every operand stored as planes, the round-2
+    kernel) -- form the same three planes and the same six products in the
+    same order: the preconditioned gradients are bitwise equal.  Eigen path
+    (bitwise-reproducible eigenvectors, round 4) and damped-inverse path."""
     from distributed_kfac_pytorch_amd.ops import precond_fused
     # and MIOpen's deterministic convolution algorithms: the raw gradients
     # themselves must be equal run to run
     monkeypatch.setattr(torch.backends.cudnn, 'deterministic', True)
     monkeypatch.setattr(torch.backends.cudnn, 'benchmark', False)
-    monkeypatch.setattr(precond_fused, 'X6_PLANES', False)
-    a, pre_a = _grads(True, 'bf16x6', channels_last=channels_last, eigen=False)
-    assert pre_a.fused.prec == precond_fused.PREC_BF16X6F
-    monkeypatch.setattr(precond_fused, 'X6_PLANES', True)
-    b, pre_b = _grads(True, 'bf16x6', channels_last=channels_last, eigen=False)
-    assert pre_b.fused.prec == precond_fused.PRECISIONS['bf16x6']
-    for step, (gs, hs) in enumerate(zip(a, b)):
-        for x, y in zip(gs, hs):
-            assert torch.equal(x, y), (step, (x - y).abs().max())
+    res = {}
+    for mode in ('fp32', 'mixed', 'planes'):
+        monkeypatch.setattr(precond_fused, 'X6_MODE', mode)
+        res[mode], pre = _grads(True, 'bf16x6', channels_last=channels_last, eigen=eigen)
+        want = {'fp32': (precond_fused.PREC_BF16X6F, None),
+                'planes': (precond_fused.PRECISIONS['bf16x6'], None),
+                'mixed': (precond_fused.PREC_BF16X6F,
+                          (precond_fused.PREC_BF16X6A, precond_fused.PREC_BF16X6B))}[mode]
+        assert pre.fused.prec == want[0]
+        if want[1] is not None:
+            assert pre.fused.stage_prec[0] == want[1][0] and pre.fused.stage_prec[-1] == want[1][1]
+    for mode in ('mixed', 'planes'):
+        for step, (gs, hs) in enumerate(zip(res['fp32'], res[mode])):
+            for x, y in zip(gs, hs):
+                if mode == 'planes' and eigen:
+                    # the all-planes kernel reads the KL dot's gradient as
+                    # hi + (mid + lo): a last-bit different clip scale
+                    err = ((x - y).norm() / y.norm().clamp_min(1e-30)).item()
+                    assert err < 1e-6 * 10 ** step, (mode, step, err)
+                else:
+                    assert torch.equal(x, y), (mode, step, (x - y).abs().max())
