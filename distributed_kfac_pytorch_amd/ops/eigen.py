@@ -195,7 +195,7 @@ FUSED_STREAMS = int(os.environ.get('KFAC_EIG_FUSED_STREAMS', '2'))
 FUSED_SPLIT = bool(int(os.environ.get('KFAC_EIG_FUSED_SPLIT', '1')))
 
 
-def _large_fused(mats, clip, stream, use_graph=True):
+def _large_fused(mats, clip, stream, use_graph=True, finite=None):
     """Every factor of the inverse update in ragged launch sequences: per
     group (_fused_groups) the fused one-launch-per-column reduction over all
     its matrices (csrc/eig_reduce.hip), the batched divide and conquer over
@@ -216,7 +216,8 @@ def _large_fused(mats, clip, stream, use_graph=True):
     for s in streams[1:]:
         s.wait_stream(caller)
     for slot, (g, st) in enumerate(zip(groups, streams)):
-        for i, r in zip(g, _fused_group([mats[i] for i in g], clip, st, use_graph, slot)):
+        fl = None if finite is None else [finite[i] for i in g]
+        for i, r in zip(g, _fused_group([mats[i] for i in g], clip, st, use_graph, slot, fl)):
             outs[i] = r
     del _INFOS[:-256]
     for g, st in zip(groups[1:], streams[1:]):
@@ -228,7 +229,7 @@ def _large_fused(mats, clip, stream, use_graph=True):
     return outs
 
 
-def _fused_group(mats, clip, stream, use_graph, slot=0):
+def _fused_group(mats, clip, stream, use_graph, slot=0, finite=None):
     dev = mats[0].device
     L = _lib.lib()
     classes = {}
@@ -248,7 +249,10 @@ def _fused_group(mats, clip, stream, use_graph, slot=0):
             B = _tri_buffers(dev, n, b, slot)     # per group: concurrent groups never share
             bufs.append((n, idx, B))
             for i, m in enumerate(idx):
-                B['A'][i, :n, :n].copy_(mats[m])
+                if finite is None:
+                    B['A'][i, :n, :n].copy_(mats[m])
+                else:
+                    sanitize(mats[m], finite[m], out=B['A'][i, :n, :n])
             dcr = _dc_records(B, n, b)
             for i in range(b):
                 r = rr[k]
@@ -406,15 +410,45 @@ def check_solver_status():
     not in the hot path."""
     global _INFOS
     infos, _INFOS = _INFOS, []
+    if not infos:
+        return
+    flat = torch.cat([i.reshape(-1).to(torch.int64) for i in infos])
+    if not bool((flat != 0).any()):      # one host read for every call
+        return
     bad = [int(i.abs().max().item()) for i in infos if (i != 0).any().item()]
     if bad:
         raise RuntimeError('symmetric eigensolver failed to converge (info={})'.format(bad))
 
 
-def symeig_many(mats, clip=0.0, solver='auto'):
-    """Eigendecompose a list of symmetric fp32 matrices -> list of (Q, d)."""
+_EYES = {}
+
+
+def _eye(n, device):
+    key = (n, str(device))
+    e = _EYES.get(key)
+    if e is None:
+        e = _EYES[key] = torch.eye(n, dtype=torch.float32, device=device)
+    return e
+
+
+def sanitize(A, ok, out=None):
+    """A where the device flag `ok` holds, else the identity (a non-finite
+    factor must not reach the solvers' data-dependent loops, which are not
+    NaN-safe) -- no host read; the caller raises on `ok` later."""
+    return torch.where(ok, A, _eye(A.shape[0], A.device), out=out)
+
+
+def symeig_many(mats, clip=0.0, solver='auto', finite=None):
+    """Eigendecompose a list of symmetric fp32 matrices -> list of (Q, d).
+
+    finite: None, or a device bool tensor (one flag per matrix): a matrix
+    whose flag is False is decomposed as the identity instead (see
+    sanitize); the caller checks the flags after enqueueing its work."""
     if len(mats) == 0:
         return []
+    if finite is not None and not _lib.use_native(mats[0]):
+        mats = [sanitize(A, finite[i]) for i, A in enumerate(mats)]
+        finite = None
     if not _lib.use_native(mats[0]):
         outs = []
         for A in mats:
@@ -426,8 +460,16 @@ def symeig_many(mats, clip=0.0, solver='auto'):
         return outs
     if solver not in ('auto', 'jacobi'):
         raise ValueError("solver must be 'auto' or 'jacobi', got {!r}".format(solver))
+    if finite is not None:
+        # paths other than the fused one-stage group take sanitised copies
+        def _clean(idx):
+            for i in idx:
+                mats[i] = sanitize(mats[i], finite[i])
+        mats = list(mats)
     huge = [i for i, A in enumerate(mats) if A.shape[0] > FUSED_MAX_N]
     if huge:
+        if finite is not None:
+            _clean(range(len(mats)))
         return _with_huge(mats, huge, clip, solver)
     nmax = max(A.shape[0] for A in mats)
     _lib.check_pgemm_extent(nmax)
@@ -439,6 +481,8 @@ def symeig_many(mats, clip=0.0, solver='auto'):
     lim = SMALL_N if solver == 'jacobi' else 1
     small = [i for i, A in enumerate(mats) if A.shape[0] <= lim]
     large = [i for i, A in enumerate(mats) if A.shape[0] > lim]
+    if finite is not None:
+        _clean(small)
     outs = [None] * len(mats)
     if small:
         for i, r in zip(small, _jacobi_small([mats[i] for i in small], clip)):
@@ -449,6 +493,8 @@ def symeig_many(mats, clip=0.0, solver='auto'):
         if TWO_STAGE_COUNT > 0:
             ts = sorted(ts, key=lambda i: -mats[i].shape[0])[:TWO_STAGE_COUNT]
         large = [i for i in large if i not in set(ts)]
+        if finite is not None:
+            _clean(ts)
     cur = torch.cuda.current_stream(mats[0].device)
     side = None
     if ts:
@@ -463,7 +509,8 @@ def symeig_many(mats, clip=0.0, solver='auto'):
             outs[i] = r
     if large:
         sub = [mats[i] for i in large]
-        res = _large_fused(sub, clip, cur)
+        res = _large_fused(sub, clip, cur,
+                           finite=None if finite is None else [finite[i] for i in large])
         for A in sub:
             A.record_stream(cur)
         for i, r in zip(large, res):

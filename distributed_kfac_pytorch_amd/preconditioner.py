@@ -67,21 +67,28 @@ def _debug_check_eig(jobs, mats, results):
                 layer, which, A.shape[0], fin, bool(torch.isfinite(A).all()), res), flush=True)
 
 
-def _check_factors_finite(jobs, mats):
-    """Raise on a non-finite factor before it reaches the eigensolvers: an
-    inverse update over NaN factors ended in an illegal-address GPU fault
-    instead of an error (the data-dependent deflation / iteration logic of the
-    solvers is not NaN-safe).  One multi-tensor norm and one host read per
-    inverse update."""
-    if not mats:
-        return
-    norms = torch.stack(torch._foreach_norm(mats, 1))
-    ok = torch.isfinite(norms)
+def _factors_finite(mats):
+    """Device flags, one per factor: finite (one multi-tensor norm, no host
+    read).  An inverse update over NaN factors once ended in an
+    illegal-address GPU fault instead of an error (the solvers' data-dependent
+    deflation / iteration logic is not NaN-safe): a flagged factor reaches the
+    solvers as the identity (eigen.sanitize) and _raise_nonfinite raises after
+    the step's work is enqueued."""
+    return torch.isfinite(torch.stack(torch._foreach_norm(mats, 1)))
+
+
+def _raise_nonfinite(jobs, ok):
     if bool(ok.all()):
         return
     bad = ['{} {}'.format(l, w) for (l, w), f in zip(jobs, ok.tolist()) if not f]
     raise FloatingPointError('non-finite K-FAC factor(s) at an inverse update: {}'.format(
         ', '.join(bad[:8])))
+
+
+def _check_factors_finite(jobs, mats):
+    """Raise on a non-finite factor now (one host read)."""
+    if mats:
+        _raise_nonfinite(jobs, _factors_finite(mats))
 
 
 class CommMethod(enum.Enum):
@@ -247,6 +254,8 @@ class KFAC(optim.Optimizer):
         self.eigen_solver = eigen_solver
         # host-checks the eigensolver status once per inverse step (one sync)
         self.check_solver = True
+        self._solver_check_due = False
+        self._deferred_checks = []
         # debug mode: checksum-compare the buffers each collective phase must
         # leave identical on every rank (utils/comm_check.py)
         self.comm_check = bool(comm_check) or \
@@ -800,7 +809,7 @@ class KFAC(optim.Optimizer):
                     self._launch_lagged_inverses(p['damping'])
             else:
                 with t('inverses'):
-                    self.compute_inverses(damping=p['damping'])
+                    self.compute_inverses(damping=p['damping'], defer_check=True)
                 if self.comm_method in (CommMethod.COMM_OPT, CommMethod.HYBRID_OPT):
                     with t('inverse_comm'):
                         self.broadcast_inverses()
@@ -821,6 +830,7 @@ class KFAC(optim.Optimizer):
             with t('update'):
                 scale = None if p['kl_clip'] is None else self._compute_grad_scale()
                 self.update_gradients(scale)
+        self._finish_solver_check()
         p['step'] += 1
         self._close_forward_count()
         return loss
@@ -927,9 +937,13 @@ class KFAC(optim.Optimizer):
         sig = self._graph_signature()
         if self._graph is not None and sig == self._graph_sig:
             if self._sync_before_replay:
-                # new eigendata came from side streams this step: drain them
-                # before the replay (see graphs.GraphedTrainStep)
-                torch.cuda.synchronize()
+                # new eigendata came from side streams this step: order the
+                # replay after them on the device (event waits, no host sync:
+                # the host keeps issuing while the eigensolver runs)
+                cur = torch.cuda.current_stream()
+                for st in self.side_streams():
+                    if st != cur:
+                        cur.wait_stream(st)
                 self._sync_before_replay = False
             self._graph.replay()
             return
@@ -1033,9 +1047,10 @@ class KFAC(optim.Optimizer):
                     jobs.append((layer, which))
         return jobs
 
-    def _solve_inverses(self, jobs, mats, damping):
+    def _solve_inverses(self, jobs, mats, damping, finite=None):
         if self.use_eigen_decomp:
-            results = eigen_ops.symeig_many(mats, clip=0.0, solver=self.eigen_solver)
+            results = eigen_ops.symeig_many(mats, clip=0.0, solver=self.eigen_solver,
+                                            finite=finite)
             if _DEBUG_EIG:
                 _debug_check_eig(jobs, mats, results)
             return [(Q.to(l.inv_dtype), d.to(l.inv_dtype))
@@ -1050,8 +1065,13 @@ class KFAC(optim.Optimizer):
             layer.finish_inverse(which, res, damping)
 
     @torch.no_grad()
-    def compute_inverses(self, damping=0.001):
-        """Eigendecompose / invert every factor this rank owns, in one batch."""
+    def compute_inverses(self, damping=0.001, defer_check=False):
+        """Eigendecompose / invert every factor this rank owns, in one batch.
+
+        defer_check (step()): the solver-status check -- a host read that waits
+        for the whole solve -- runs at the end of step(), after the eigendata
+        store, the preconditioning and the gradient update are enqueued behind
+        the solve, so the device never idles while the host issues them."""
         self._drop_lagged_inverses()
         self.join_factor_comm()
         jobs = self._inverse_jobs()
@@ -1059,11 +1079,31 @@ class KFAC(optim.Optimizer):
         if not jobs:
             return
         mats = [l.state[w].to(torch.float32) for l, w in jobs]
-        _check_factors_finite(jobs, mats)
-        results = self._solve_inverses(jobs, mats, damping)
+        if defer_check and self.use_eigen_decomp and mats[0].is_cuda:
+            # no host read before the solve: flagged factors are solved as the
+            # identity and the flags are checked at the end of step()
+            finite = _factors_finite(mats)
+            results = self._solve_inverses(jobs, mats, damping, finite)
+            self._deferred_checks.append((jobs, finite))
+        else:
+            _check_factors_finite(jobs, mats)
+            results = self._solve_inverses(jobs, mats, damping)
         if self.use_eigen_decomp and self.check_solver:
-            eigen_ops.check_solver_status()
+            if defer_check:
+                self._solver_check_due = True
+            else:
+                eigen_ops.check_solver_status()
         self._store_inverses(jobs, results, damping)
+
+    def _finish_solver_check(self):
+        """The host reads step() deferred past its enqueued work: non-finite
+        factors of this step's inverse update, then the solver status."""
+        checks, self._deferred_checks = self._deferred_checks, []
+        for jobs, finite in checks:
+            _raise_nonfinite(jobs, finite)
+        if self._solver_check_due:
+            self._solver_check_due = False
+            eigen_ops.check_solver_status()
 
     # ------------------------------------------------------ lagged inverses
     # inverse_lag = L > 0 (opt-in; 0 is the reference's synchronous schedule,

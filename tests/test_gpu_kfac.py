@@ -100,3 +100,40 @@ def test_gpu_inverse_many_size_classes():
         M = A.double() + 0.003 * torch.eye(A.shape[0], device=dev, dtype=torch.float64)
         ref = torch.linalg.inv(M)
         assert (out.double() - ref).norm() / ref.norm() < 1e-4
+
+
+def test_gpu_nonfinite_factor_raises_after_enqueue():
+    """A NaN factor at an inverse step: no host read before the solve (the
+    factor reaches the solvers as the identity, eigen.sanitize), no device
+    fault, and step() still raises FloatingPointError -- after the step's work
+    is enqueued (KFAC._finish_solver_check) -- naming the factor; the next
+    inverse update with finite factors is clean again."""
+    torch.manual_seed(0)
+    model = SmallNet().cuda()
+    pre = kfac.KFAC(model, factor_update_freq=1, inv_update_freq=2, lr=0.05, damping=0.003,
+                    use_hip_graphs=False)
+    opt = torch.optim.SGD(model.parameters(), lr=0.05, momentum=0.9)
+    x = torch.randn(8, 3, 8, 8, device='cuda')
+    y = torch.randint(0, 10, (8,), device='cuda')
+
+    def step():
+        opt.zero_grad()
+        nn.functional.cross_entropy(model(x), y).backward()
+        pre.step()
+
+    step()                                    # step 0: inverse update, finite
+    step()                                    # step 1: plain
+    layer = pre.layers[1]
+    saved = layer.state['A'].clone()
+    pre.compute_factor_in_hook = True         # keep the poisoned factor (no EMA in step())
+    layer.state['A'].fill_(float('nan'))
+    with pytest.raises(FloatingPointError, match='non-finite'):
+        step()                                # step 2: inverse update over the NaN factor
+    torch.cuda.synchronize()
+    layer.state['A'].copy_(saved)
+    pre.compute_factor_in_hook = False
+    pre.param_groups[0]['step'] = 4
+    step()                                    # step 4: inverse update, finite again
+    torch.cuda.synchronize()
+    for p in model.parameters():
+        assert torch.isfinite(p.grad).all()
