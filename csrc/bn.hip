@@ -28,8 +28,6 @@
 // Layout: x[m * C + c], m < M = N H W, C % 8 == 0, 16-byte aligned rows.
 #include "common.h"
 
-#include <cstdlib>
-
 namespace {
 
 typedef unsigned u32x4n __attribute__((ext_vector_type(4)));
@@ -421,229 +419,12 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(
   }
 }
 
-// ------------------------------------------------ small layers: one launch
-// For small M (ResNet-50's layer4 at batch 32: M = 1568) the three launches
-// of each direction are launch / latency bound (~20-25 us per BN layer for a
-// few MB).  Here one workgroup owns a channel group of width cb for ALL M
-// rows: pass 1 reduces the statistics inside the workgroup (lanes of one
-// channel vector sum their rows, a fixed-order xor butterfly over the wave,
-// then the waves in order), pass 2 normalises (forward) or forms dx
-// (backward) re-reading its rows from L2 -- one launch, no cross-workgroup
-// reduction, deterministic.
-struct SmallGeo { int cb, tpr, rpi; };
-
-SmallGeo small_geometry(int C) {
-  SmallGeo g;
-  // >= 64 workgroups where the channels allow it, 16-byte vectors
-  g.cb = 8;
-  while (C / (2 * g.cb) >= 64 && g.cb < 64 && C % (2 * g.cb) == 0) g.cb *= 2;
-  g.tpr = g.cb / 8;
-  g.rpi = NT / g.tpr;
-  return g;
-}
-
-// sum of v over the lanes of this wave with the same (lane % tpr), fixed
-// xor-butterfly order; every such lane ends with the wave sum
-__device__ __forceinline__ float wave_sum_stride(float v, int tpr) {
-  for (int off = tpr; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-
-// acc[16] of every thread -> tot[16] (fp64) for this thread's channel vector:
-// wave butterflies, then the NT/64 wave partials in wave order
-__device__ __forceinline__ void small_block_sum16(const float* acc, double* tot, int cv, int tpr,
-                                                  double (*sh)[8][16]) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float ws[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) ws[i] = wave_sum_stride(acc[i], tpr);
-  if (lane < tpr) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) sh[w][lane][i] = (double)ws[i];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    double t = 0.0;
-#pragma unroll
-    for (int q = 0; q < NT / 64; ++q) t += sh[q][cv][i];
-    tot[i] = t;
-  }
-}
-
-template <bool RELU, bool ADD>
-__global__ __launch_bounds__(NT) void bn_small_fwd_kernel(
-    const uint16_t* __restrict__ x, const uint16_t* __restrict__ z, long long M, int C, SmallGeo g,
-    float eps, float momentum, const float* __restrict__ w, const float* __restrict__ b,
-    float* __restrict__ rmean, float* __restrict__ rvar, long long* __restrict__ nbt,
-    uint16_t* __restrict__ y, float* __restrict__ save_mean, float* __restrict__ save_invstd) {
-  __shared__ double sh[NT / 64][8][16];
-  const int t = threadIdx.x, cv = t % g.tpr, rr = t / g.tpr;
-  const int c0 = blockIdx.x * g.cb + cv * 8;
-  if (blockIdx.x == 0 && t == 0 && nbt != nullptr) nbt[0] += 1;
-  const AS1 u32x4n* X = (const AS1 u32x4n*)x;
-  const long long cs = (long long)C / 8, step = (long long)g.rpi * cs;
-  float k[8];
-  unpack8(X[c0 / 8], k);                 // shift: row 0
-  float acc[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-  long long m = rr;
-  const AS1 u32x4n* Xp = X + (m * C + c0) / 8;
-  for (; m + 3 * g.rpi < M; m += 4 * g.rpi, Xp += 4 * step) {
-    u32x4n q[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) q[u] = Xp[u * step];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      float f[8];
-      unpack8(q[u], f);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float d = f[i] - k[i];
-        acc[i] += d;
-        acc[8 + i] = fmaf(d, d, acc[8 + i]);
-      }
-    }
-  }
-  for (; m < M; m += g.rpi, Xp += step) {
-    float f[8];
-    unpack8(*Xp, f);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float d = f[i] - k[i];
-      acc[i] += d;
-      acc[8 + i] = fmaf(d, d, acc[8 + i]);
-    }
-  }
-  double tot[16];
-  small_block_sum16(acc, tot, cv, g.tpr, sh);
-  float sc[8], shf[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const double s1 = tot[i], s2 = tot[8 + i];
-    const double mean = (double)k[i] + s1 / (double)M;
-    const double m2 = fmax(s2 - s1 * (s1 / (double)M), 0.0);
-    const double var = m2 / (double)M;
-    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-    const int c = c0 + i;
-    sc[i] = (w ? w[c] : 1.f) * invstd;
-    shf[i] = (b ? b[c] : 0.f) - (float)mean * sc[i];
-    if (rr == 0) {
-      save_mean[c] = (float)mean;
-      save_invstd[c] = invstd;
-      if (rmean != nullptr) {
-        const double unb = M > 1 ? m2 / (double)(M - 1) : var;
-        rmean[c] = (float)((1.0 - momentum) * (double)rmean[c] + momentum * mean);
-        rvar[c] = (float)((1.0 - momentum) * (double)rvar[c] + momentum * unb);
-      }
-    }
-  }
-  const AS1 u32x4n* Z = (const AS1 u32x4n*)z;
-  AS1 u32x4n* Y = (AS1 u32x4n*)y;
-  for (long long mm = rr; mm < M; mm += g.rpi)
-    apply8<RELU, ADD>(X, Z, Y, (mm * C + c0) / 8, sc, shf);
-}
-
-template <bool RELU, bool ADD>
-__global__ __launch_bounds__(NT) void bn_small_bwd_kernel(
-    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y, const uint16_t* __restrict__ x,
-    const float* __restrict__ w, const float* __restrict__ mean, const float* __restrict__ invstd,
-    long long M, int C, SmallGeo g, uint16_t* __restrict__ dx, uint16_t* __restrict__ dz,
-    float* __restrict__ dw, float* __restrict__ db) {
-  __shared__ double sh[NT / 64][8][16];
-  const int t = threadIdx.x, cv = t % g.tpr, rr = t / g.tpr;
-  const int c0 = blockIdx.x * g.cb + cv * 8;
-  const AS1 u32x4n* DY = (const AS1 u32x4n*)dy;
-  const AS1 u32x4n* Y = (const AS1 u32x4n*)y;
-  const AS1 u32x4n* X = (const AS1 u32x4n*)x;
-  float mu[8], is[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) { mu[i] = mean[c0 + i]; is[i] = invstd[c0 + i]; }
-  float acc[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-  const long long step = (long long)g.rpi * (C / 8);
-  long long m = rr, v = (m * C + c0) / 8;
-  for (; m + g.rpi < M; m += 2 * g.rpi, v += 2 * step) {
-    u32x4n qg[2], qx[2], qy[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      qg[u] = DY[v + u * step];
-      qx[u] = X[v + u * step];
-      if (RELU) qy[u] = Y[v + u * step];
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      float gv[8], xv[8], yv[8];
-      unpack8(qg[u], gv);
-      unpack8(qx[u], xv);
-      if (RELU) unpack8(qy[u], yv);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float gg = (!RELU || yv[i] > 0.f) ? gv[i] : 0.f;
-        acc[i] += gg;
-        acc[8 + i] = fmaf(gg, (xv[i] - mu[i]) * is[i], acc[8 + i]);
-      }
-    }
-  }
-  for (; m < M; m += g.rpi, v += step) {
-    float gv[8], xv[8], yv[8];
-    unpack8(DY[v], gv);
-    unpack8(X[v], xv);
-    if (RELU) unpack8(Y[v], yv);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float gg = (!RELU || yv[i] > 0.f) ? gv[i] : 0.f;
-      acc[i] += gg;
-      acc[8 + i] = fmaf(gg, (xv[i] - mu[i]) * is[i], acc[8 + i]);
-    }
-  }
-  double tot[16];
-  small_block_sum16(acc, tot, cv, g.tpr, sh);
-  float ca[8], cb[8], cx[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int c = c0 + i;
-    const double sg = tot[i], sgx = tot[8 + i];
-    if (rr == 0) {
-      if (dw) dw[c] = (float)sgx;
-      if (db) db[c] = (float)sg;
-    }
-    // the affine (A, B, X) of bn_bwd_finalize_kernel
-    const double a = (double)(w ? w[c] : 1.f) * (double)is[i];
-    const double k1 = sg / (double)M, k2 = sgx / (double)M;
-    const double ak = a * k2 * (double)is[i];
-    ca[i] = (float)a;
-    cb[i] = (float)(ak * (double)mu[i] - a * k1);
-    cx[i] = (float)(-ak);
-  }
-  AS1 u32x4n* DX = (AS1 u32x4n*)dx;
-  AS1 u32x4n* DZ = (AS1 u32x4n*)dz;
-  for (long long mm = rr; mm < M; mm += g.rpi)
-    bwd_apply8<RELU, ADD>(DY, Y, X, DX, DZ, (mm * C + c0) / 8, ca, cb, cx);
-}
-
-// the one-launch path for M <= this (KFAC_BN_SMALL_M, kfac_bn_set_small_m)
-long long g_bn_small_m = [] {
-  const char* e = getenv("KFAC_BN_SMALL_M");
-  return e ? atoll(e) : 2048LL;
-}();
-
 int apply_grid(long long nvec) {
   long long b = (nvec + NT - 1) / NT;
   return (int)(b < 8192 ? (b > 0 ? b : 1) : 8192);
 }
 
 }  // namespace
-
-// rows up to which a BN call takes the one-launch path (0: never); returns
-// the previous value (tests compare both paths)
-KFAC_API long long kfac_bn_set_small_m(long long m) {
-  const long long prev = g_bn_small_m;
-  g_bn_small_m = m;
-  return prev;
-}
 
 // workspace floats of one BN call: chunk partials (2 per channel per chunk)
 // + scale/shift (forward) or the dx coefficients (backward)
@@ -659,22 +440,6 @@ KFAC_API int kfac_bn_forward(const void* x, const void* z, const float* w, const
   if (C % 8 || M <= 0 || ((uintptr_t)x & 15) || ((uintptr_t)y & 15) ||
       (z && ((uintptr_t)z & 15)))
     return -2;
-  if (M <= g_bn_small_m) {
-    const SmallGeo sg = small_geometry(C);
-    const dim3 grid(C / sg.cb);
-    const uint16_t* X = (const uint16_t*)x;
-    const uint16_t* Z = (const uint16_t*)z;
-    uint16_t* Y = (uint16_t*)y;
-#define KFAC_BN_SMALL_FWD(R, A)                                                                    \
-    hipLaunchKernelGGL((bn_small_fwd_kernel<R, A>), grid, dim3(NT), 0, stream, X, Z, M, C, sg, eps, \
-                       momentum, w, b, rmean, rvar, nbt, Y, save_mean, save_invstd)
-    if (relu && z) KFAC_BN_SMALL_FWD(true, true);
-    else if (relu) KFAC_BN_SMALL_FWD(true, false);
-    else if (z) KFAC_BN_SMALL_FWD(false, true);
-    else KFAC_BN_SMALL_FWD(false, false);
-#undef KFAC_BN_SMALL_FWD
-    return (int)hipGetLastError();
-  }
   const Geo g = geometry(M, C);
   float* part = ws;
   float* scale = ws + 2LL * g.nchunks * C;
@@ -707,24 +472,6 @@ KFAC_API int kfac_bn_backward(const void* dy, const void* y, const void* x, cons
   if (C % 8 || M <= 0 || ((uintptr_t)dy & 15) || ((uintptr_t)x & 15) || ((uintptr_t)dx & 15) ||
       (relu && ((uintptr_t)y & 15)) || (dz && ((uintptr_t)dz & 15)))
     return -2;
-  if (M <= g_bn_small_m) {
-    const SmallGeo sg = small_geometry(C);
-    const dim3 grid(C / sg.cb);
-    const uint16_t* DY = (const uint16_t*)dy;
-    const uint16_t* Y = (const uint16_t*)y;
-    const uint16_t* X = (const uint16_t*)x;
-    uint16_t* DX = (uint16_t*)dx;
-    uint16_t* DZ = (uint16_t*)dz;
-#define KFAC_BN_SMALL_BWD(R, A)                                                                     \
-    hipLaunchKernelGGL((bn_small_bwd_kernel<R, A>), grid, dim3(NT), 0, stream, DY, Y, X, w,          \
-                       save_mean, save_invstd, M, C, sg, DX, DZ, dw, db)
-    if (relu && dz) KFAC_BN_SMALL_BWD(true, true);
-    else if (relu) KFAC_BN_SMALL_BWD(true, false);
-    else if (dz) KFAC_BN_SMALL_BWD(false, true);
-    else KFAC_BN_SMALL_BWD(false, false);
-#undef KFAC_BN_SMALL_BWD
-    return (int)hipGetLastError();
-  }
   const Geo g = geometry(M, C);
   float* part = ws;
   float* coef = ws + 2LL * g.nchunks * C;

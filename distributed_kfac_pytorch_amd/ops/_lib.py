@@ -146,7 +146,6 @@ _SIGS = {
     'kfac_dc_ws_bytes': [c_int],
     'kfac_dc_info_offset': [c_int],
     'kfac_bn_ws_floats': [c_ll, c_int],
-    'kfac_bn_set_small_m': [c_ll],
     'kfac_bn_forward': [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll,
                         c_int, ctypes.c_float, ctypes.c_float, c_int, c_vp],
     'kfac_bn_backward': [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll,
@@ -158,8 +157,7 @@ _RESTYPES = {'kfac_dc_ws_bytes': c_ll, 'kfac_sy2sb_ws_floats': c_ll,
              'kfac_reduce_ws_floats': c_ll, 'kfac_syrk_splits': c_ll,
              'kfac_chol_ws_bytes': c_ll, 'kfac_chol_info_offset': c_ll,
              'kfac_syrk_problem_set_part': None, 'kfac_syrk_problem_set_dscale': None,
-             'kfac_bn_ws_floats': c_ll, 'kfac_event_create': c_vp,
-             'kfac_bn_set_small_m': c_ll}
+             'kfac_bn_ws_floats': c_ll, 'kfac_event_create': c_vp}
 
 
 def _load():

@@ -7,10 +7,7 @@ optional) with the semantics of `nn.BatchNorm2d` in training mode: batch
 statistics (biased variance) normalise, the running statistics move by
 `momentum` with the unbiased variance, `num_batches_tracked` counts the call.
 On a GPU, for a bf16 channels_last input with C % 8 == 0, it is three
-kernels forward and three backward (hipGraph-capturable, deterministic), or
-ONE each way for small layers (M = N H W <= 2048 rows, ResNet-50's layer4 at
-batch 32: a workgroup per channel group reduces and normalises all rows
-itself, `set_small_m`);
+kernels forward and three backward (hipGraph-capturable, deterministic);
 anything else (CPU, eval mode, fp32, other layouts, momentum=None) takes the
 stock `bn(x)` path.  `KFAC_FUSED_BN=0` disables the fused kernels.
 
@@ -25,7 +22,7 @@ import torch.nn.functional as F
 
 from . import _lib
 
-__all__ = ['bn_act', 'eligible', 'ENABLED', 'set_small_m']
+__all__ = ['bn_act', 'eligible', 'ENABLED']
 
 ENABLED = os.environ.get('KFAC_FUSED_BN', '1') != '0'
 
@@ -46,12 +43,6 @@ def eligible(x, bn, z=None):
     if z is not None and (z.dtype != x.dtype or z.shape != x.shape or not _nhwc(z)):
         return False
     return True
-
-
-def set_small_m(m):
-    """Rows (N H W) up to which a call takes the one-launch kernels (0:
-    never); returns the previous threshold."""
-    return int(_lib.lib().kfac_bn_set_small_m(int(m)))
 
 
 def _ptr(t):
