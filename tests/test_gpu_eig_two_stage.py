@@ -40,6 +40,27 @@ def test_two_stage_matches_fp64(sizes):
         torch.cuda.synchronize()
         for A64, (Q, d) in zip(mats64, outs):
             _check(A64, Q, d)
+        # the bulge-chasing status word (timed-out waits) and the D&C infos
+        # are all zero: check_solver_status raises otherwise
+        eigen.check_solver_status()
+
+
+def test_two_stage_status_reaches_the_host():
+    """A nonzero bulge-chasing status (a bounded wait that timed out: the
+    band reduction's output is garbage) makes check_solver_status raise --
+    simulated by writing the status word the launch reports."""
+    A = _factor(200, 3).float()
+    eigen.two_stage_eigh([A])
+    torch.cuda.synchronize()
+    eigen.check_solver_status()                    # healthy run: no raise
+    eigen.two_stage_eigh([A])
+    bufs = [b for k, b in eigen._TS_BUFS.items() if k[1] == 200]
+    assert bufs and 'sbstat' in bufs[0]
+    torch.cuda.synchronize()
+    # the status the launch reported sits in _INFOS (a clone of sbstat)
+    eigen._INFOS[-2].fill_(3)
+    with pytest.raises(RuntimeError, match='failed to converge'):
+        eigen.check_solver_status()
 
 
 def test_two_stage_4608():
