@@ -75,25 +75,35 @@ Geo geometry(long long M, int C) {
 }
 
 // sums over this block's chunk of rows for 8 channels per thread, reduced
-// over the block's row lanes into the lanes of row 0 (fixed order)
-__device__ __forceinline__ void block_reduce16(float* acc, float (*red)[17], int rr, int cv,
-                                               int tpr, int rpi) {
-  const int t = rr * tpr + cv;
+// over the block's row lanes into the lanes of row 0 (fixed order).
+// Lanes of one wave that share a channel octet (lane % tpr) are folded by xor
+// shuffles at distances tpr .. 32 (every lane ends with its octet's wave sum),
+// then the four wave sums are added in wave order through LDS.  The round-4
+// form -- every row's 16 sums through LDS, then the row-0 lanes adding all
+// rpi rows one after another (31 dependent LDS steps at 64 channels) -- held
+// the C = 64 statistics launches at ~15 us for 13 MB.
+__device__ __forceinline__ void block_reduce16(float* acc, float (*red)[32][17], int cv, int tpr) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int d = tpr; d < 64; d <<= 1) {
 #pragma unroll
-  for (int i = 0; i < 16; ++i) red[t][i] = acc[i];
+    for (int i = 0; i < 16; ++i) acc[i] += __shfl_xor(acc[i], d, 64);
+  }
+  if (lane < tpr) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) red[w][lane][i] = acc[i];
+  }
   __syncthreads();
-  if (rr == 0) {
-    for (int q = 1; q < rpi; ++q) {
+  if (w == 0 && lane < tpr) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[i] += red[q * tpr + cv][i];
-    }
+    for (int i = 0; i < 16; ++i)
+      acc[i] = (red[0][cv][i] + red[1][cv][i]) + (red[2][cv][i] + red[3][cv][i]);
   }
 }
 
 // ---------------------------------------------------------------- forward
 __global__ __launch_bounds__(NT) void bn_stats_kernel(const uint16_t* __restrict__ x, long long M,
                                                       int C, Geo g, float* __restrict__ part) {
-  __shared__ float red[NT][17];
+  __shared__ float red[NT / 64][32][17];
   const int cg = blockIdx.x, chunk = blockIdx.y;
   const int t = threadIdx.x, cv = t % g.tpr, rr = t / g.tpr;
   const int c0 = cg * g.cb + cv * 8;
@@ -136,7 +146,7 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(const uint16_t* __restrict
       acc[8 + i] = fmaf(d, d, acc[8 + i]);
     }
   }
-  block_reduce16(acc, red, rr, cv, g.tpr, g.rpi);
+  block_reduce16(acc, red, cv, g.tpr);
   if (rr == 0) {
     const float n = (float)(m1 - m0);
     // channel-major partials [c][chunk][2]: the finalize wave of a channel
@@ -272,7 +282,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
     const uint16_t* __restrict__ x, const float* __restrict__ mean,
     const float* __restrict__ invstd, long long M, int C, Geo g, float* __restrict__ part) {
-  __shared__ float red[NT][17];
+  __shared__ float red[NT / 64][32][17];
   const int cg = blockIdx.x, chunk = blockIdx.y;
   const int t = threadIdx.x, cv = t % g.tpr, rr = t / g.tpr;
   const int c0 = cg * g.cb + cv * 8;
@@ -324,7 +334,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(
       acc[8 + i] = fmaf(gg, (xv[i] - mu[i]) * is[i], acc[8 + i]);
     }
   }
-  block_reduce16(acc, red, rr, cv, g.tpr, g.rpi);
+  block_reduce16(acc, red, cv, g.tpr);
   if (rr == 0) {
     AS1 float* o = gptr(part) + ((long long)c0 * g.nchunks + chunk) * 2;   // [c][chunk][2]
 #pragma unroll
