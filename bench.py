@@ -300,7 +300,10 @@ def main():
                                        post_update=weights.master_to_model
                                        if weights is not None else None)
     else:
-        step = graphs.GraphedTrainStep(train_step, pre, [opt], enabled=use_graphs)
+        # forward_backward / update as well: inverse steps replay a forward/
+        # backward graph (factors in its captured hooks), only the update is eager
+        step = graphs.GraphedTrainStep(train_step, pre, [opt], enabled=use_graphs,
+                                       forward_backward=forward_backward, update=update)
 
     for _ in range(args.warmup):
         step()

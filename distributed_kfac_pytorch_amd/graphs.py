@@ -14,7 +14,10 @@ compiler):
             broadcast) and the very first steps        -> the update runs
             eagerly; once the factor-step forward/backward graphs exist an
             inverse step replays them (it is a factor step too) and only
-            the update is eager
+            the update is eager.  A single-segment trainer given
+            `forward_backward` and `update` as well replays a forward/backward
+            graph of its own on inverse steps (factors inside the captured
+            hooks, KFAC.hook_factors) instead of running them eagerly
 
 Two modes:
   single-segment  `step_fn` does everything (one process): one graph per kind.
@@ -70,6 +73,7 @@ Eager steps and replays run on one side stream, joined to the caller's
 stream by events; the device is synchronised once after each eager
 (inverse-update) step, which also drains the eigensolver's worker streams.
 """
+import contextlib
 import gc
 import warnings
 
@@ -106,6 +110,12 @@ class GraphedTrainStep(object):
         # (e.g. ops/mixed.BF16Weights.master_to_model)
         self.post_update = post_update
         self.segmented = step_fn is None
+        # single-segment trainer that also names its forward/backward and
+        # update: inverse steps replay an 'invfb' graph + the eager update
+        self.hybrid = (not self.segmented and forward_backward is not None
+                       and update is not None and preconditioner is not None
+                       and not isinstance(forward_backward, (list, tuple))
+                       and hasattr(preconditioner, 'hook_factors'))
         self.pre = preconditioner
         if self.segmented and preconditioner is not None:
             # no side-stream fork may span the fb / update graph boundary
@@ -205,7 +215,7 @@ class GraphedTrainStep(object):
         preconditioning, optimizer) then runs eagerly.  Needs every factor fb
         segment captured already, workers assigned and no lagged solve due."""
         pre = self.pre
-        if not (self.graph_inverse_fb and self.segmented and pre is not None
+        if not (self.graph_inverse_fb and (self.segmented or self.hybrid) and pre is not None
                 and pre.workers_assigned):
             return False
         p = pre.param_groups[0]
@@ -213,6 +223,8 @@ class GraphedTrainStep(object):
             return False
         if getattr(pre, 'inverse_apply_due', None) is not None and pre.inverse_apply_due():
             return False
+        if self.hybrid:
+            return True      # its own 'invfb' graph: warmed up / captured on the way
         return all(self._key('fb' if i == 0 else 'fb%d' % i, 'factor') in self.graphs
                    for i in range(len(self.fbs)))
 
@@ -261,19 +273,20 @@ class GraphedTrainStep(object):
         if self.enabled and kind == 'eager' and self._inverse_fb_graphed():
             self.eager_steps += 1
             self._prepare_factor()
-            loss = None
-            for i, (fb, cm) in enumerate(zip(self.fbs, self.comms)):
-                out = self._run_segment('fb' if i == 0 else 'fb%d' % i, 'factor', fb,
-                                        advances=False)
-                if i == 0:
-                    loss = out
-                if cm is not None:
-                    cm()
-            cur = torch.cuda.current_stream()
-            self.side.wait_stream(cur)
-            with torch.cuda.stream(self.side):
-                self.update()
-            cur.wait_stream(self.side)
+            with (self.pre.hook_factors() if self.hybrid else contextlib.nullcontext()):
+                loss = None
+                for i, (fb, cm) in enumerate(zip(self.fbs, self.comms)):
+                    seg = 'invfb' if self.hybrid else ('fb' if i == 0 else 'fb%d' % i)
+                    out = self._run_segment(seg, 'factor', fb, advances=False)
+                    if i == 0:
+                        loss = out
+                    if cm is not None:
+                        cm()
+                cur = torch.cuda.current_stream()
+                self.side.wait_stream(cur)
+                with torch.cuda.stream(self.side):
+                    self.update()
+                cur.wait_stream(self.side)
             self._join_side_streams()
             return loss
         if not self.enabled or kind == 'eager':
@@ -436,5 +449,11 @@ class GraphedTrainStep(object):
                 continue
             for _ in range(self.warmup + 1):
                 p['step'] = s
+                self()
+        if self.hybrid and self.pre.inverse_lag == 0:
+            # the inverse steps' forward/backward graph too (real inverse
+            # updates: each runs the eigensolver once)
+            for _ in range(self.warmup + 1):
+                p['step'] = 0
                 self()
         p['step'] = saved

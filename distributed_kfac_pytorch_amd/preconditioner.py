@@ -541,6 +541,22 @@ class KFAC(optim.Optimizer):
         finally:
             self._defer_hook = prev
 
+    @contextlib.contextmanager
+    def hook_factors(self):
+        """Inside this block the hooks compute this step's factors themselves
+        (as with compute_factor_in_hook=True) and step() does not compute them
+        again.  graphs.GraphedTrainStep uses it for a one-process (single-
+        segment) trainer's inverse-update steps: their forward/backward replays
+        a graph with the factor launches inside, and only the update runs
+        eagerly (a replayed graph runs no Python hooks, so factors computed in
+        step() from hook-saved tensors would read another graph's buffers)."""
+        prev = self.compute_factor_in_hook
+        self.compute_factor_in_hook = True
+        try:
+            yield
+        finally:
+            self.compute_factor_in_hook = prev
+
     def _forward_hook(self, module, input, output, reverse=False):
         if torch.is_grad_enabled() and self.early_factors:
             self._count_forward(module)

@@ -22,7 +22,7 @@ def deterministic_convs():
 
 
 def _train(use_graphs, steps=25, precision='fp32', segmented=False, set_to_none=False, lag=0,
-           amp=True):
+           amp=True, hybrid=False):
     torch.manual_seed(0)
     m = resnet_cifar.resnet20().cuda().to(memory_format=torch.channels_last)
     opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9)
@@ -44,20 +44,24 @@ def _train(use_graphs, steps=25, precision='fp32', segmented=False, set_to_none=
         opt.step()
         return loss
 
-    if segmented:
-        def fb():
-            opt.zero_grad(set_to_none=False)
-            with torch.autocast('cuda', dtype=torch.bfloat16):
-                loss = F.cross_entropy(m(x), y)
-            loss.backward()
-            return loss
+    def fb():
+        opt.zero_grad(set_to_none=set_to_none if hybrid else False)
+        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=amp):
+            loss = F.cross_entropy(m(x), y)
+        loss.backward()
+        return loss
 
-        def update():
-            pre.step()
-            opt.step()
+    def update():
+        pre.step()
+        opt.step()
+
+    if segmented:
         step = graphs.GraphedTrainStep(None, pre, [opt], warmup=1, enabled=use_graphs,
                                        forward_backward=fb, communicate=lambda: None,
                                        update=update)
+    elif hybrid:
+        step = graphs.GraphedTrainStep(step_fn, pre, [opt], warmup=1, enabled=use_graphs,
+                                       forward_backward=fb, update=update)
     else:
         step = graphs.GraphedTrainStep(step_fn, pre, [opt], warmup=1, enabled=use_graphs)
     losses = []
@@ -95,6 +99,27 @@ def test_graphed_matches_eager():
     for a, b in zip(le, lg):
         assert abs(a - b) <= 1e-5 * max(1.0, abs(a)), (le, lg)
     assert _pdiff(pe, pg) <= 1e-5, _pdiff(pe, pg)
+
+
+def test_hybrid_inverse_steps_replay_their_forward_backward():
+    """Single-segment trainer that also names forward_backward / update (the
+    one-GPU bench): inverse steps 10 and 20 run their forward/backward with the
+    factors inside the hooks (KFAC.hook_factors) -- eagerly at step 10 (warm-up),
+    as a captured 'invfb' graph at step 20 -- and only the update eagerly.
+    Matches the all-eager run, whose factors are computed in step()."""
+    prev = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        le, pe, _ = _train(False, steps=25, amp=False)
+        lh, ph, sh = _train(True, steps=25, amp=False, hybrid=True)
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = prev
+    assert sh.hybrid and sh.replays > 0
+    assert any(k[0] == 'invfb' for k in sh.graphs), list(sh.graphs)
+    assert not sh.pre.compute_factor_in_hook        # restored after each inverse step
+    for a, b in zip(le, lh):
+        assert abs(a - b) <= 1e-6 * max(1.0, abs(a)), (le, lh)
+    assert _pdiff(pe, ph) <= 1e-6, _pdiff(pe, ph)
 
 
 def _check_losses(le, le2, lg, rel):
