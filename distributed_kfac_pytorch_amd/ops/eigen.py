@@ -27,6 +27,16 @@ SMALL_N = 192
 FUSED_MAX_N = 16384   # csrc/eig_reduce.hip NMAX
 BT = 128   # back-transformation block (csrc/eig_backtransform.hip)
 _streams = {}
+# debug / probes: a list -> _fused_group appends (group slot, stage, event)
+# after each stage it enqueues (scripts/probes/probe_eig_stream_ends.py)
+STAGE_EVENTS = None
+
+
+def _mark(slot, stage, stream):
+    if STAGE_EVENTS is not None:
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(stream)
+        STAGE_EVENTS.append((slot, stage, e))
 
 
 def _side_streams(device, k):
@@ -265,12 +275,16 @@ def _fused_group(mats, clip, stream, use_graph, slot=0, finite=None):
                 r.n = n
                 dr[k] = dcr[i]
                 k += 1
+        _mark(slot, 'staged', stream)
         _lib.check(L.kfac_reduce_batched(rr, total, int(use_graph), cs), 'kfac_reduce_batched')
+        _mark(slot, 'reduce', stream)
         _lib.check(L.kfac_dc_batched(dr, total, int(use_graph), cs), 'kfac_dc_batched')
+        _mark(slot, 'dc', stream)
         for n, idx, B in bufs:
             b = len(idx)
             _lib.check(L.kfac_tridiag_backtransform(*_bt_args(B, n, b), int(use_graph), cs),
                        'kfac_tridiag_backtransform')
+            _mark(slot, 'bt%d' % n, stream)
             _INFOS.append(_dc_info(B, n, b))
             Q = B['Z'][:, :, :n].transpose(1, 2).contiguous()
             D = B['w'].clone()
