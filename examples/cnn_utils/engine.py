@@ -72,8 +72,12 @@ class GraphedTrainer(object):
                                                 communicate=grad_sync, update=self._update,
                                                 phased_update=self.scaler is None)
         else:
+            # forward_backward / update too: inverse steps replay a forward/
+            # backward graph with the factors in its hooks (bench.py's one-GPU path)
             self.step = graphs.GraphedTrainStep(self._train_step, preconditioner, [optimizer],
-                                                enabled=args.cuda)
+                                                enabled=args.cuda,
+                                                forward_backward=self._forward_backward,
+                                                update=self._update)
 
     def _forward_backward(self, ragged=False):
         if self.grad_sync is not None:
