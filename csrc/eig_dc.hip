@@ -330,9 +330,17 @@ __global__ __launch_bounds__(256) void dc_prep_kernel(const DcMat* __restrict__ 
     int ps = 0;
     AS1 int* rp = M.rp + 2LL * lo;
     AS1 float* rcs = M.rcs + 2LL * lo;
+    // the next element's values are loaded before this one's stores (which
+    // only write survivors at q <= p): the scan is one serial lane, and a
+    // load issued behind the stores waited out the whole LDS round trip
+    double dn = sd2[0], zn = sz2[0];
+    int sn = ssrc2[0];
     for (int p = 0; p < m; ++p) {
-      const double dp = sd2[p], zp = sz2[p];
-      const int sp = ssrc2[p];
+      const double dp = dn, zp = zn;
+      const int sp = sn;
+      if (p + 1 < m) {
+        dn = sd2[p + 1]; zn = sz2[p + 1]; sn = ssrc2[p + 1];
+      }
       double dv = 0.0;
       int dsrc_v = -1;
       if (rho * fabs(zp) <= tol) {
@@ -341,10 +349,13 @@ __global__ __launch_bounds__(256) void dc_prep_kernel(const DcMat* __restrict__ 
         have = true; pd = dp; pz = zp; ps = sp;
         continue;
       } else {
-        const double tau = hypot(zp, pz);
-        const double c = zp / tau, s = -pz / tau;
         const double tt = dp - pd;
-        if (fabs(tt * c * s) <= tol) {
+        // |tt c s| <= tol with c = zp / tau, s = -pz / tau, tau = hypot(zp, pz),
+        // tested as |tt zp pz| <= tol (zp^2 + pz^2): the square root and the
+        // divisions only when a rotation deflates (rare)
+        if (fabs(tt * zp * pz) <= tol * fma(zp, zp, pz * pz)) {
+          const double tau = hypot(zp, pz);
+          const double c = zp / tau, s = -pz / tau;
           rp[2 * r] = ps & SRC_MASK;
           rp[2 * r + 1] = sp & SRC_MASK;
           rcs[2 * r] = (float)c;
