@@ -39,7 +39,13 @@
 //   S3  Z[col][j0+i] -= sum_c W2t[col][c] Vt_k[i][c]       (Vt_k = V_k^T copy)
 namespace {
 
-constexpr int BT = 128;       // reflectors per block
+// reflectors per block: 256 (round 5; 128 before): each block is one pass
+// over Z for its update and one for V_k^T Z, so the block width halves the
+// Z traffic of the sequence, and the Z update's k-loop doubles.  T_k is
+// built from its two 128-row halves (larft_kernel) and their coupling
+// (t_merge_kernel).
+constexpr int BT = 256;
+constexpr int LB = 128;       // larft sub-block
 constexpr int KCH = 512;      // split-K chunk of S1
 constexpr int TILE_F32 = 0;   // pgemm 128 x 128 fp32, 4 waves (best since round 2: profiles/r2_pgemm_sweep.log)
 // GEMM precision of the back-transformation: bf16x6 on the fp32 operands
@@ -86,9 +92,9 @@ __global__ __launch_bounds__(256) void make_v_kernel(float* A, int lda, long lon
   for (int i = threadIdx.x; i <= j + shift && i < n; i += 256) row[i] = (i == j + shift) ? 1.f : 0.f;
 }
 
-// T_k (upper triangular, ROW-major BT x BT, zero beyond kb) from
-// G_k = V_k V_k^T (row-major, ld BT) and tau (LAPACK larft, forward /
-// columnwise).  larft's column recursion T(0:i, i) = -tau_i T(0:i, 0:i)
+// The two diagonal LB x LB sub-blocks of T_k (upper triangular, ROW-major
+// BT x BT, zero beyond kb) from G_k = V_k V_k^T (row-major, ld BT) and tau
+// (LAPACK larft, forward / columnwise), one workgroup per sub-block.  larft's column recursion T(0:i, i) = -tau_i T(0:i, 0:i)
 // G(0:i, i) is BT dependent steps (~320 us per launch at BT = 128,
 // profiles/r3_eig_kernel_stats.csv); the same T is the inverse of the upper
 // triangular U = diag(1 / tau) + striu(G), computed here by recursive
@@ -99,19 +105,21 @@ __global__ __launch_bounds__(256) void make_v_kernel(float* A, int lda, long lon
 constexpr int LT = 256;   // larft threads
 __global__ __launch_bounds__(LT) void larft_kernel(const float* G, float* T, const float* tau,
                                                    int n, int nblk) {
-  __shared__ float sU[BT][BT + 1];
-  __shared__ float sT[BT][BT + 1];
-  __shared__ float sW[BT / 2][BT / 2 + 1];
-  __shared__ int live[BT];
-  const int k = blockIdx.x, mat = blockIdx.y, tid = threadIdx.x;
-  const long long off = ((long long)mat * nblk + k) * BT * BT;
-  const int j0 = k * BT;
-  const int kb = (n - j0) < BT ? (n - j0) : BT;
+  __shared__ float sU[LB][LB + 1];
+  __shared__ float sT[LB][LB + 1];
+  __shared__ float sW[LB / 2][LB / 2 + 1];
+  __shared__ int live[LB];
+  const int k = blockIdx.x / (BT / LB), sb = blockIdx.x % (BT / LB);
+  const int mat = blockIdx.y, tid = threadIdx.x;
+  // sub-block sb: rows / columns sb LB .. sb LB + LB - 1 of block k
+  const long long off = ((long long)mat * nblk + k) * BT * BT + (long long)sb * LB * (BT + 1);
+  const int j0 = k * BT + sb * LB;
+  const int kb = (n - j0) < LB ? (n - j0 > 0 ? n - j0 : 0) : LB;
   const float* tj = tau + (long long)mat * n + j0;
-  for (int r = tid; r < BT; r += LT) live[r] = (r < kb) && (tj[r] != 0.f);
+  for (int r = tid; r < LB; r += LT) live[r] = (r < kb) && (tj[r] != 0.f);
   __syncthreads();
-  for (int e = tid; e < BT * BT; e += LT) {
-    const int r = e / BT, c = e % BT;
+  for (int e = tid; e < LB * LB; e += LT) {
+    const int r = e / LB, c = e % LB;
     float u = 0.f;
     if (r == c) u = live[r] ? 1.f / tj[r] : 1.f;
     else if (c > r && live[r] && live[c]) u = G[off + (long long)r * BT + c];
@@ -119,15 +127,15 @@ __global__ __launch_bounds__(LT) void larft_kernel(const float* G, float* T, con
     sT[r][c] = (r == c) ? 1.f / u : 0.f;
   }
   __syncthreads();
-  for (int b = 1; b < BT; b *= 2) {
-    const int pairs = BT / (2 * b), per = b * b;
+  for (int b = 1; b < LB; b *= 2) {
+    const int pairs = LB / (2 * b), per = b * b;
     // W = U12 T22 for every pair (U12: rows p0 .. p0+b, cols p0+b .. p0+2b)
     for (int e = tid; e < pairs * per; e += LT) {
       const int p = e / per, w = e % per, r = w / b, c = w % b;
       const int p0 = 2 * p * b;
       float acc = 0.f;
       for (int q = 0; q <= c; ++q) acc = fmaf(sU[p0 + r][p0 + b + q], sT[p0 + b + q][p0 + b + c], acc);
-      sW[(p * b + r) % (BT / 2)][c] = acc;
+      sW[(p * b + r) % (LB / 2)][c] = acc;
     }
     __syncthreads();
     // T12 = -T11 W
@@ -135,14 +143,53 @@ __global__ __launch_bounds__(LT) void larft_kernel(const float* G, float* T, con
       const int p = e / per, w = e % per, r = w / b, c = w % b;
       const int p0 = 2 * p * b;
       float acc = 0.f;
-      for (int q = r; q < b; ++q) acc = fmaf(sT[p0 + r][p0 + q], sW[(p * b + q) % (BT / 2)][c], acc);
+      for (int q = r; q < b; ++q) acc = fmaf(sT[p0 + r][p0 + q], sW[(p * b + q) % (LB / 2)][c], acc);
       sT[p0 + r][p0 + b + c] = -acc;
     }
     __syncthreads();
   }
-  for (int e = tid; e < BT * BT; e += LT) {
-    const int r = e / BT, c = e % BT;
+  for (int e = tid; e < LB * LB; e += LT) {
+    const int r = e / LB, c = e % LB;
     T[off + (long long)r * BT + c] = (live[r] && live[c]) ? sT[r][c] : 0.f;
+  }
+}
+
+// The coupling of T_k's two halves: T = U^-1 for the block upper-triangular
+// U = [U11 U12; 0 U22] with U12 = G12 (the strict upper part of G_k), so
+// T12 = -T11 G12 T22, and T21 = 0.  One workgroup per block: W = G12 T22 into
+// LDS in 32-row panels, then T12 = -T11 W (dead rows / columns of T11 / T22
+// are zero already, so their products vanish).  ~4 MFLOP per block.
+__global__ __launch_bounds__(256) void t_merge_kernel(const float* G, float* T, int nblk) {
+  __shared__ float sW[LB][LB + 1];
+  __shared__ float sA[32][LB + 1];
+  const int k = blockIdx.x, mat = blockIdx.y, tid = threadIdx.x;
+  const long long off = ((long long)mat * nblk + k) * BT * BT;
+  const float* G12 = G + off + LB;                        // rows 0.., columns LB..
+  const float* T11 = T + off;
+  const float* T22 = T + off + (long long)LB * BT + LB;
+  float* T12 = T + off + LB;
+  const int c = tid & (LB - 1), rh = tid >> 7;            // column, row half
+  // W = G12 T22 (T22 upper triangular: q <= c)
+  for (int r0 = 0; r0 < LB; r0 += 32) {
+    for (int e = tid; e < 32 * LB; e += 256) sA[e / LB][e % LB] = G12[(long long)(r0 + e / LB) * BT + e % LB];
+    __syncthreads();
+    for (int r = rh; r < 32; r += 2) {
+      float acc = 0.f;
+      for (int q = 0; q <= c; ++q) acc = fmaf(sA[r][q], T22[(long long)q * BT + c], acc);
+      sW[r0 + r][c] = acc;
+    }
+    __syncthreads();
+  }
+  // T12 = -T11 W (T11 upper triangular: p >= r)
+  for (int r0 = 0; r0 < LB; r0 += 32) {
+    for (int e = tid; e < 32 * LB; e += 256) sA[e / LB][e % LB] = T11[(long long)(r0 + e / LB) * BT + e % LB];
+    __syncthreads();
+    for (int r = rh; r < 32; r += 2) {
+      float acc = 0.f;
+      for (int p = r0 + r; p < LB; ++p) acc = fmaf(sA[r][p], sW[p][c], acc);
+      T12[(long long)(r0 + r) * BT + c] = -acc;
+    }
+    __syncthreads();
   }
 }
 
@@ -286,8 +333,10 @@ int run_plan(const BtArgs& a, const BtPlan& plan, hipStream_t stream) {
         err = (int)hipGetLastError();
         break;
       default:
-        hipLaunchKernelGGL(larft_kernel, dim3(nblk, a.batch), dim3(LT), 0, stream, a.Tbuf,
-                           a.Tbuf + tstride * a.batch, a.tau, a.n, nblk);
+        hipLaunchKernelGGL(larft_kernel, dim3(nblk * (BT / LB), a.batch), dim3(LT), 0, stream,
+                           a.Tbuf, a.Tbuf + tstride * a.batch, a.tau, a.n, nblk);
+        hipLaunchKernelGGL(t_merge_kernel, dim3(nblk, a.batch), dim3(256), 0, stream, a.Tbuf,
+                           a.Tbuf + tstride * a.batch, nblk);
         err = (int)hipGetLastError();
     }
     if (err) return err;
@@ -364,6 +413,7 @@ KFAC_API int kfac_band_backtransform(float* A, int lda, long long strideA, const
 }
 
 KFAC_API int kfac_backtransform_slabs(int lda) { return nslab(lda); }
+KFAC_API int kfac_backtransform_block() { return BT; }
 
 KFAC_API int kfac_backtransform_prepare(float* A, int lda, long long strideA, const float* tau,
                                         float* Z, int ldz, long long strideZ, int n, int batch,

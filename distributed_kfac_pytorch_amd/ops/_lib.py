@@ -80,6 +80,7 @@ _SIGS = {
     'kfac_sy2sb_nmax': [],
     'kfac_sb2st_batched': [ctypes.POINTER(Sb2stRecord), c_int, c_int, c_vp],
     'kfac_backtransform_slabs': [c_int],
+    'kfac_backtransform_block': [],
     'kfac_event_create': [],
     'kfac_event_destroy': [c_vp],
     'kfac_event_record_external': [c_vp, c_vp],

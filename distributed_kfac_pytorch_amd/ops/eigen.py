@@ -25,7 +25,7 @@ __all__ = ['symeig_many', 'inverse_many', 'SMALL_N']
 
 SMALL_N = 192
 FUSED_MAX_N = 16384   # csrc/eig_reduce.hip NMAX
-BT = 128   # back-transformation block (csrc/eig_backtransform.hip)
+BT = 256   # back-transformation block (csrc/eig_backtransform.hip kfac_backtransform_block)
 _streams = {}
 # debug / probes: a list -> _fused_group appends (group slot, stage, event)
 # after each stage it enqueues (scripts/probes/probe_eig_stream_ends.py)
@@ -92,6 +92,9 @@ def _tri_buffers(dev, n, b, slot=0):
     bufs = _TRI_BUFS.get(key)
     if bufs is None:
         L = _lib.lib()
+        if int(L.kfac_backtransform_block()) != BT:
+            raise RuntimeError('back-transformation block: library {} vs eigen.BT {}'.format(
+                int(L.kfac_backtransform_block()), BT))
         # A: lda x lda per matrix, lda = n rounded up to the reduction's 128-row
         # tiles, zero past n (its symv tiles read whole tiles unmasked; the
         # MFMA GEMMs of the back-transformation step k by 64)
