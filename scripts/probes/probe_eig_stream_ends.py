@@ -21,6 +21,8 @@ def main():
     dev = torch.device('cuda', torch.cuda.current_device())
     torch.cuda.set_stream(torch.cuda.Stream())
     ns = sizes()
+    # KFAC_PROBE_MIN_N: drop the factors below this size (what they cost the rest)
+    ns = [n for n in ns if n >= int(os.environ.get('KFAC_PROBE_MIN_N', '0'))]
     g = torch.Generator(device=dev).manual_seed(0)
     mats = []
     for n in ns:
