@@ -234,13 +234,20 @@ class KFACLayer(object):
             self._store_result('Q' + which, result[0])
             self._store_result('d' + which, result[1])
             if which == 'G' and self.prediv_eigenvalues:
-                if self.state.get('dA') is None:
-                    raise ValueError('compute_A_inv must be called before compute_G_inv if '
-                                     'prediv_eigenvalues is True.')
-                self._store_result('dGdA', precond_ops.outer_reciprocal(
-                    self.state['dG'], self.state['dA'], damping))
+                self._store_outer_reciprocal(damping)
         else:
             self._store_result(which + '_inv', result)
+
+    def _store_outer_reciprocal(self, damping):
+        """dGdA = 1 / (dG dA^T + damping) from the stored eigenvalues, in place
+        when the buffer exists."""
+        if self.state.get('dA') is None:
+            raise ValueError('compute_A_inv must be called before compute_G_inv if '
+                             'prediv_eigenvalues is True.')
+        cur = self.state.get('dGdA')
+        out = cur if (cur is not None and cur.dtype == torch.float32) else None
+        self._store_result('dGdA', precond_ops.outer_reciprocal(
+            self.state['dG'], self.state['dA'], damping, out=out))
 
     def _compute_factor_inverse(self, factor, damping=0.001):
         F = factor.to(torch.float32)

@@ -28,8 +28,11 @@ FUSED_MAX_N = 16384   # csrc/eig_reduce.hip NMAX
 BT = 256   # back-transformation block (csrc/eig_backtransform.hip kfac_backtransform_block)
 _streams = {}
 # debug / probes: a list -> _fused_group appends (group slot, stage, event)
-# after each stage it enqueues (scripts/probes/probe_eig_stream_ends.py)
+# after each stage it enqueues (scripts/probes/probe_eig_stream_ends.py).
+# KFAC_EIG_STAGE_LOG=1: every native symeig_many call records them, and the
+# next check_solver_status() prints the stage times to stderr.
 STAGE_EVENTS = None
+STAGE_LOG = os.environ.get('KFAC_EIG_STAGE_LOG') == '1'
 
 
 def _mark(slot, stage, stream):
@@ -425,7 +428,15 @@ def check_solver_status():
     launch of the two-stage path (nonzero = bounded waits that timed out, the
     band reduction's output is garbage).  Syncs; call once per inverse step,
     not in the hot path."""
-    global _INFOS
+    global _INFOS, STAGE_EVENTS
+    if STAGE_LOG and STAGE_EVENTS:
+        evs, STAGE_EVENTS = STAGE_EVENTS, None
+        evs[-1][2].synchronize()
+        t0 = evs[0][2]
+        import sys
+        print('[kfac-eig] ' + ', '.join('%s%s %.2f' % ('' if slot < 0 else 'g%d ' % slot, stage,
+                                                         t0.elapsed_time(e))
+                                        for slot, stage, e in evs[1:]), file=sys.stderr)
     infos, _INFOS = _INFOS, []
     if not infos:
         return
@@ -461,6 +472,7 @@ def symeig_many(mats, clip=0.0, solver='auto', finite=None):
     finite: None, or a device bool tensor (one flag per matrix): a matrix
     whose flag is False is decomposed as the identity instead (see
     sanitize); the caller checks the flags after enqueueing its work."""
+    global STAGE_EVENTS
     if len(mats) == 0:
         return []
     if finite is not None and not _lib.use_native(mats[0]):
@@ -513,6 +525,10 @@ def symeig_many(mats, clip=0.0, solver='auto', finite=None):
         if finite is not None:
             _clean(ts)
     cur = torch.cuda.current_stream(mats[0].device)
+    if STAGE_LOG and not STAGE_EVENTS:
+        STAGE_EVENTS = []
+        _mark(-1, 'start', cur)
+    _mark(-1, 'symeig', cur)
     side = None
     if ts:
         # the two-stage group on its own stream, under the one-stage chains
@@ -537,6 +553,7 @@ def symeig_many(mats, clip=0.0, solver='auto', finite=None):
         for i in ts:
             outs[i][0].record_stream(cur)
             outs[i][1].record_stream(cur)
+    _mark(-1, 'end', cur)
     return outs
 
 

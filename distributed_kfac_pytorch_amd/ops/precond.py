@@ -21,10 +21,13 @@ __all__ = ['outer_reciprocal', 'precondition_eigen', 'precondition_inverse', 'kl
            'apply_gradients']
 
 
-def outer_reciprocal(dG, dA, damping):
-    """1 / (dG[:, None] * dA[None, :] + damping)."""
+def outer_reciprocal(dG, dA, damping, out=None):
+    """1 / (dG[:, None] * dA[None, :] + damping) (written into `out`, a
+    contiguous fp32 nG x nA tensor, when given)."""
     if _lib.use_native(dG) and dG.dtype == torch.float32 and dA.dtype == torch.float32:
-        out = torch.empty(dG.shape[0], dA.shape[0], dtype=torch.float32, device=dG.device)
+        if out is None or out.dtype != torch.float32 or not out.is_contiguous() or \
+                out.shape != (dG.shape[0], dA.shape[0]):
+            out = torch.empty(dG.shape[0], dA.shape[0], dtype=torch.float32, device=dG.device)
         _lib.check(_lib.lib().kfac_outer_recip(_lib.ptr(dG), _lib.ptr(dA), _lib.ptr(out),
                                                dG.shape[0], dA.shape[0], float(damping),
                                                _lib.stream(dG.device)), 'kfac_outer_recip')
