@@ -237,6 +237,7 @@ class FusedPreconditioner(object):
         self._stage_tables = None
         # superseded device tables stay alive: a captured graph may use them
         self._retired_tables = []
+        self._split_tables = {}       # refresh_eigen job tables by content
         self.damping = 0.0
         self.kl_buf = None
         self._build_stage_tables()
@@ -363,7 +364,17 @@ class FusedPreconditioner(object):
                 r.tiles_c = _cdiv(cc, 64)
                 r.tile_begin = tiles
                 tiles += _cdiv(rr, 64) * r.tiles_c
-            table = _upload((SplitRec * len(lst))(*lst), self.device)
+            # the job tables only change when a buffer moves: uploaded once
+            # per content (a host-to-device copy inside the inverse step would
+            # wait behind the eigensolver's queued work on some runtimes)
+            raw = bytes(memoryview((SplitRec * len(lst))(*lst)).cast('B'))
+            table = self._split_tables.get(raw)
+            if table is None:
+                if len(self._split_tables) >= 8:
+                    self._retired_tables.extend(self._split_tables.values())
+                    self._split_tables.clear()
+                table = self._split_tables[raw] = _upload((SplitRec * len(lst))(*lst),
+                                                          self.device)
             _lib.check(L.kfac_split_copy(prec, _lib.ptr(table), len(lst), tiles, stream),
                        'kfac_split_copy')
             keep.append(table)
