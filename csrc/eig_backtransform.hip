@@ -156,41 +156,75 @@ __global__ __launch_bounds__(LT) void larft_kernel(const float* G, float* T, con
 
 // The coupling of T_k's two halves: T = U^-1 for the block upper-triangular
 // U = [U11 U12; 0 U22] with U12 = G12 (the strict upper part of G_k), so
-// T12 = -T11 G12 T22, and T21 = 0.  One workgroup per block: W = G12 T22 into
-// LDS in 32-row panels, then T12 = -T11 W (dead rows / columns of T11 / T22
-// are zero already, so their products vanish).  ~4 MFLOP per block.
+// T12 = -T11 G12 T22, and T21 = 0.  One workgroup per block, operands in LDS,
+// 8 x 8 outputs per thread: W = G12 T22, then T12 = -T11 W.  Full-length
+// k-loops: T22 (T11) is zero below (left of) its diagonal, and dead rows /
+// columns of T11 / T22 are zero already, so the extra terms add exact zeros
+// (the sums are those of the triangular loops, bit for bit).  A first
+// version reading T22 from memory inside a triangular loop took 371 us per
+// 3 x 4608 back-transformation.
 __global__ __launch_bounds__(256) void t_merge_kernel(const float* G, float* T, int nblk) {
-  __shared__ float sW[LB][LB + 1];
-  __shared__ float sA[32][LB + 1];
+  __shared__ float s0[LB][LB + 1];
+  __shared__ float s1[LB][LB + 1];
   const int k = blockIdx.x, mat = blockIdx.y, tid = threadIdx.x;
   const long long off = ((long long)mat * nblk + k) * BT * BT;
   const float* G12 = G + off + LB;                        // rows 0.., columns LB..
   const float* T11 = T + off;
   const float* T22 = T + off + (long long)LB * BT + LB;
   float* T12 = T + off + LB;
-  const int c = tid & (LB - 1), rh = tid >> 7;            // column, row half
-  // W = G12 T22 (T22 upper triangular: q <= c)
-  for (int r0 = 0; r0 < LB; r0 += 32) {
-    for (int e = tid; e < 32 * LB; e += 256) sA[e / LB][e % LB] = G12[(long long)(r0 + e / LB) * BT + e % LB];
-    __syncthreads();
-    for (int r = rh; r < 32; r += 2) {
-      float acc = 0.f;
-      for (int q = 0; q <= c; ++q) acc = fmaf(sA[r][q], T22[(long long)q * BT + c], acc);
-      sW[r0 + r][c] = acc;
-    }
-    __syncthreads();
+  for (int e = tid; e < LB * LB; e += 256) {
+    const int r = e / LB, c = e % LB;
+    s0[r][c] = G12[(long long)r * BT + c];
+    s1[r][c] = T22[(long long)r * BT + c];
   }
-  // T12 = -T11 W (T11 upper triangular: p >= r)
-  for (int r0 = 0; r0 < LB; r0 += 32) {
-    for (int e = tid; e < 32 * LB; e += 256) sA[e / LB][e % LB] = T11[(long long)(r0 + e / LB) * BT + e % LB];
-    __syncthreads();
-    for (int r = rh; r < 32; r += 2) {
-      float acc = 0.f;
-      for (int p = r0 + r; p < LB; ++p) acc = fmaf(sA[r][p], sW[p][c], acc);
-      T12[(long long)(r0 + r) * BT + c] = -acc;
-    }
-    __syncthreads();
+  __syncthreads();
+  const int ty = tid >> 4, tx = tid & 15;                 // rows ty + 16 i, columns tx + 16 j
+  float acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) acc[i][jj] = 0.f;
+  for (int q = 0; q < LB; ++q) {
+    float a[8], b[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = s0[ty + 16 * i][q];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) b[jj] = s1[q][tx + 16 * jj];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) acc[i][jj] = fmaf(a[i], b[jj], acc[i][jj]);
   }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) s0[ty + 16 * i][tx + 16 * jj] = acc[i][jj];   // W
+  for (int e = tid; e < LB * LB; e += 256) {
+    const int r = e / LB, c = e % LB;
+    s1[r][c] = T11[(long long)r * BT + c];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) acc[i][jj] = 0.f;
+  for (int p = 0; p < LB; ++p) {
+    float a[8], b[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = s1[ty + 16 * i][p];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) b[jj] = s0[p][tx + 16 * jj];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) acc[i][jj] = fmaf(a[i], b[jj], acc[i][jj]);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj)
+      T12[(long long)(ty + 16 * i) * BT + tx + 16 * jj] = -acc[i][jj];
 }
 
 struct BtArgs {
