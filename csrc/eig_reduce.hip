@@ -92,10 +92,18 @@ __device__ inline void hh_scalars(double alpha, double sig2, double& beta, doubl
 }
 
 // workgroup -> (matrix, first workgroup of that matrix) from the launch's
-// ascending offsets: lane i tests offset i (one load + ballot, no LDS)
+// ascending offsets: lane i tests offset i (one load + ballot, no LDS); a
+// launch whose active matrices all have the same workgroup count passes
+// -count instead (one dependent table read less per launch: the batch of
+// equal-size largest factors is the inverse update's critical chain)
 __device__ __forceinline__ void find_mat(const int* __restrict__ offs, int nact, int& mi,
                                          int& base) {
   const int lane = threadIdx.x & 63, b = blockIdx.x;
+  if (nact < 0) {      // uniform launch: every active matrix has -nact workgroups (no table read)
+    mi = b / -nact;
+    base = mi * -nact;
+    return;
+  }
   if (nact <= 64) {     // one load; the base offset comes from lane mi (no second round trip)
     const int o = gld_if(gptr(offs), lane, lane < nact, 0x7fffffff);
     mi = __builtin_amdgcn_readfirstlane(__popcll(__ballot(o <= b)) - 1);
@@ -903,6 +911,19 @@ RPlan* plan_for(const KfacReduceRecord* recs, int count, bool capture, int* err)
       for (int k = 0; k < 3; ++k) {
         offs[((size_t)k * P.nmax + j) * (nm + 1) + nm] = acc[k];
         P.grid[k][j] = acc[k];
+        // uniform launch: the active matrices (a prefix: sizes descend) share one count
+        const int na = P.nact[k][j];
+        if (na > 0 && acc[k] % na == 0) {
+          int c0[3];
+          counts(P.n_sorted[0], j, c0);
+          bool uni = true;
+          for (int i = 1; i < na && uni; ++i) {
+            int ci[3];
+            counts(P.n_sorted[i], j, ci);
+            uni = ci[k] == c0[k];
+          }
+          if (uni && c0[k] > 0 && c0[k] * na == acc[k]) P.nact[k][j] = -c0[k];
+        }
       }
       // F reads the partials of S(j-1): nt - j / TB blocks of the largest matrix
       const int nt0 = (P.n_sorted[0] + TB - 1) / TB;
