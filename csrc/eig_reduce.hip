@@ -66,6 +66,37 @@ struct RMat {
   long long sP, sTS, sDS, sX;             // slot strides (floats); 2 slots each
 };
 
+__host__ __device__ inline long long kfac_a16(long long x) { return (x + 15) / 16 * 16; }
+
+// Workspace layout of one matrix (floats): V, W and the 2-slot partial rings
+struct WsLayout {
+  long long V, W, P, TS, DS, XH, AV, SC, total, sP, sTS, sDS, sX;
+  int nt, ld;
+};
+
+__host__ __device__ inline WsLayout ws_layout(long long n) {
+  WsLayout L;
+  L.nt = (int)((n + TB - 1) / TB);
+  L.ld = L.nt * TB;
+  const long long nt = L.nt;
+  L.sP = kfac_a16(2 * nt * L.ld);
+  L.sTS = kfac_a16(nt * (nt + 1) > 4 ? nt * (nt + 1) : 4);
+  L.sDS = kfac_a16(nt * NK);
+  L.sX = kfac_a16(L.ld);
+  long long o = 0;
+  L.V = o; o += kfac_a16((long long)NB * L.ld);
+  L.W = o; o += kfac_a16((long long)NB * L.ld);
+  L.P = o; o += 2 * L.sP;
+  L.TS = o; o += 2 * L.sTS + 1024;         // float4 loads past the triangle stay inside
+  L.DS = o; o += 2 * L.sDS;
+  L.XH = o; o += 2 * L.sX;
+  L.AV = o; o += 2 * L.sX;
+  L.SC = o; o += kfac_a16(8);
+  L.total = (o + 63) / 64 * 64;
+  return L;
+}
+
+
 // debug: per-column stamps (s_memrealtime, 100 MHz) of the first F and S
 // workgroups into a caller buffer (kfac_reduce_stamps)
 __device__ unsigned long long* g_stamps = nullptr;
@@ -129,9 +160,7 @@ __device__ __forceinline__ void find_mat(const int* __restrict__ offs, int nact,
 // blocks of S(j-1) (nt - j / TB) of every matrix of the launch: fixes the
 // number of partial loads per thread, all issued up front.
 template <int RB>
-__global__ __launch_bounds__(256) void red_fin_kernel(const RMat* __restrict__ mats,
-                                                      const int* __restrict__ offs, int nact,
-                                                      int j) {
+__device__ __forceinline__ void fin_body(const RMat& M, int base, int j) {
   constexpr int DQ = RB / 4;                            // DS loads per thread
   constexpr int TQ = (RB * (RB + 1) + 1023) / 1024;     // float4 TS loads per thread
   constexpr int PK = RB / 4;                            // P partial pairs per thread
@@ -141,10 +170,6 @@ __global__ __launch_bounds__(256) void red_fin_kernel(const RMat* __restrict__ m
   __shared__ float sq[4][4][FB];                        // per quarter: yh, c3, c3', c2 of each row
   const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6;
   unsigned long long* const stamps = blockIdx.x == 0 ? g_stamps : nullptr;
-  STAMP(0);
-  int mi, base;
-  find_mat(offs, nact, mi, base);
-  const RMat M = mats[mi];
   const int n = M.n, nt = M.nt;
   const long long lda = M.lda, ld = M.ld;
   // first row block: the first row S(j) reads (its tiles start at a 128-row
@@ -389,6 +414,18 @@ __global__ __launch_bounds__(256) void red_fin_kernel(const RMat* __restrict__ m
   STAMP(4);
 }
 
+template <int RB>
+__global__ __launch_bounds__(256) void red_fin_kernel(const RMat* __restrict__ mats,
+                                                      const int* __restrict__ offs, int nact,
+                                                      int j) {
+  unsigned long long* const stamps = blockIdx.x == 0 ? g_stamps : nullptr;
+  STAMP(0);
+  int mi, base;
+  find_mat(offs, nact, mi, base);
+  const RMat M = mats[mi];
+  fin_body<RB>(M, base, j);
+}
+
 // ------------------------------------------------------------------- U
 // A[I][K] -= L_I R_K^T with L = [V | W], R = [W | V] (rows >= q+1, upper):
 // the panel's rank-2NB update, 4 waves of 64 x 64.  X6 (default): the fp32
@@ -419,15 +456,10 @@ __device__ __forceinline__ void frag3(const float* src, bf16x8_t& h8, bf16x8_t& 
 }
 
 template <bool X6>
-__global__ __launch_bounds__(256) void red_upd_kernel(const RMat* __restrict__ mats,
-                                                      const int* __restrict__ offs, int nact,
-                                                      int q) {
+__device__ __forceinline__ void upd_body(const RMat& M, int base, int q) {
   __shared__ float sL[TB][2 * NB + 1];
   __shared__ float sR[TB][2 * NB + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  int mi, base;
-  find_mat(offs, nact, mi, base);
-  const RMat M = mats[mi];
   const int n = M.n, nt = M.nt;
   const int s0 = (q + 1) / TB;
   int I, K;
@@ -530,6 +562,16 @@ __global__ __launch_bounds__(256) void red_upd_kernel(const RMat* __restrict__ m
         if ((gr >= q + 1) & (gr < n) & (gc >= gr) & (gc < n))
           A[(unsigned)gr * ulda + gc] = old[a][b][x] - acc[a][b][x];
       }
+}
+
+template <bool X6>
+__global__ __launch_bounds__(256) void red_upd_kernel(const RMat* __restrict__ mats,
+                                                      const int* __restrict__ offs, int nact,
+                                                      int q) {
+  int mi, base;
+  find_mat(offs, nact, mi, base);
+  const RMat M = mats[mi];
+  upd_body<X6>(M, base, q);
 }
 
 // ------------------------------------------------------------------- S
@@ -673,15 +715,10 @@ __device__ __forceinline__ void symv_halves(const RMat& M, int I, int K, int hr0
 // (local - nh / SNH), the NK
 // partial kinds of its 128 rows into DS (wave = 16 kinds, lane = row, fixed
 // order).
-__global__ __launch_bounds__(256) void red_symv_kernel(const RMat* __restrict__ mats,
-                                                       const int* __restrict__ offs, int nact,
-                                                       int j) {
+__device__ __forceinline__ void symv_body(const RMat& M, int base, int j) {
   __shared__ SymvShared sred;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   unsigned long long* const stamps = g_stamps;
-  int mi, base;
-  find_mat(offs, nact, mi, base);
-  const RMat M = mats[mi];
   const int n = M.n, nt = M.nt;
   const long long ld = M.ld;
   const int s0 = (j + 1) / TB;
@@ -743,6 +780,15 @@ __global__ __launch_bounds__(256) void red_symv_kernel(const RMat* __restrict__ 
     symv_halves<false, SNH>(M, I, K, half0 & 1, cs, half0, sred, j, stamps);
 }
 
+__global__ __launch_bounds__(256) void red_symv_kernel(const RMat* __restrict__ mats,
+                                                       const int* __restrict__ offs, int nact,
+                                                       int j) {
+  int mi, base;
+  find_mat(offs, nact, mi, base);
+  const RMat M = mats[mi];
+  symv_body(M, base, j);
+}
+
 // ------------------------------------------------------------------ host
 struct RPlan {
   RMat* d_mats = nullptr;
@@ -800,12 +846,13 @@ int enqueue(const RPlan& P, hipStream_t stream) {
       default: launch_fin<128>(P, of, j, stream); break;
     }
     if (P.grid[1][j] > 0) {
-      if (g_upd_x6)
+      if (g_upd_x6) {
         hipLaunchKernelGGL(red_upd_kernel<true>, dim3(P.grid[1][j]), dim3(256), 0, stream,
                            P.d_mats, of + kstride, P.nact[1][j], j);
-      else
+      } else {
         hipLaunchKernelGGL(red_upd_kernel<false>, dim3(P.grid[1][j]), dim3(256), 0, stream,
                            P.d_mats, of + kstride, P.nact[1][j], j);
+      }
     }
     if (P.grid[2][j] > 0)
       hipLaunchKernelGGL(red_symv_kernel, dim3(P.grid[2][j]), dim3(256), 0, stream, P.d_mats,
@@ -816,34 +863,6 @@ int enqueue(const RPlan& P, hipStream_t stream) {
 
 std::mutex g_mu;
 std::map<std::string, RPlan> g_plans;
-
-struct WsLayout {
-  long long V, W, P, TS, DS, XH, AV, SC, total, sP, sTS, sDS, sX;
-  int nt, ld;
-};
-
-WsLayout ws_layout(long long n) {
-  auto a16 = [](long long x) { return (x + 15) / 16 * 16; };
-  WsLayout L;
-  L.nt = (int)((n + TB - 1) / TB);
-  L.ld = L.nt * TB;
-  const long long nt = L.nt;
-  L.sP = a16(2 * nt * L.ld);
-  L.sTS = a16(std::max<long long>(2 * h_tri((int)nt), 4));
-  L.sDS = a16(nt * NK);
-  L.sX = a16(L.ld);
-  long long o = 0;
-  L.V = o; o += a16((long long)NB * L.ld);
-  L.W = o; o += a16((long long)NB * L.ld);
-  L.P = o; o += 2 * L.sP;
-  L.TS = o; o += 2 * L.sTS + 1024;         // float4 loads past the triangle stay inside
-  L.DS = o; o += 2 * L.sDS;
-  L.XH = o; o += 2 * L.sX;
-  L.AV = o; o += 2 * L.sX;
-  L.SC = o; o += a16(8);
-  L.total = (o + 63) / 64 * 64;
-  return L;
-}
 
 }  // namespace
 
