@@ -18,6 +18,7 @@ __global__ __launch_bounds__(64) void tiny_kernel(float* buf) {
 // (zeroed by the host before the launch).  Every wait is bounded: after
 // ~2^22 polls the workgroup flags `err` and every later wait returns at
 // once, so all waves always reach the end.
+template <int SLEEP>
 __global__ __launch_bounds__(64) void persistent_kernel(unsigned* counter, unsigned* err,
                                                         float* buf, int phases) {
   for (int p = 0; p < phases; ++p) {
@@ -33,7 +34,7 @@ __global__ __launch_bounds__(64) void persistent_kernel(unsigned* counter, unsig
           __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(SLEEP);
       }
       __atomic_thread_fence(__ATOMIC_ACQUIRE);
     }
@@ -78,11 +79,19 @@ int pvc_chain(hipStream_t s, int n, int which) {
 }
 
 // one persistent launch of `grid` workgroups (<= 256: one per CU) running `phases` barriers
-int pvc_persistent(hipStream_t s, int phases, int grid) {
+// sleep: s_sleep argument between polls (1, 8 or 32; ~64 cycles each)
+int pvc_persistent(hipStream_t s, int phases, int grid, int sleep) {
   if (grid < 1 || grid > 256) return 20;
   if (hipMemsetAsync(g_sync, 0, 2 * sizeof(unsigned), s) != hipSuccess) return 21;
-  hipLaunchKernelGGL(persistent_kernel, dim3(grid), dim3(64), 0, s, g_sync, g_sync + 1,
-                     g_buf + 1024, phases);
+  if (sleep == 32)
+    hipLaunchKernelGGL(persistent_kernel<32>, dim3(grid), dim3(64), 0, s, g_sync, g_sync + 1,
+                       g_buf + 1024, phases);
+  else if (sleep == 8)
+    hipLaunchKernelGGL(persistent_kernel<8>, dim3(grid), dim3(64), 0, s, g_sync, g_sync + 1,
+                       g_buf + 1024, phases);
+  else
+    hipLaunchKernelGGL(persistent_kernel<1>, dim3(grid), dim3(64), 0, s, g_sync, g_sync + 1,
+                       g_buf + 1024, phases);
   return (int)hipGetLastError();
 }
 

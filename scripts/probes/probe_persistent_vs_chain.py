@@ -24,11 +24,11 @@ def main():
     lib = ctypes.CDLL(os.path.join(HERE, 'persistent_vs_chain.so'))
     vp = ctypes.c_void_p
     lib.pvc_chain.argtypes = [vp, ctypes.c_int, ctypes.c_int]
-    lib.pvc_persistent.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+    lib.pvc_persistent.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]
     assert lib.pvc_init() == 0
     s1, s2, s3 = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
 
-    def run(chain_a, chain_b, pers_grid):
+    def run(chain_a, chain_b, pers_grid, sleep=1):
         cur = torch.cuda.current_stream()
         e0 = torch.cuda.Event(enable_timing=True)
         e0.record(cur)
@@ -45,21 +45,23 @@ def main():
             ends['B'].record(s2)
         if pers_grid:
             s3.wait_event(e0)
-            assert lib.pvc_persistent(vp(s3.cuda_stream), n, pers_grid) == 0
+            assert lib.pvc_persistent(vp(s3.cuda_stream), n, pers_grid, sleep) == 0
             ends['P'] = torch.cuda.Event(enable_timing=True)
             ends['P'].record(s3)
         torch.cuda.synchronize()
         err = lib.pvc_err() if pers_grid else 0
         return {k: e0.elapsed_time(e) for k, e in ends.items()}, err
 
-    cases = [('A alone', (1, 0, 0)), ('A + chain B', (1, 1, 0)),
-             ('persistent 256 alone', (0, 0, 256)), ('A + persistent 256', (1, 0, 256)),
-             ('persistent 64 alone', (0, 0, 64)), ('A + persistent 64', (1, 0, 64))]
+    cases = [('A alone', (1, 0, 0, 1)), ('A + chain B', (1, 1, 0, 1))]
+    for grid in (256, 64, 16):
+        for sl in (1, 8, 32):
+            cases += [('persistent %d sleep %d alone' % (grid, sl), (0, 0, grid, sl)),
+                      ('A + persistent %d sleep %d' % (grid, sl), (1, 0, grid, sl))]
     for rep in range(3):
-        for name, (a, b, p) in cases:
-            t, err = run(a, b, p)
+        for name, (a, b, p, sl) in cases:
+            t, err = run(a, b, p, sl)
             if rep == 2:
-                print('%-22s %s%s' % (name, '  '.join(
+                print('%-32s %s%s' % (name, '  '.join(
                     '%s %.2f ms (%.2f us/step)' % (k, v, 1e3 * v / n) for k, v in sorted(t.items())),
                     '  ERR %d' % err if err else ''), flush=True)
             if err:
