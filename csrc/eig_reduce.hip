@@ -31,6 +31,12 @@
 // ~9.5 us per column (profiles/r3_stamps_*.log).  Moving them into S, where
 // they run beside the tiles, leaves F a load -> reduce -> scalar -> row chain.
 //
+// Once a matrix's trailing part is at most KFAC_REDUCE_TAIL rows (default
+// 768), its columns run as ONE launch each (L below: F's row work done
+// redundantly by the tile workgroups, the panel replaced by an in-register
+// rank-2 update of the tile; model scripts/models/sytrd_tail_model.py), and
+// in columns where blocked and tail matrices meet, S and L share a launch.
+//
 // The recurrence (unnormalised xh, scalars one launch late) is modelled
 // exactly in scripts/models/sytrd_fused_model.py (fp64, 1e-15).  Storage:
 // row-major, UPPER triangle maintained; output d, e, tau and reflector j in
@@ -127,9 +133,9 @@ __device__ inline void hh_scalars(double alpha, double sig2, double& beta, doubl
 // launch whose active matrices all have the same workgroup count passes
 // -count instead (one dependent table read less per launch: the batch of
 // equal-size largest factors is the inverse update's critical chain)
-__device__ __forceinline__ void find_mat(const int* __restrict__ offs, int nact, int& mi,
-                                         int& base) {
-  const int lane = threadIdx.x & 63, b = blockIdx.x;
+__device__ __forceinline__ void find_mat_b(const int* __restrict__ offs, int nact, int b,
+                                           int& mi, int& base) {
+  const int lane = threadIdx.x & 63;
   if (nact < 0) {      // uniform launch: every active matrix has -nact workgroups (no table read)
     mi = b / -nact;
     base = mi * -nact;
@@ -149,6 +155,10 @@ __device__ __forceinline__ void find_mat(const int* __restrict__ offs, int nact,
   }
   mi = cnt - 1;
   base = offs[mi];
+}
+__device__ __forceinline__ void find_mat(const int* __restrict__ offs, int nact, int& mi,
+                                         int& base) {
+  find_mat_b(offs, nact, blockIdx.x, mi, base);
 }
 
 // ------------------------------------------------------------------- F
@@ -789,27 +799,424 @@ __global__ __launch_bounds__(256) void red_symv_kernel(const RMat* __restrict__ 
   symv_body(M, base, j);
 }
 
+// ------------------------------------------------------------------- L
+// The single-launch tail (model: scripts/models/sytrd_tail_model.py).  Once a
+// matrix's trailing part is small (n - j0 <= the tail size, j0 a panel start
+// whose U flushed the panel), column k > j0 is ONE launch: F's row work moves
+// into the tile workgroups (each finishes column k-1 redundantly for the 192
+// rows its half tile touches) and the panel goes away -- the launch applies
+// column k-1's rank-2 update to its tile in registers, stores it (rows >= k+2:
+// row k+1 is read by every workgroup of the launch, its update lives in AV),
+// then runs the symv of column k on the updated tile.  Per column that is one
+// dependent launch instead of two and no V / W panel; the price is a
+// read-modify-write of the trailing upper triangle, which is L2 / MALL
+// resident at these sizes.
+//
+// Entering L(k) (slot ps = what S(k-1) / L(k-1) left): storage rows >= k+1 =
+// A^(k-1); AV = row k of A^(k-1); XH = xh_{k-1}; P / TS / DS its partial sums;
+// SC = alpha_{k-1}, d_{k-1}.  Row slots: 0..127 the K block's rows (the
+// tile's columns), 128..191 the I half's rows (off-diagonal tiles only).
+// The diagonal half 0 of block b owns block b's outputs (XH, AV, DS, the
+// reflector); workgroup 0 the scalars.  k == n-1: one workgroup, scalars only.
+constexpr int TSLOT = 192;
+
+__device__ __forceinline__ void tail_vw(double tau, double s, double alpha2, bool pivot, float xh,
+                                        float a, float yh, float& v, float& w) {
+  v = pivot ? 1.f : (float)(s * (double)xh);
+  w = (float)(tau * ((double)a + s * (double)yh) + alpha2 * (double)v);
+}
+
+// the half tile (I, K, hr) of L: column k-1's rank-2 update applied to the
+// loaded values (row k+1 taken from a_k), rows >= k+2 stored, then the symv
+// of column k on the updated values (as symv_halves).  Thread: rows
+// 4 R .. 4 R + 3 of the half x columns 8 cg .. 8 cg + 7.  Every operand comes
+// from LDS as 16-byte reads issued together; the diagonal masks are selects.
+template <bool DIAG>
+__device__ __forceinline__ void tail_tile(const fx4 (&at)[4][2], const float* sv, const float* sw,
+                                          const float* sx, const float* sa, float (*cred)[TB],
+                                          float* rsum, AS1 float* gA, const RMat& M, int cs, int k,
+                                          int I, int K, int hr, double& tp) {
+  const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6;
+  const int rg = lane >> 4, cg = lane & 15, R = q * 4 + rg;
+  const int n = M.n, ib = I * TB + hr * HT;
+  const unsigned uld = (unsigned)M.ld, ulda = (unsigned)M.lda;
+  const int rs = (DIAG ? hr * HT : TB) + 4 * R;          // slot of this thread's first row
+  const fx4 vr4 = *(const fx4*)(sv + rs), wr4 = *(const fx4*)(sw + rs), xr4 = *(const fx4*)(sx + rs);
+  const fx4 vc0 = *(const fx4*)(sv + 8 * cg), vc1 = *(const fx4*)(sv + 8 * cg + 4);
+  const fx4 wc0 = *(const fx4*)(sw + 8 * cg), wc1 = *(const fx4*)(sw + 8 * cg + 4);
+  const fx4 xc0 = *(const fx4*)(sx + 8 * cg), xc1 = *(const fx4*)(sx + 8 * cg + 4);
+  const fx4 ac0 = *(const fx4*)(sa + 8 * cg), ac1 = *(const fx4*)(sa + 8 * cg + 4);
+  const float vr[4] = {vr4.x, vr4.y, vr4.z, vr4.w}, wr[4] = {wr4.x, wr4.y, wr4.z, wr4.w};
+  const float xrv[4] = {xr4.x, xr4.y, xr4.z, xr4.w};
+  const float vc[8] = {vc0.x, vc0.y, vc0.z, vc0.w, vc1.x, vc1.y, vc1.z, vc1.w};
+  const float wc[8] = {wc0.x, wc0.y, wc0.z, wc0.w, wc1.x, wc1.y, wc1.z, wc1.w};
+  const float xcv[8] = {xc0.x, xc0.y, xc0.z, xc0.w, xc1.x, xc1.y, xc1.z, xc1.w};
+  const float acv[8] = {ac0.x, ac0.y, ac0.z, ac0.w, ac1.x, ac1.y, ac1.z, ac1.w};
+  float av[4][8];
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const bool piv = (ib + 4 * R + rr == k + 1);
+    const float t[8] = {at[rr][0].x, at[rr][0].y, at[rr][0].z, at[rr][0].w,
+                        at[rr][1].x, at[rr][1].y, at[rr][1].z, at[rr][1].w};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) av[rr][c] = piv ? acv[c] : t[c] - (vr[rr] * wc[c] + wr[rr] * vc[c]);
+  }
+  // store rows >= k+2 (row k+1 stays A^(k-1): every workgroup reads it), upper, inside n.
+  // Plain stores: the line stays in this XCD's L2, and within a 128-column
+  // window the same workgroup index (same XCD) reads the tile next column;
+  // write-through (sc1) stores measured slower (profiles/r6_wt_*.log)
+  const int gc0 = K * TB + 8 * cg;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int gr = ib + 4 * R + rr;
+    AS1 float* dst = gA + (unsigned)gr * ulda + gc0;
+    const bool rok = (gr >= k + 2) & (gr < n);
+    if (rok & (gc0 + 8 <= n) & (!DIAG || gc0 >= gr)) {
+      const fx4 o0 = {av[rr][0], av[rr][1], av[rr][2], av[rr][3]};
+      const fx4 o1 = {av[rr][4], av[rr][5], av[rr][6], av[rr][7]};
+      *(AS1 fx4*)dst = o0;
+      *(AS1 fx4*)(dst + 4) = o1;
+    } else if (rok) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        if ((gc0 + c < n) & (!DIAG || gc0 + c >= gr)) dst[c] = av[rr][c];
+    }
+  }
+  float rp[4], cp[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) cp[c] = 0.f;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      if (DIAG) {   // upper triangle: row sums take col >= row, column sums col > row
+        const int lr = hr * HT + 4 * R + rr, lc = 8 * cg + c;
+        acc += (lc >= lr) ? av[rr][c] * xcv[c] : 0.f;
+        cp[c] += (lc > lr) ? av[rr][c] * xrv[rr] : 0.f;
+      } else {
+        acc += av[rr][c] * xcv[c];
+        cp[c] += av[rr][c] * xrv[rr];
+      }
+    }
+    rp[rr] = row16_sum(acc);
+  }
+#pragma unroll
+  for (int c = 0; c < 8; ++c) cp[c] = swap_sum32(swap_sum16(cp[c]));
+  if (rg == 0) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) cred[q][8 * cg + c] = cp[c];
+  }
+  const float myrow = cg == 0 ? rp[0] : (cg == 1 ? rp[1] : (cg == 2 ? rp[2] : rp[3]));
+  const float myx = cg == 0 ? xrv[0] : (cg == 1 ? xrv[1] : (cg == 2 ? xrv[2] : xrv[3]));
+  if (DIAG) {
+    if (cg < 4) rsum[4 * R + cg] = myrow;
+  } else if (cg < 4) {
+    gptr(M.P)[cs * M.sP + (unsigned)(2 * K) * uld + ib + 4 * R + cg] = myrow;
+    tp = (double)myx * (double)myrow;
+  }
+}
+
+template <int RB>
+__device__ __forceinline__ void tail_body(const RMat& M, int local, int k, bool first) {
+  constexpr int PK = RB / 4;
+  constexpr int TQ = (RB * (RB + 1) + 1023) / 1024;
+  static_assert(RB <= 64, "DS partials: one lane per row block");
+  __shared__ float sq[4][TSLOT];        // per quarter of the P columns: yh partial of each slot row
+  __shared__ __attribute__((aligned(16))) float sv[TSLOT], sw[TSLOT], sx[TSLOT], sa[TB];
+  __shared__ float cred[4][TB];
+  __shared__ float rsum[HT];
+  __shared__ double sdk[2], stt[4], sds[2][2], tred[4];
+  const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6;
+  const int n = M.n, nt = M.nt;
+  const unsigned uld = (unsigned)M.ld, ulda = (unsigned)M.lda;
+  const int cs = k & 1, ps = cs ^ 1;
+  const int s0p = k / TB, s0 = (k + 1) / TB;
+  const bool last = (k == n - 1), has1 = !last;
+  int I = 0, K = 0;
+  const int hr = local & 1;
+  if (!last) {
+    tri_index(local >> 1, nt - s0, I, K);
+    I += s0; K += s0;
+  }
+  const bool diag = (I == K);
+  const bool owner = !last && diag && hr == 0;
+  const int nslot = last ? 0 : (diag ? TB : TSLOT);
+  const int ib = I * TB + hr * HT;                       // first row of the half tile
+  auto slot_row = [&](int sl) -> int { return sl < TB ? K * TB + sl : ib + (sl - TB); };
+  const AS1 float* DSp = gptr(M.DS) + ps * M.sDS;
+  const AS1 float* TSp = gptr(M.TS) + ps * M.sTS;
+  const AS1 float* Pp = gptr(M.P) + ps * M.sP;
+  const AS1 float* XHp = gptr(M.XH) + ps * M.sX;
+  const AS1 float* AVp = gptr(M.AV) + ps * M.sX;
+  AS1 float* const gA = gptr(M.A);
+  AS1 float* const gSC = gptr(M.SC);
+  const int ntri = (nt - s0p) * (nt - s0p + 1);          // half tiles of the previous launch
+  unsigned long long* const stamps = first ? g_stamps : nullptr;
+  const int j = k;
+  STAMP(1);
+
+  // ---- every load up front (clamped indices, out-of-range terms dropped at use)
+  const float dk = gld_if32(DSp, (unsigned)min(s0p + lane, nt - 1) * NK + (q & 1),
+                            (q < 2) & (s0p + lane < nt), 0.f);
+  fx4 tq[TQ];
+  const fx4 z4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < TQ; ++u)
+    tq[u] = gld_if32((const AS1 fx4*)TSp, (unsigned)(tid + 256 * u), 4 * (tid + 256 * u) < ntri, z4);
+  auto pcol_ok = [&](int col, int B) -> bool {
+    return (col >= 2 * s0p) & (col < 2 * nt) & (((col & 1) == 0) | ((col >> 1) <= B));
+  };
+  const int bk = k / TB, bk1 = (k + 1) / TB;
+  float pj = 0.f, pj1 = 0.f;                             // pivot rows k, k+1: lane = P column
+#pragma unroll
+  for (int h = 0; h < (2 * RB + 63) / 64; ++h) {
+    const int col = 2 * s0p + lane + 64 * h;
+    pj += gld_if32(Pp, (unsigned)col * uld + k, pcol_ok(col, bk), 0.f);
+    pj1 += gld_if32(Pp, (unsigned)col * uld + k + 1, has1 & pcol_ok(col, bk1), 0.f);
+  }
+  const float alpha = gSC[ps * 4];
+  const float dprev = gSC[ps * 4 + 1];
+  const float ak = AVp[k];
+  const float ak1 = gld_if32(AVp, k + 1, has1, 0.f);
+  const float xhk1 = gld_if32(XHp, k + 1, has1, 0.f);
+  // this wave's quarter of the P columns of slot rows lane + 64 g
+  float pk[3][2 * PK];
+#pragma unroll
+  for (int g = 0; g < 3; ++g) {
+    const int rc = min(slot_row(lane + 64 * g), n - 1);
+#pragma unroll
+    for (int i = 0; i < PK; ++i) {
+      const unsigned t2 = 2 * min(s0p + q + 4 * i, nt - 1);
+      pk[g][2 * i] = Pp[t2 * uld + rc];
+      pk[g][2 * i + 1] = Pp[(t2 + 1) * uld + rc];
+    }
+  }
+  // the slot row of this thread (tid < nslot): xh_{k-1}, a_{k-1}, storage row k+1
+  const int rme = slot_row(min(tid, TSLOT - 1));
+  const int rmc = min(rme, n - 1);
+  const float xhr = XHp[(unsigned)rmc];
+  const float avr = AVp[(unsigned)rmc];
+  const float arow = gld_if32(gA, (unsigned)(k + 1) * ulda + max(rmc, k + 1), has1, 0.f);
+  // the half tile: rows ib + 4 R + rr, columns K TB + 8 cg + 0..7
+  const int rg = lane >> 4, cg = lane & 15, R = q * 4 + rg;
+  fx4 at[4][2];
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      at[rr][h] = *(const AS1 fx4*)(gA + (unsigned)min(ib + 4 * R + rr, nt * TB - 1) * ulda +
+                                    K * TB + 8 * cg + 4 * h);
+  __builtin_amdgcn_sched_barrier(0);
+
+  // ---- global sums of column k-1, the slot rows' yh partials
+  {
+    const double dsum = wave_sum_d((double)dk);
+    if (q < 2 && lane == 0) sdk[q] = dsum;
+    double t = 0.0;
+#pragma unroll
+    for (int u = 0; u < TQ; ++u) {
+      const int f = 4 * (tid + 256 * u);
+      t += (f < ntri) ? (double)tq[u].x : 0.0;
+      t += (f + 1 < ntri) ? (double)tq[u].y : 0.0;
+      t += (f + 2 < ntri) ? (double)tq[u].z : 0.0;
+      t += (f + 3 < ntri) ? (double)tq[u].w : 0.0;
+    }
+    t = wave_sum_d(t);
+    if (lane == 0) stt[q] = t;
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+      const int B = slot_row(lane + 64 * g) / TB;
+      float yq = 0.f;
+#pragma unroll
+      for (int i = 0; i < PK; ++i) {
+        const int T = s0p + q + 4 * i;
+        yq += (T < nt) ? pk[g][2 * i] : 0.f;
+        yq += ((T < nt) & (T <= B)) ? pk[g][2 * i + 1] : 0.f;
+      }
+      sq[q][lane + 64 * g] = yq;
+    }
+  }
+  const float yk = wave_sum(pj), yk1 = wave_sum(pj1);
+  kfac_lds_barrier();
+  STAMP(2);
+
+  // ---- scalars of column k-1 (every thread, identically), pivot rows k, k+1
+  const double sig2 = sdk[0], xa = sdk[1];
+  const double xy = ((stt[0] + stt[1]) + (stt[2] + stt[3]));
+  double beta, tau, s;
+  hh_scalars((double)alpha, sig2, beta, tau, s);
+  const double vy = (double)ak + 2.0 * s * xa + s * s * xy;
+  const double alpha2 = -0.5 * tau * tau * vy;
+  float vk, wk, vk1 = 0.f, wk1 = 0.f;
+  tail_vw(tau, s, alpha2, true, 0.f, ak, yk, vk, wk);
+  if (has1) tail_vw(tau, s, alpha2, false, xhk1, ak1, yk1, vk1, wk1);
+  if (local == 0 && tid == 0) {
+    M.d[k - 1] = dprev;
+    M.e[k - 1] = (float)beta;
+    M.tau[k - 1] = (float)tau;
+    gA[(unsigned)(k - 1) * ulda + k] = (float)beta;
+    const float dkk = (float)((double)ak - 2.0 * (double)wk);
+    if (last) {
+      M.d[k] = dkk;
+      M.e[k] = 0.f;
+      M.tau[k] = 0.f;
+    } else {
+      gSC[cs * 4 + 1] = dkk;
+    }
+  }
+  if (last) return;
+  STAMP(3);
+
+  // ---- the slot rows: v, w of column k-1; x_k (-> xh_k), a_k = row k+1 of A^(k)
+  {
+    float v = 0.f, w = 0.f, xn = 0.f, an = 0.f;
+    if (tid < nslot) {
+      const int r = rme;
+      float yh = (sq[0][tid] + sq[1][tid]) + (sq[2][tid] + sq[3][tid]);
+      if (r >= k && r < n) {
+        if (r == k) {
+          v = vk; w = wk;
+        } else if (r == k + 1) {
+          v = vk1; w = wk1;
+        } else {
+          tail_vw(tau, s, alpha2, false, xhr, avr, yh, v, w);
+        }
+      }
+      const float x = avr - w - wk * v;
+      xn = (r >= k + 2 && r < n) ? x : 0.f;
+      an = (r >= k + 1 && r < n) ? arow - vk1 * w - wk1 * v : 0.f;
+      sv[tid] = v; sw[tid] = w; sx[tid] = xn;
+      if (tid < TB) sa[tid] = an;
+      if (owner && r < n) {
+        gptr(M.XH)[cs * M.sX + r] = xn;
+        gptr(M.AV)[cs * M.sX + r] = an;
+        if (r >= k + 1) gA[(unsigned)(k - 1) * ulda + r] = v;   // reflector k-1: v[k+1:]
+        if (r == k + 1) gSC[cs * 4] = x;                       // alpha_k
+      }
+    }
+    if (owner && q < 2) {        // block sums |xh_k|^2, xh_k . a_k (rows 0..127 = waves 0, 1)
+      const double s0v = wave_sum_d((double)xn * (double)xn);
+      const double s1v = wave_sum_d((double)xn * (double)an);
+      if (lane == 0) { sds[q][0] = s0v; sds[q][1] = s1v; }
+    }
+  }
+  kfac_lds_barrier();
+  STAMP(4);
+  if (owner && tid < 2)
+    gptr(M.DS)[cs * M.sDS + (long long)K * NK + tid] = (float)(sds[0][tid] + sds[1][tid]);
+
+  // ---- the tile: column k-1's rank-2 update, store, then the symv of column k
+  double tp = 0.0;
+  if (diag)
+    tail_tile<true>(at, sv, sw, sx, sa, cred, rsum, gA, M, cs, k, I, K, hr, tp);
+  else
+    tail_tile<false>(at, sv, sw, sx, sa, cred, rsum, gA, M, cs, k, I, K, hr, tp);
+  AS1 float* const Pc = gptr(M.P) + cs * M.sP;
+  STAMP(5);
+  kfac_lds_barrier();
+  if (tid < TB) {
+    float v = (cred[0][tid] + cred[1][tid]) + (cred[2][tid] + cred[3][tid]);
+    if (diag) {
+      const int rl = tid - hr * HT;
+      if (rl >= 0 && rl < HT) v += rsum[rl];
+    }
+    Pc[(unsigned)(2 * I + hr) * uld + K * TB + tid] = v;
+    tp += (double)sx[tid] * (double)v;
+  }
+  {
+    const double t = wave_sum_d(tp);
+    if (lane == 0) tred[q] = t;
+  }
+  kfac_lds_barrier();
+  if (tid == 0)
+    gptr(M.TS)[cs * M.sTS + local] = (float)((tred[0] + tred[1]) + (tred[2] + tred[3]));
+  STAMP(6);
+}
+
+template <int RB>
+__global__ __launch_bounds__(256) void red_tail_kernel(const RMat* __restrict__ mats,
+                                                       const int* __restrict__ offs, int nact,
+                                                       int k) {
+  unsigned long long* const stamps = blockIdx.x == 0 ? g_stamps : nullptr;
+  const int j = k;
+  STAMP(0);
+  int mi, base;
+  find_mat(offs, nact, mi, base);
+  const RMat M = mats[mi];
+  tail_body<RB>(M, blockIdx.x - base, k, blockIdx.x == 0);
+}
+
+// a column where blocked and tail matrices are both active: S(j) of the
+// blocked ones (workgroups 0 .. grid_s - 1) and L(j) of the tail ones in ONE
+// launch, so a mixed batch does not pay a third dependent launch per column
+template <int RB>
+__global__ __launch_bounds__(256) void red_symv_tail_kernel(const RMat* __restrict__ mats,
+                                                            const int* __restrict__ offs_s,
+                                                            int nact_s, int grid_s,
+                                                            const int* __restrict__ offs_l,
+                                                            int nact_l, int j) {
+  int mi, base;
+  if ((int)blockIdx.x < grid_s) {
+    find_mat_b(offs_s, nact_s, blockIdx.x, mi, base);
+    const RMat M = mats[mi];
+    symv_body(M, base, j);
+  } else {
+    const int b = blockIdx.x - grid_s;
+    find_mat_b(offs_l, nact_l, b, mi, base);
+    const RMat M = mats[mi];
+    tail_body<RB>(M, b - base, j, false);
+  }
+}
+
 // ------------------------------------------------------------------ host
+constexpr int NKIND = 4;        // F, U, S, L
 struct RPlan {
   RMat* d_mats = nullptr;
-  int* d_offs = nullptr;        // [3][nmax][nm + 1]: F, U, S workgroup offsets
+  int* d_offs = nullptr;        // [NKIND][nmax][nm + 1]: F, U, S, L workgroup offsets
   std::vector<int> n_sorted;    // descending
-  std::vector<int> grid[3];     // [nmax] total workgroups per launch kind
-  std::vector<int> nact[3];
+  std::vector<int> grid[NKIND]; // [nmax] total workgroups per launch kind
+  std::vector<int> nact[NKIND];
   std::vector<int> rb;          // [nmax] F unroll class
+  std::vector<int> rbt;         // [nmax] L unroll class
   int nmax = 0;
   hipGraphExec_t exec = nullptr;
 };
 
 inline int h_tri(int m) { return m * (m + 1) / 2; }
 
-// workgroups of matrix n at column j: F, U (panel start only), S
-void counts(int n, int j, int out[3]) {
+// trailing size (rows) from which a matrix's columns run as single tail
+// launches (KFAC_REDUCE_TAIL, 0 = never); capped so the tail's P partials fit
+// its unroll classes (<= 40 row blocks)
+constexpr int TAIL_MAX = 38 * TB;
+int tail_rows() {
+  static const int t = [] {
+    const char* e = getenv("KFAC_REDUCE_TAIL");
+    const int v = e ? atoi(e) : 768;
+    return std::max(0, std::min(v, TAIL_MAX));
+  }();
+  return t;
+}
+
+// the panel start j0 after which matrix n runs tail launches (n: no tail)
+int tail_start(int n) {
+  const int T = tail_rows();
+  if (T <= 0) return n;
+  const int j0 = n <= T ? 0 : (n - T + NB - 1) / NB * NB;
+  return j0 >= n - 1 ? n : j0;
+}
+
+// workgroups of matrix n at column j: F, U (panel start only), S -- blocked
+// columns j <= j0 -- and L, the tail columns j > j0
+void counts(int n, int j, int out[NKIND]) {
   const int nt = (n + TB - 1) / TB, nf = (n + FB - 1) / FB;
   const int ntr = nt - (j + 1) / TB;
-  out[0] = (j <= n - 1) ? nf - std::min(((j + 1) / TB) * (TB / FB), j / FB) : 0;
-  out[1] = (j % NB == 0 && j > 0 && j <= n - 2) ? h_tri(ntr) : 0;
-  out[2] = (j <= n - 2) ? 2 * h_tri(ntr) / SNH + ntr : 0;
+  const int j0 = tail_start(n);
+  const bool blk = j <= j0;
+  out[0] = (blk && j <= n - 1) ? nf - std::min(((j + 1) / TB) * (TB / FB), j / FB) : 0;
+  out[1] = (blk && j % NB == 0 && j > 0 && j <= n - 2) ? h_tri(ntr) : 0;
+  out[2] = (blk && j <= n - 2) ? 2 * h_tri(ntr) / SNH + ntr : 0;
+  out[3] = blk ? 0 : (j <= n - 2 ? 2 * h_tri(ntr) : (j == n - 1 ? 1 : 0));
 }
 
 int rb_class(int blocks) {
@@ -831,32 +1238,66 @@ const bool g_upd_x6 = [] {
   return !(e && !strcmp(e, "f32"));
 }();
 
+template <int RB>
+void launch_tail(const RPlan& P, const int* of, int j, hipStream_t s) {
+  hipLaunchKernelGGL(red_tail_kernel<RB>, dim3(P.grid[3][j]), dim3(256), 0, s, P.d_mats, of,
+                     P.nact[3][j], j);
+}
+
 int enqueue(const RPlan& P, hipStream_t stream) {
   const int nm = (int)P.n_sorted.size();
   const size_t kstride = (size_t)P.nmax * (nm + 1);
   for (int j = 0; j < P.nmax; ++j) {
     const int* of = P.d_offs + (size_t)j * (nm + 1);
-    switch (P.rb[j]) {
-      case 8: launch_fin<8>(P, of, j, stream); break;
-      case 16: launch_fin<16>(P, of, j, stream); break;
-      case 24: launch_fin<24>(P, of, j, stream); break;
-      case 40: launch_fin<40>(P, of, j, stream); break;
-      case 64: launch_fin<64>(P, of, j, stream); break;
-      case 96: launch_fin<96>(P, of, j, stream); break;
-      default: launch_fin<128>(P, of, j, stream); break;
+    if (P.grid[0][j] > 0) {
+      switch (P.rb[j]) {
+        case 8: launch_fin<8>(P, of, j, stream); break;
+        case 16: launch_fin<16>(P, of, j, stream); break;
+        case 24: launch_fin<24>(P, of, j, stream); break;
+        case 40: launch_fin<40>(P, of, j, stream); break;
+        case 64: launch_fin<64>(P, of, j, stream); break;
+        case 96: launch_fin<96>(P, of, j, stream); break;
+        default: launch_fin<128>(P, of, j, stream); break;
+      }
     }
     if (P.grid[1][j] > 0) {
-      if (g_upd_x6) {
-        hipLaunchKernelGGL(red_upd_kernel<true>, dim3(P.grid[1][j]), dim3(256), 0, stream,
-                           P.d_mats, of + kstride, P.nact[1][j], j);
-      } else {
-        hipLaunchKernelGGL(red_upd_kernel<false>, dim3(P.grid[1][j]), dim3(256), 0, stream,
-                           P.d_mats, of + kstride, P.nact[1][j], j);
+      const dim3 g(P.grid[1][j]);
+      const int* ou = of + kstride;
+      if (g_upd_x6)
+        hipLaunchKernelGGL(red_upd_kernel<true>, g, dim3(256), 0, stream, P.d_mats, ou,
+                           P.nact[1][j], j);
+      else
+        hipLaunchKernelGGL(red_upd_kernel<false>, g, dim3(256), 0, stream, P.d_mats, ou,
+                           P.nact[1][j], j);
+    }
+    if (P.grid[2][j] > 0 && P.grid[3][j] > 0) {
+      const int* os = of + 2 * kstride;
+      const int* ot = of + 3 * kstride;
+      const dim3 g(P.grid[2][j] + P.grid[3][j]);
+#define KFAC_ST(RB_)                                                                          \
+  hipLaunchKernelGGL(red_symv_tail_kernel<RB_>, g, dim3(256), 0, stream, P.d_mats, os,        \
+                     P.nact[2][j], P.grid[2][j], ot, P.nact[3][j], j)
+      switch (P.rbt[j]) {
+        case 8: KFAC_ST(8); break;
+        case 16: KFAC_ST(16); break;
+        case 24: KFAC_ST(24); break;
+        default: KFAC_ST(40); break;
       }
+#undef KFAC_ST
+      continue;
     }
     if (P.grid[2][j] > 0)
       hipLaunchKernelGGL(red_symv_kernel, dim3(P.grid[2][j]), dim3(256), 0, stream, P.d_mats,
                          of + 2 * kstride, P.nact[2][j], j);
+    if (P.grid[3][j] > 0) {
+      const int* ot = of + 3 * kstride;
+      switch (P.rbt[j]) {
+        case 8: launch_tail<8>(P, ot, j, stream); break;
+        case 16: launch_tail<16>(P, ot, j, stream); break;
+        case 24: launch_tail<24>(P, ot, j, stream); break;
+        default: launch_tail<40>(P, ot, j, stream); break;
+      }
+    }
   }
   return (int)hipGetLastError();
 }
@@ -910,45 +1351,51 @@ RPlan* plan_for(const KfacReduceRecord* recs, int count, bool capture, int* err)
     if ((*err = (int)hipMemcpy(P.d_mats, mats.data(), sizeof(RMat) * mats.size(),
                                hipMemcpyHostToDevice)) != 0)
       return nullptr;
-    std::vector<int> offs((size_t)3 * P.nmax * (nm + 1), 0);
-    for (int k = 0; k < 3; ++k) {
+    std::vector<int> offs((size_t)NKIND * P.nmax * (nm + 1), 0);
+    for (int k = 0; k < NKIND; ++k) {
       P.grid[k].assign(P.nmax, 0);
       P.nact[k].assign(P.nmax, 0);
     }
     P.rb.assign(P.nmax, 0);
+    P.rbt.assign(P.nmax, 0);
     for (int j = 0; j < P.nmax; ++j) {
-      int acc[3] = {0, 0, 0};
+      int acc[NKIND] = {0, 0, 0, 0};
+      int rbf = 1, rbl = 1;     // row blocks of the previous launch's partials (F / L readers)
       for (int i = 0; i < nm; ++i) {
-        int cnt[3];
+        int cnt[NKIND];
         counts(P.n_sorted[i], j, cnt);
-        for (int k = 0; k < 3; ++k) {
+        const int blocks = (P.n_sorted[i] + TB - 1) / TB - j / TB;
+        if (cnt[0] > 0) rbf = std::max(rbf, blocks);
+        if (cnt[3] > 0) rbl = std::max(rbl, blocks);
+        for (int k = 0; k < NKIND; ++k) {
           offs[((size_t)k * P.nmax + j) * (nm + 1) + i] = acc[k];
           if (cnt[k] > 0) P.nact[k][j] = i + 1;
           acc[k] += cnt[k];
         }
       }
-      for (int k = 0; k < 3; ++k) {
+      for (int k = 0; k < NKIND; ++k) {
         offs[((size_t)k * P.nmax + j) * (nm + 1) + nm] = acc[k];
         P.grid[k][j] = acc[k];
         // uniform launch: the active matrices (a prefix: sizes descend) share one count
         const int na = P.nact[k][j];
         if (na > 0 && acc[k] % na == 0) {
-          int c0[3];
+          int c0[NKIND];
           counts(P.n_sorted[0], j, c0);
           bool uni = true;
           for (int i = 1; i < na && uni; ++i) {
-            int ci[3];
+            int ci[NKIND];
             counts(P.n_sorted[i], j, ci);
             uni = ci[k] == c0[k];
           }
           if (uni && c0[k] > 0 && c0[k] * na == acc[k]) P.nact[k][j] = -c0[k];
         }
       }
-      // F reads the partials of S(j-1): nt - j / TB blocks of the largest matrix
-      const int nt0 = (P.n_sorted[0] + TB - 1) / TB;
+      // F / L read the partials of the previous launch: nt - j / TB blocks
       static const int rb_min = getenv("KFAC_REDUCE_RB_MIN") ? atoi(getenv("KFAC_REDUCE_RB_MIN")) : 1;
-      P.rb[j] = rb_class(std::max(rb_min, nt0 - j / TB));
+      P.rb[j] = rb_class(std::max(rb_min, rbf));
       if (P.rb[j] < 0) { *err = -6; return nullptr; }
+      P.rbt[j] = rbl <= 8 ? 8 : (rbl <= 16 ? 16 : (rbl <= 24 ? 24 : 40));
+      if (rbl > 40) { *err = -6; return nullptr; }
     }
     if ((*err = (int)hipMalloc(&P.d_offs, sizeof(int) * offs.size())) != 0) return nullptr;
     if ((*err = (int)hipMemcpy(P.d_offs, offs.data(), sizeof(int) * offs.size(),

@@ -18,6 +18,7 @@ import torch
 from . import _lib
 
 __all__ = ['outer_reciprocal', 'precondition_eigen', 'precondition_inverse', 'kl_dot',
+           'kl_scale_reference',
            'apply_gradients']
 
 
@@ -131,6 +132,18 @@ def kl_dot(pairs):
 def kl_scale(vg, lr, kl_clip):
     """Host-side KL-clip scale (CPU path): None when vg == 0."""
     s = float(vg) * lr ** 2
+    if s == 0.0:
+        return None
+    return min(1.0, math.sqrt(kl_clip / abs(s)))
+
+
+def kl_scale_reference(pairs, lr, kl_clip):
+    """KL-clip scale of the host path with the reference's rounding
+    (/root/reference/kfac/preconditioner.py:660-682): one float32 sum of
+    v * g * lr^2 per tensor, accumulated as a Python float; None when 0."""
+    s = 0.0
+    for v, g in pairs:
+        s += (v.reshape(g.shape) * g * lr ** 2).sum().item()
     if s == 0.0:
         return None
     return min(1.0, math.sqrt(kl_clip / abs(s)))

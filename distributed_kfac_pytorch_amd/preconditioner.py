@@ -707,8 +707,9 @@ class KFAC(optim.Optimizer):
     def side_streams(self):
         """The streams other than the current one that K-FAC's last step may
         have left work on: the factor stream, the fused chain's side stream,
-        the eigensolver's workers, and the lagged-inverse stream unless a
-        lagged update is still in flight (that one runs on purpose).  Not the
+        the eigensolver's workers and the lagged-inverse stream -- the last
+        two only when no lagged update is in flight (that one runs on purpose
+        on both).  Not the
         deferred factor all-reduce, which is joined by join_factor_comm()."""
         out = []
         if self._factor_stream is not None:
@@ -716,7 +717,12 @@ class KFAC(optim.Optimizer):
         side = getattr(self.fused, '_side', None)
         if side is not None:
             out.append(side)
-        if self._inv_stream is not None and not self.inverses_in_flight:
+        if self.inverses_in_flight:
+            # the lagged solve owns _inv_stream AND the eigensolver's worker
+            # streams until it is joined: waiting on either would serialise
+            # the overlap inverse_lag exists for
+            return out
+        if self._inv_stream is not None:
             out.append(self._inv_stream)
         if self.layers and self.layers[0].module.weight.is_cuda:
             from .ops import eigen as eigen_ops
@@ -1486,5 +1492,10 @@ class KFAC(optim.Optimizer):
         g = self.param_groups[0]
         if self._fused_kl is not None:
             return _DeviceKLScale(self._fused_kl, g['lr'], g['kl_clip'])
-        vg = precond_ops.kl_dot(self._grad_pairs())
+        pairs = self._grad_pairs()
+        if not pairs[0][0].is_cuda:
+            # host path: the reference's own arithmetic, so a CPU run
+            # reproduces its trajectory (tests/test_training_quality.py)
+            return precond_ops.kl_scale_reference(pairs, g['lr'], g['kl_clip'])
+        vg = precond_ops.kl_dot(pairs)
         return _DeviceKLScale(vg, g['lr'], g['kl_clip'])

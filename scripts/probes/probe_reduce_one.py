@@ -47,6 +47,15 @@ def main():
                            ('last 64', slice(n - 66, n - 2))):
             f = full[rows]
             nxt = full[rows.start + 1:rows.stop + 1]
+            if (f[:, 6] > 0).all():
+                # tail launch L: 0 start, 1 record, 2 loads + sums, 3 scalars,
+                # 4 slot rows, 5 tile update + symv, 6 end
+                ph = [(f[:, k + 1] - f[:, k]).mean().item() for k in range(6)]
+                print(name, 'L phases ns: ' + ' '.join('%6.0f' % v for v in ph),
+                      '| L total %6.0f | L->L %6.0f | col %6.0f' % (
+                          (f[:, 6] - f[:, 0]).mean().item(), (nxt[:, 0] - f[:, 6]).mean().item(),
+                          (nxt[:, 0] - f[:, 0]).mean().item()))
+                continue
             ph = [(f[:, k + 1] - f[:, k]).mean().item() for k in range(4)]
             print(name, 'F phases ns: ' + ' '.join('%6.0f' % v for v in ph),
                   '| F total %6.0f | F->S gap %6.0f | S tile %6.0f (rec %5.0f load %5.0f rest %5.0f) | S part %6.0f | S->F %6.0f | col %6.0f' % (

@@ -1,0 +1,131 @@
+"""Multi-step training quality of the GPU paths.
+
+The reference K-FAC's 100-step loss curve on the ResNet-20 task of
+tests/_training_task.py (fixture written on the CPU from /root/reference/kfac
+by scripts/make_training_fixture.py) against:
+
+(i)  this framework on the GPU in fp32 (precond_precision='fp32', no autocast,
+     eager): the first steps before the trajectories decorrelate, the first
+     step's preconditioned gradients, and every 25-step window of the loss;
+(ii) the bench configuration (bf16 autocast numerics through bf16-stored
+     weights with fp32 masters, bf16x6 preconditioning, the whole step as
+     replayed hipGraphs, early A factors): every 25-step window within a band
+     of run (i) -- a stale eigenbasis under graphs or a wrong EMA order shows
+     up here, not in the one-step parity tests.
+
+Bands: a 1-ulp perturbation of the KL-clip scale alone moves the CPU run's
+windows by up to 0.026 (chaotic divergence over 100 steps); K-FAC switched off
+(plain SGD) moves window 3 by 0.15.
+"""
+import os
+
+import pytest
+import torch
+
+import distributed_kfac_pytorch_amd as kfac
+from distributed_kfac_pytorch_amd import graphs
+from distributed_kfac_pytorch_amd.ops import mixed
+from tests import _training_task as T
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _fixture():
+    return torch.load(os.path.join(ROOT, T.FIXTURE), weights_only=True)
+
+
+def _band(a, ref, abs_tol, rel_tol):
+    return [abs(x - r) <= abs_tol + rel_tol * r for x, r in zip(a, ref)]
+
+
+def _fp32_run():
+    dev = torch.device('cuda')
+    net = T.model().to(dev)
+    pre = kfac.KFAC(net, precond_precision='fp32', **T.KFAC_KW)
+    opt = torch.optim.SGD(net.parameters(), **T.SGD_KW)
+    losses, grads0 = [], None
+    for i, (x, y) in enumerate(T.batches()):
+        x, y = x.to(dev), y.to(dev)
+        opt.zero_grad()
+        loss = T.loss_fn(net(x), y)
+        loss.backward()
+        pre.step()
+        if i == 0:
+            grads0 = [p.grad.detach().cpu().clone() for p in net.parameters()]
+        opt.step()
+        losses.append(float(loss))
+    return losses, grads0
+
+
+def _bench_config_run():
+    dev = torch.device('cuda')
+    net = T.model().to(dev).to(memory_format=torch.channels_last)
+    weights = mixed.BF16Weights(net)
+    opt = torch.optim.SGD(weights.parameters(net), fused=True, **T.SGD_KW)
+    pre = kfac.KFAC(net, precond_precision='bf16x6', early_factors=True, **T.KFAC_KW)
+    pre.set_grad_params(weights.grad_params())
+    x = torch.zeros(T.BATCH, 3, 32, 32, device=dev).to(memory_format=torch.channels_last)
+    y = torch.zeros(T.BATCH, dtype=torch.long, device=dev)
+
+    def forward_backward():
+        net.zero_grad(set_to_none=False)
+        with torch.autocast(device_type='cuda', dtype=torch.bfloat16):
+            loss = T.loss_fn(net(x), y)
+        loss.backward()
+        weights.grads_to_master()
+        return loss
+
+    def update():
+        pre.step()
+        opt.step()
+        weights.master_to_model()
+
+    def train_step():
+        loss = forward_backward()
+        update()
+        return loss
+
+    step = graphs.GraphedTrainStep(train_step, pre, [opt], forward_backward=forward_backward,
+                                   update=update)
+    losses = []
+    for xb, yb in T.batches():
+        x.copy_(xb)
+        y.copy_(yb)
+        losses.append(float(step()))
+    return losses, step
+
+
+@pytest.fixture(scope='module')
+def fp32_run():
+    return _fp32_run()
+
+
+def test_gpu_fp32_tracks_reference_curve(fp32_run):
+    fx = _fixture()
+    losses, grads0 = fp32_run
+    ref = fx['losses'].tolist()
+    # before the trajectories decorrelate: step by step
+    for i in range(5):
+        assert abs(losses[i] - ref[i]) <= 2e-3 * ref[i], (i, losses[:5], ref[:5])
+    # the first step's preconditioned gradients (HIP factors, eigensolver, chain)
+    for g, r in zip(grads0, fx['grads0']):
+        assert (g - r).norm() <= 1e-3 * r.norm() + 1e-8, (g - r).norm() / r.norm()
+    w, wr = T.window_means(losses), T.window_means(ref)
+    assert all(_band(w, wr, 0.02, 0.15)), (w, wr)
+
+
+def test_bench_config_tracks_fp32_run(fp32_run):
+    fx = _fixture()
+    base, _ = fp32_run
+    losses, step = _bench_config_run()
+    assert step.replays > 50, step.replays          # the run was graphed
+    w, wb = T.window_means(losses), T.window_means(base)
+    assert all(_band(w, wb, 0.05, 0.25)), (w, wb)
+    # and against the reference itself
+    wr = T.window_means(fx['losses'].tolist())
+    assert all(_band(w, wr, 0.05, 0.25)), (w, wr)
+    sgd = fx['sgd_losses'].tolist()
+    print('[training-quality] K-FAC ref %s | fp32 %s | bench cfg %s | SGD %s' % (
+        ' '.join('%.3f' % v for v in wr), ' '.join('%.3f' % v for v in wb),
+        ' '.join('%.3f' % v for v in w), ' '.join('%.3f' % v for v in T.window_means(sgd))))
