@@ -32,8 +32,21 @@ FLAGS = ['-O3', '-std=c++17', '-fPIC', '--offload-arch=' + ARCH, '-munsafe-fp-at
 LIBS = []
 
 
+# The two-stage eigensolver (dense -> band -> tridiagonal, round 4) loses to
+# the one-stage path on every routing measured (profiles/r5_eig_two_stage_
+# mid_routing.log); it is built only on request: KFAC_BUILD_TWO_STAGE=1.
+TWO_STAGE_SOURCES = ('eig_sy2sb.hip', 'eig_sb2st.hip', 'eig_q2.hip')
+
+
+def two_stage_enabled():
+    return os.environ.get('KFAC_BUILD_TWO_STAGE') == '1'
+
+
 def sources():
-    return sorted(glob.glob(os.path.join(CSRC, '*.hip')))
+    srcs = sorted(glob.glob(os.path.join(CSRC, '*.hip')))
+    if not two_stage_enabled():
+        srcs = [s for s in srcs if os.path.basename(s) not in TWO_STAGE_SOURCES]
+    return srcs
 
 
 def _stale(target, deps):
@@ -54,12 +67,21 @@ def _compile(src):
     return obj
 
 
+def compile_optional():
+    """Compile (not link) the opt-in sources, so every .hip stays buildable."""
+    os.makedirs(BUILD, exist_ok=True)
+    return [_compile(os.path.join(CSRC, f)) for f in TWO_STAGE_SOURCES]
+
+
 def build(force=False, jobs=None, verbose=True):
     os.makedirs(BUILD, exist_ok=True)
     os.makedirs(OUT_DIR, exist_ok=True)
     srcs = sources()
     deps = srcs + glob.glob(os.path.join(CSRC, '*.h'))
-    if not force and not _stale(LIB, deps):
+    stamp = LIB + '.sources'
+    listing = '\n'.join(os.path.basename(x) for x in srcs)
+    same_set = os.path.exists(stamp) and open(stamp).read() == listing
+    if not force and same_set and not _stale(LIB, deps):
         return LIB
     if force:
         for o in glob.glob(os.path.join(BUILD, '*.o')):
@@ -73,6 +95,8 @@ def build(force=False, jobs=None, verbose=True):
     if r.returncode != 0:
         raise RuntimeError('link failed:\n{}\n{}'.format(' '.join(cmd), r.stderr))
     os.replace(tmp, LIB)
+    with open(stamp, 'w') as f:
+        f.write(listing)
     if verbose:
         print('built', LIB, 'from', len(objs), 'sources for', ARCH)
     return LIB

@@ -16,8 +16,22 @@
 // preconditioning chain, split once per inverse update -- and the other, the
 // per-step operand, fp32 and split while it is staged: half the per-k-step
 // split work of PREC_BF16X6F
+// Low-plane mixed modes (one operand stored as 16-bit planes once per inverse
+// update -- the eigenvector operand -- the other fp32, converted while staged):
+// PREC_F16X3A / B: fp16 hi / lo planes, x' = x 2^e ~= hi + lo (22 significand
+//   bits), three v_mfma_f32_32x32x16_f16 per product (lo.hi + hi.lo + hi.hi);
+//   the eigenvector planes carry e = 14 (|q| <= 1), the fp32 operand e = 14 -
+//   exponent(max |x|) from a per-problem max slot its producer filled
+//   (atomicMax of |x| bits: deterministic), undone in the epilogue (exact).
+// PREC_H1A / B, PREC_F1A / B: one bf16 / fp16 plane, one MFMA per product:
+//   the reference's inv_dtype = bfloat16 / float16 preconditioning
+//   (kfac/layers/base.py:435-441,463,470) on the grouped chain.
 enum { PREC_F32 = 0, PREC_BF16X3 = 1, PREC_BF16X6 = 2, PREC_BF16X6F = 3, PREC_BF16X6A = 4,
-       PREC_BF16X6B = 5 };
+       PREC_BF16X6B = 5, PREC_F16X3A = 6, PREC_F16X3B = 7, PREC_H1A = 8, PREC_H1B = 9,
+       PREC_F1A = 10, PREC_F1B = 11 };
+// split_copy / store_planes modes of the low-plane eigenvector operands
+enum { STORE_F16X2 = 20, STORE_BF16X1 = 21, STORE_F16X1 = 22 };
+constexpr int LP_QEXP = 14;      // scale exponent of the fp16 eigenvector planes
 // EPI_SUB: C -= A B^T (f32); EPI_ATOMIC: C += A B^T with f32 atomics (split-K)
 enum { EPI_STORE = 0, EPI_HADAMARD = 1, EPI_HADAMARD_VEC = 2, EPI_FINAL = 3, EPI_SUB = 4,
        EPI_ATOMIC = 5 };
@@ -33,6 +47,9 @@ struct PGemm {
   const void* g_hi; const void* g_lo; long long ldg;
   int M, N, K, epi;
   int tile_begin, tiles_n;
+  // low-plane modes: max |x| bits of the fp32 operand (read), of this stage's
+  // output (atomicMax, when it feeds the next stage), a slot to zero (or null)
+  const unsigned* sc_in; unsigned* sc_out; unsigned* sc_zero;
 };
 
 // dst[r][c] (planes or fp32, ld ldo) <- src[r][c] (fp32, ld lds), or the

@@ -89,10 +89,28 @@ __device__ __forceinline__ void store_planes(void* hi, void* lo, long long o, fl
     H[o] = h;
     M[o] = m;
     (M + (M - H))[o] = l;
+  } else if (PREC == STORE_F16X2) {
+    const float x = v * (float)(1 << LP_QEXP);
+    const _Float16 h = (_Float16)x;
+    ((uint16_t*)hi)[o] = __builtin_bit_cast(uint16_t, h);
+    ((uint16_t*)lo)[o] = f32_to_f16_bits(x - (float)h);
+  } else if (PREC == STORE_BF16X1) {
+    ((uint16_t*)hi)[o] = f32_to_bf16_bits(v);
+  } else if (PREC == STORE_F16X1) {
+    ((uint16_t*)hi)[o] = f32_to_f16_bits(v * (float)(1 << LP_QEXP));
   } else {
     ((float*)hi)[o] = v;
   }
 }
+
+// scale exponent of an fp32 operand whose max |x| has the bits `mx`: max |x| 2^e
+// lands in [2^13, 2^14) (fp16 max 65504); 0 for an all-zero or non-finite
+// operand (inf / NaN then propagate through the conversions)
+__device__ __forceinline__ int lp_exp(unsigned mx) {
+  const int ex = (int)((mx >> 23) & 0xff);
+  return (mx == 0u || ex == 0xff) ? 0 : 14 - (ex - 127) - 1;
+}
+__device__ __forceinline__ float pow2f(int e) { return __uint_as_float((unsigned)(127 + e) << 23); }
 
 // Tile geometry: BM x BN output tile per workgroup of WM x WN waves (each
 // wave owns a (BM/WM) x (BN/WN) sub-tile of 32x32 MFMA tiles), TK = 32 deep
@@ -120,7 +138,15 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   constexpr bool X3 = (PREC == PREC_BF16X3), X6 = (PREC == PREC_BF16X6);
   constexpr bool X6F = (PREC == PREC_BF16X6F);     // fp32 in memory, planes in LDS
   constexpr bool X6A = (PREC == PREC_BF16X6A), X6B = (PREC == PREC_BF16X6B);
-  constexpr bool X6M = X6A || X6B;                // one operand planes, one fp32
+  // low-plane mixed modes (pgemm.h): LPA / LPB = which operand is the planes one
+  constexpr bool LPA = PREC == PREC_F16X3A || PREC == PREC_H1A || PREC == PREC_F1A;
+  constexpr bool LPB = PREC == PREC_F16X3B || PREC == PREC_H1B || PREC == PREC_F1B;
+  constexpr bool LP = LPA || LPB;
+  constexpr bool LPH = PREC == PREC_F16X3A || PREC == PREC_F16X3B || PREC == PREC_F1A ||
+                       PREC == PREC_F1B;           // fp16 (scaled) vs bf16
+  constexpr int LPN = (PREC == PREC_F16X3A || PREC == PREC_F16X3B) ? 2 : 1;   // planes
+  constexpr bool PA = X6A || LPA, PB = X6B || LPB;  // plane operand in memory
+  constexpr bool X6M = X6A || X6B || LP;          // one operand planes, one fp32
   constexpr bool SPL = X3 || X6;                  // split-bf16 planes in memory
   constexpr bool SWZ = X6F || X6M;                // 64-byte swizzled LDS rows
   constexpr bool IMG16 = SPL || SWZ;              // bf16 plane image in LDS
@@ -136,7 +162,7 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   constexpr int LDB16 = SWZ ? TK : TK + 8;
   constexpr int LDF32 = TK + 4;   // 16-byte aligned chunk writes
   // one LDS array (guide: a second __shared__ object can de-pipeline loads)
-  constexpr int PL = (X6 || SWZ) ? 3 : (X3 ? 2 : 1);   // planes
+  constexpr int PL = LP ? LPN : ((X6 || SWZ) ? 3 : (X3 ? 2 : 1));   // planes
   constexpr int LDS_BYTES = IMG16 ? (PL * (BM + BN) * LDB16 * 2) : ((BM + BN) * LDF32 * 4);
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES * (DBUF ? 2 : 1)];
 
@@ -193,7 +219,7 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   // ---- loader: 16-byte chunks.  bf16 planes: per operand 2 planes x rows x 4
   // chunks (8 elements); f32: rows x 8 chunks (4 elements)
   // per operand: planes in memory (bf16, 8 elements per 16-byte chunk) or fp32
-  constexpr bool APL = SPL || X6A, BPL = SPL || X6B;
+  constexpr bool APL = SPL || PA, BPL = SPL || PB;
   constexpr int CPRA = APL ? TK / 8 : TK / 4, CPRB = BPL ? TK / 8 : TK / 4;   // chunks per row and plane
   constexpr int MPLA = APL ? PL : 1, MPLB = BPL ? PL : 1;                     // planes in memory
   constexpr int ESZA = APL ? 2 : 4, ESZB = BPL ? 2 : 4;
@@ -223,8 +249,8 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   unsigned offa[QA], offb[QB];
   bool oka[QA], okb[QB];
   // X6A / X6B: byte stride between the planes of the plane operand
-  const unsigned pstride_a = X6A ? (unsigned)(Al - Ah) : 0u;
-  const unsigned pstride_b = X6B ? (unsigned)(Bl - Bh) : 0u;
+  const unsigned pstride_a = PA ? (unsigned)(Al - Ah) : 0u;
+  const unsigned pstride_b = PB ? (unsigned)(Bl - Bh) : 0u;
 #pragma unroll
   for (int q = 0; q < QA; ++q) {
     const int c = tid + NT * q;
@@ -232,7 +258,7 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
     chunk_rc(c, BM, CPRA, ESZA, row, kof);
     oka[q] = m0 + row < M;
     offa[q] = ((unsigned)(oka[q] ? m0 + row : m0) * (unsigned)lda + kof) * ESZA;
-    if (X6A) offa[q] += (unsigned)(c / (BM * CPRA)) * pstride_a;
+    if (PA) offa[q] += (unsigned)(c / (BM * CPRA)) * pstride_a;
   }
 #pragma unroll
   for (int q = 0; q < QB; ++q) {
@@ -241,9 +267,12 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
     chunk_rc(c, BN, CPRB, ESZB, row, kof);
     okb[q] = n0 + row < N;
     offb[q] = ((unsigned)(okb[q] ? n0 + row : n0) * (unsigned)ldb + kof) * ESZB;
-    if (X6B) offb[q] += (unsigned)(c / (BN * CPRB)) * pstride_b;
+    if (PB) offb[q] += (unsigned)(c / (BN * CPRB)) * pstride_b;
   }
   const u32x4n z4 = {0u, 0u, 0u, 0u};
+  // low-plane fp16 modes: scale of the fp32 operand (its producer's max slot)
+  const int lp_e = (LP && LPH) ? lp_exp(*(const AS1 unsigned*)P.sc_in) : 0;
+  const float lp_s = pow2f(lp_e);
   // X6F: buffer loads -- the per-thread byte offset stays in one VGPR and the
   // k-step advances the scalar soffset: no 64-bit address rebuilt per load
   // (operands < 4 GiB, checked on the host)
@@ -299,6 +328,30 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
     *(u32x2n*)(dst + plane_stride) = pm;
     *(u32x2n*)(dst + 2 * plane_stride) = pl;
   };
+  // LP: four fp32 values -> LPN fp16 (scaled by lp_s) or one bf16 quad
+  auto store_lp = [&](uint16_t* dst, long long plane_stride, const u32x4n& v) {
+    typedef unsigned u32x2n __attribute__((ext_vector_type(2)));
+    uint16_t h[4], l[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float x = __uint_as_float(v[e]);
+      if (LPH) {
+        const float xs = x * lp_s;
+        const _Float16 hh = (_Float16)xs;
+        h[e] = __builtin_bit_cast(uint16_t, hh);
+        l[e] = f32_to_f16_bits(xs - (float)hh);
+      } else {
+        h[e] = f32_to_bf16_bits(x);
+        l[e] = 0;
+      }
+    }
+    const u32x2n ph = {h[0] | ((unsigned)h[1] << 16), h[2] | ((unsigned)h[3] << 16)};
+    *(u32x2n*)dst = ph;
+    if (LPN == 2) {
+      const u32x2n pl = {l[0] | ((unsigned)l[1] << 16), l[2] | ((unsigned)l[3] << 16)};
+      *(u32x2n*)(dst + plane_stride) = pl;
+    }
+  };
   // rows past the problem are zeroed HERE, not at the load: a select on a
   // loaded value consumes it, so the compiler waited for the next k-step's
   // loads right after issuing them -- before this k-step's MFMAs (the global
@@ -312,7 +365,8 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
       int row, kof;
       chunk_rc(c, BM, CPRA, ESZA, row, kof);
       const u32x4n v = oka[q] ? ra[SET][q] : z4;
-      if (X6A) *(u32x4n*)((uint16_t*)img + (plane * BM + row) * LDB16 + x6f_off(row, kof)) = v;
+      if (PA) *(u32x4n*)((uint16_t*)img + (plane * BM + row) * LDB16 + x6f_off(row, kof)) = v;
+      else if (LP) store_lp((uint16_t*)img + row * LDB16 + x6f_off(row, kof), (long long)BM * LDB16, v);
       else if (SWZ) store_split((uint16_t*)img + row * LDB16 + x6f_off(row, kof), (long long)BM * LDB16, v);
       else if (SPL) *(u32x4n*)((uint16_t*)img + (plane * BM + row) * LDB16 + kof) = v;
       else *(u32x4n*)((float*)img + row * LDF32 + kof) = (row & 16) ? v.zwxy : v;
@@ -324,7 +378,9 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
       int row, kof;
       chunk_rc(c, BN, CPRB, ESZB, row, kof);
       const u32x4n v = okb[q] ? rb[SET][q] : z4;
-      if (X6B) *(u32x4n*)((uint16_t*)img + (PL * BM + plane * BN + row) * LDB16 + x6f_off(row, kof)) = v;
+      if (PB) *(u32x4n*)((uint16_t*)img + (PL * BM + plane * BN + row) * LDB16 + x6f_off(row, kof)) = v;
+      else if (LP) store_lp((uint16_t*)img + (PL * BM + row) * LDB16 + x6f_off(row, kof),
+                            (long long)BN * LDB16, v);
       else if (SWZ) store_split((uint16_t*)img + (PL * BM + row) * LDB16 + x6f_off(row, kof),
                                 (long long)BN * LDB16, v);
       else if (SPL) *(u32x4n*)((uint16_t*)img + (PL * BM + plane * BN + row) * LDB16 + kof) = v;
@@ -370,6 +426,47 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[j], acc[i][j], 0, 0, 0);
           }
         }
+      }
+    } else if constexpr (LP) {
+      typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+      const uint16_t* sA0 = (const uint16_t*)cur;
+      const uint16_t* sB0 = sA0 + PL * BM * LDB16;
+#pragma unroll
+      for (int kk = 0; kk < TK / 16; ++kk) {
+        u16x8 bp[LPN][NJ], ap[LPN][MI];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int row = brow0 + j * 32 + lr;
+          const int off = row * LDB16 + x6f_off(row, kk * 16 + lh * 8);
+#pragma unroll
+          for (int p = 0; p < LPN; ++p) bp[p][j] = *(const u16x8*)(sB0 + p * BN * LDB16 + off);
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int row = arow0 + i * 32 + lr;
+          const int off = row * LDB16 + x6f_off(row, kk * 16 + lh * 8);
+#pragma unroll
+          for (int p = 0; p < LPN; ++p) ap[p][i] = *(const u16x8*)(sA0 + p * BM * LDB16 + off);
+        }
+        // smallest terms first: lo.hi, hi.lo, hi.hi (LPN = 2), term-major
+        constexpr int NTERM = LPN == 2 ? 3 : 1;
+        constexpr int TA[3] = {1, 0, 0}, TBp[3] = {0, 1, 0};
+#pragma unroll
+        for (int t = 0; t < NTERM; ++t)
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+              const int ta = NTERM == 1 ? 0 : TA[t], tb = NTERM == 1 ? 0 : TBp[t];
+              if constexpr (LPH)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(
+                    __builtin_bit_cast(f16x8_t, ap[ta][i]), __builtin_bit_cast(f16x8_t, bp[tb][j]),
+                    acc[i][j], 0, 0, 0);
+              else
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                    __builtin_bit_cast(bf16x8_t, ap[ta][i]), __builtin_bit_cast(bf16x8_t, bp[tb][j]),
+                    acc[i][j], 0, 0, 0);
+            }
       }
     } else if constexpr (X6 || SWZ) {
       const uint16_t* sA0 = (const uint16_t*)cur;
@@ -497,6 +594,9 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   const unsigned ldc = (unsigned)P.ldc, ldd = (unsigned)P.ldd, ldg = (unsigned)P.ldg;
   const float damping = P.damping;
   float kl_part = 0.f;
+  // LP fp16: C = acc 2^-(LP_QEXP + lp_e) (exact: a power of two)
+  const float lp_unscale = (LP && LPH) ? pow2f(-(LP_QEXP + lp_e)) : 1.f;
+  float lp_max = 0.f;                             // max |stored C| (next stage's scale)
   // one straight-line loop nest per epilogue kind (a run-time kind test per
   // element would split the loads into basic blocks with a wait each)
   auto run = [&](auto kind) {
@@ -539,9 +639,11 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
           const int m = m0 + arow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
           if (m >= M || n >= N) continue;
           float v = acc[i][j][r];
+          if constexpr (LP && LPH) v *= lp_unscale;
           const unsigned o = (unsigned)m * ldc + n;
           if constexpr (E == EPI_HADAMARD) v *= aux[r];
           if constexpr (E == EPI_HADAMARD_VEC) v /= (aux2[r] * aux[r] + damping);
+          if constexpr (LP) lp_max = fmaxf(lp_max, fabsf(v));
           if constexpr (E == EPI_FINAL) {
             Cf[o] = v;
             kl_part += v * (aux[r] + aux2[r]);
@@ -574,6 +676,24 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
     case EPI_ATOMIC: run(std::integral_constant<int, EPI_ATOMIC>()); break;
     default: run(std::integral_constant<int, EPI_STORE>()); break;
   }
+  if constexpr (LP) {
+    // the next stage's scale: max |C| of this problem (one atomic per wave;
+    // max is order-independent: deterministic); and the slot this stage frees
+    if (P.sc_out != nullptr) {           // uniform: one atomic per workgroup
+      float m = lp_max;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+      float* lpm = (float*)(smem + 64);    // past the KL partials' slots
+      if (lane == 0) lpm[wave] = m;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        float mm = 0.f;
+        for (int w = 0; w < WM * WN; ++w) mm = fmaxf(mm, lpm[w]);
+        if (mm > 0.f) atomicMax(P.sc_out, __float_as_uint(mm));
+      }
+    }
+    if (P.sc_zero != nullptr && local == 0 && threadIdx.x == 0) *P.sc_zero = 0u;
+  }
   if (kl != nullptr) {
     // one f64 partial per workgroup (waves summed in order, LDS is free after
     // the k-loop's last barrier); kfac_kl_finalize adds the slots in a fixed
@@ -600,6 +720,9 @@ struct GatherJob {
   void* o_hi; void* o_lo; long long ldo;
   int nG, nA, kk, kw, wdtype, bdtype;
   int tile_begin, tiles_g;
+  // low-plane modes: max |Gct| bits (atomicMax) and the 3 slots of the
+  // chain's intermediates, zeroed for this step (either may be null)
+  unsigned* amax; unsigned* zero3;
 };
 
 __device__ __forceinline__ float load_any(const void* p, long long i, int dt) {
@@ -613,7 +736,7 @@ __device__ __forceinline__ float load_any(const void* p, long long i, int dt) {
 // mutable table (with zero_grad(set_to_none=True) every eager step allocates
 // new gradients while the captured graph keeps its own), and no ~4 KB table
 // travels as a by-value kernel argument (corrupted in hipGraph replays).
-constexpr int MAX_GATHER = 36;   // 36 x 104 B: the batch stays under the 4 KB kernel-argument limit
+constexpr int MAX_GATHER = 32;   // 32 x 120 B: the batch stays under the 4 KB kernel-argument limit
 struct GatherBatch {
   int count, pad[3];
   GatherJob job[MAX_GATHER];
@@ -636,6 +759,8 @@ __global__ __launch_bounds__(256) void gather_grad_kernel(const GatherBatch* __r
   const int a0 = ta * 64, g0 = tg * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 64 x 4
   const int wcols = J.nA - (J.bias ? 1 : 0);
+  if (J.zero3 != nullptr && local == 0 && threadIdx.x < 3) J.zero3[threadIdx.x] = 0u;
+  float vmax = 0.f;
   // read: lanes walk a (column), rows g
   for (int r = ty; r < 64; r += 4) {
     const int g = g0 + r, a = a0 + tx;
@@ -650,8 +775,19 @@ __global__ __launch_bounds__(256) void gather_grad_kernel(const GatherBatch* __r
       }
     }
     tile[r][tx] = v;
+    vmax = fmaxf(vmax, fabsf(v));
+  }
+  __shared__ float wmax[4];
+  if (J.amax != nullptr) {     // one atomic per workgroup (all of a layer's hit one word)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, off, 64));
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = vmax;
   }
   __syncthreads();
+  if (J.amax != nullptr && threadIdx.x == 0) {
+    const float m = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+    if (m > 0.f) atomicMax(J.amax, __float_as_uint(m));
+  }
   // write Gct[a][g]: lanes walk g
   for (int r = ty; r < 64; r += 4) {
     const int a = a0 + r, g = g0 + tx;
@@ -768,6 +904,19 @@ KFAC_API int kfac_pgemm(int prec, int tile, const void* dev_table, int count, in
   } else if (prec == PREC_BF16X6B) {
     hipLaunchKernelGGL((pgemm_kernel<PREC_BF16X6B, 128, 128, 2, 2, 2, false, true>), g, dim3(256),
                        0, stream, t, count, kl);
+  } else if (prec >= PREC_F16X3A && prec <= PREC_F1B) {
+#define KFAC_LP(P_)                                                                              \
+  hipLaunchKernelGGL((pgemm_kernel<P_, 128, 128, 2, 2, 2, false, true>), g, dim3(256), 0, stream, \
+                     t, count, kl)
+    switch (prec) {
+      case PREC_F16X3A: KFAC_LP(PREC_F16X3A); break;
+      case PREC_F16X3B: KFAC_LP(PREC_F16X3B); break;
+      case PREC_H1A: KFAC_LP(PREC_H1A); break;
+      case PREC_H1B: KFAC_LP(PREC_H1B); break;
+      case PREC_F1A: KFAC_LP(PREC_F1A); break;
+      default: KFAC_LP(PREC_F1B); break;
+    }
+#undef KFAC_LP
   } else if (prec == PREC_F32) {
     KFAC_PGEMM_LAUNCH(PREC_F32)
   } else {
@@ -813,6 +962,12 @@ KFAC_API int kfac_split_copy(int prec, const void* dev_jobs, int count, int tota
   const SplitJob* j = (const SplitJob*)dev_jobs;
   if (prec == PREC_BF16X3)
     hipLaunchKernelGGL(split_copy_kernel<PREC_BF16X3>, dim3(total_tiles), dim3(256), 0, stream, j, count);
+  else if (prec == STORE_F16X2)
+    hipLaunchKernelGGL(split_copy_kernel<STORE_F16X2>, dim3(total_tiles), dim3(256), 0, stream, j, count);
+  else if (prec == STORE_BF16X1)
+    hipLaunchKernelGGL(split_copy_kernel<STORE_BF16X1>, dim3(total_tiles), dim3(256), 0, stream, j, count);
+  else if (prec == STORE_F16X1)
+    hipLaunchKernelGGL(split_copy_kernel<STORE_F16X1>, dim3(total_tiles), dim3(256), 0, stream, j, count);
   else if (prec == PREC_BF16X6)
     hipLaunchKernelGGL(split_copy_kernel<PREC_BF16X6>, dim3(total_tiles), dim3(256), 0, stream, j, count);
   else

@@ -172,6 +172,8 @@ def _load():
         try:
             lib = ctypes.CDLL(LIB_PATH)
             for name, argt in _SIGS.items():
+                if name in OPTIONAL and not hasattr(lib, name):
+                    continue          # built only with KFAC_BUILD_TWO_STAGE=1
                 fn = getattr(lib, name)
                 fn.argtypes = argt
                 fn.restype = _RESTYPES.get(name, c_int)
@@ -179,6 +181,18 @@ def _load():
         except OSError as e:
             _load_error = str(e)
         return _lib
+
+
+# entry points of the opt-in two-stage solver (csrc/build.py TWO_STAGE_SOURCES)
+OPTIONAL = frozenset(['kfac_sy2sb_batched', 'kfac_sy2sb_ws_floats', 'kfac_sy2sb_nmax',
+                      'kfac_sb2st_batched', 'kfac_sb2st_debug_stamps', 'kfac_sb2st_debug_phases',
+                      'kfac_q2_batched', 'kfac_q2_nmax'])
+
+
+def has(name):
+    """True when the loaded library exports `name` (optional entry points)."""
+    l = _load()
+    return l is not None and hasattr(l, name)
 
 
 def available():

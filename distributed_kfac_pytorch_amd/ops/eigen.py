@@ -357,6 +357,9 @@ def _two_stage_group(mats, clip, stream, use_graph=True, slot=0):
     two-stage solver on `stream`: one batched launch sequence per stage."""
     dev = mats[0].device
     L = _lib.lib()
+    if not _lib.has('kfac_sy2sb_batched'):
+        raise RuntimeError('the two-stage eigensolver is not in this build: rebuild with '
+                           'KFAC_BUILD_TWO_STAGE=1 python csrc/build.py')
     classes = {}
     for i, A in enumerate(mats):
         classes.setdefault(A.shape[0], []).append(i)

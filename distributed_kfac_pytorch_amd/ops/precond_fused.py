@@ -43,8 +43,22 @@ from . import _lib
 
 __all__ = ['FusedPreconditioner', 'PRECISIONS']
 
-PRECISIONS = {'fp32': 0, 'bf16x3': 1, 'bf16x6': 2}
-PLANES = {'fp32': 1, 'bf16x3': 2, 'bf16x6': 3}
+PRECISIONS = {'fp32': 0, 'bf16x3': 1, 'bf16x6': 2, 'fp16x3': 6}
+PLANES = {'fp32': 1, 'bf16x3': 2, 'bf16x6': 3, 'fp16x3': 1}
+# Low-plane mixed modes (csrc/pgemm.h): the eigenvector operands stored once per
+# inverse update as 16-bit planes, the per-step operands fp32 and converted
+# while staged; fp16 operands carry a power-of-two scale (eigenvectors 2^14,
+# the per-step operand from the max |x| its producer recorded).
+#   'fp16x3'  fp16 hi / lo planes, 3 MFMAs per product (22 significand bits)
+#   'bf16x1' / 'fp16x1'  one plane, one MFMA: KFAC(inv_dtype=bfloat16 / float16)
+# name -> (stage prec with the planes as A, as B, split store mode, planes,
+#          plane dtype, scaled)
+LP_CFG = {'fp16x3': (6, 7, 20, 2, torch.float16, True),
+          'bf16x1': (8, 9, 21, 1, torch.bfloat16, False),
+          'fp16x1': (10, 11, 22, 1, torch.float16, True)}
+LP_QSCALE = 2.0 ** 14          # csrc/pgemm.h LP_QEXP
+# the chain precision KFAC(inv_dtype=...) runs on when it is not float32
+INV_DTYPE_PRECISION = {torch.bfloat16: 'bf16x1', torch.float16: 'fp16x1'}
 PREC_BF16X6F = 3   # csrc/pgemm.h: bf16x6 products on fp32 operands, planes split into LDS
 PREC_BF16X6A, PREC_BF16X6B = 4, 5   # one operand (A / B) stored as planes, the other fp32
 # bf16x6 operand storage (same products, same order, bitwise-equal results):
@@ -88,9 +102,11 @@ def _tile_class(M, N, precision):
         # the instantiated configurations: 0 (2 waves / SIMD), 8 (uncapped
         # registers), 9 (two LDS images); X6_BIG (1 = 256 x 256, 6 = 256 x 128,
         # 7 = 128 x 256, fp32-operand mode only) for problems with M, N >= 256
-        if X6_BIG is not None and M >= 256 and N >= 256:
+        if X6_BIG is not None and X6_MODE == 'fp32' and M >= 256 and N >= 256:
             return X6_BIG
         return TILE_CFG if TILE_CFG in (8, 9) else 0
+    if precision in LP_CFG:
+        return 0                 # the one instantiated configuration
     if BIG_TILES and M >= 256 and N >= 256:
         return 1
     return TILE_CFG if TILE_CFG is not None else TILE_CFG_DEFAULT[precision]
@@ -104,7 +120,9 @@ class PGemmRec(ctypes.Structure):
                 ('vm', ctypes.c_void_p), ('vn', ctypes.c_void_p), ('damping', ctypes.c_float),
                 ('g_hi', ctypes.c_void_p), ('g_lo', ctypes.c_void_p), ('ldg', ctypes.c_longlong),
                 ('M', ctypes.c_int), ('N', ctypes.c_int), ('K', ctypes.c_int), ('epi', ctypes.c_int),
-                ('tile_begin', ctypes.c_int), ('tiles_n', ctypes.c_int)]
+                ('tile_begin', ctypes.c_int), ('tiles_n', ctypes.c_int),
+                ('sc_in', ctypes.c_void_p), ('sc_out', ctypes.c_void_p),
+                ('sc_zero', ctypes.c_void_p)]
 
 
 class GatherRec(ctypes.Structure):
@@ -114,7 +132,8 @@ class GatherRec(ctypes.Structure):
                 ('o_hi', ctypes.c_void_p), ('o_lo', ctypes.c_void_p), ('ldo', ctypes.c_longlong),
                 ('nG', ctypes.c_int), ('nA', ctypes.c_int), ('kk', ctypes.c_int), ('kw', ctypes.c_int),
                 ('wdtype', ctypes.c_int), ('bdtype', ctypes.c_int),
-                ('tile_begin', ctypes.c_int), ('tiles_g', ctypes.c_int)]
+                ('tile_begin', ctypes.c_int), ('tiles_g', ctypes.c_int),
+                ('amax', ctypes.c_void_p), ('zero3', ctypes.c_void_p)]
 
 
 class SplitRec(ctypes.Structure):
@@ -156,15 +175,19 @@ def _upload(recs, device):
 
 
 class _Operand(object):
-    """rows x ld operand, k-contiguous, zero-padded along k: fp32, or 2 / 3
-    bf16 planes in ONE allocation (the kernels find plane p at hi + p (lo - hi))."""
-    __slots__ = ('t', 'hi', 'lo', 'ld', 'rows')
+    """rows x ld operand, k-contiguous, zero-padded along k: fp32, or 16-bit
+    planes (bf16 by default; `dtype` fp16 / bf16 for the low-plane modes, any
+    plane count) in ONE allocation (the kernels find plane p at hi + p (lo - hi))."""
+    __slots__ = ('t', 'hi', 'lo', 'ld', 'rows', 'scale')
 
-    def __init__(self, rows, k, planes, device):
+    def __init__(self, rows, k, planes, device, dtype=None):
         self.rows, self.ld = rows, _pad32(k)
-        if planes > 1:
-            self.t = torch.zeros(planes, rows, self.ld, dtype=torch.bfloat16, device=device)
-            self.hi, self.lo = self.t[0].data_ptr(), self.t[1].data_ptr()
+        self.scale = LP_QSCALE if dtype == torch.float16 else 1.0
+        if planes > 1 or dtype is not None:
+            self.t = torch.zeros(planes, rows, self.ld, dtype=dtype or torch.bfloat16,
+                                 device=device)
+            self.hi = self.t[0].data_ptr()
+            self.lo = self.t[1].data_ptr() if planes > 1 else self.hi
         else:
             self.t = torch.zeros(rows, self.ld, dtype=torch.float32, device=device)
             self.hi = self.lo = self.t.data_ptr()
@@ -172,20 +195,24 @@ class _Operand(object):
     def value(self):
         """fp32 view of the stored matrix (tests / debugging)."""
         if self.t.dim() == 3:
-            return self.t.float().sum(0)
+            return self.t.float().sum(0) / self.scale
         return self.t.clone()
 
 
 class _LayerBufs(object):
-    def __init__(self, layer, planes, device, inverse=False, q_planes=None):
+    def __init__(self, layer, planes, device, inverse=False, q_planes=None, q_dtype=None):
         self.layer = layer
         nG, nA = layer.grad_shape
         self.nG, self.nA = nG, nA
         qp = planes if q_planes is None else q_planes     # eigenvector operands
+        # persistent fp32 staging copies of eigendata that is not fp32-
+        # contiguous (inv_dtype 16-bit, packed triangles): the split job table
+        # then keys on fixed addresses (no table per temporary)
+        self.stage = {}
         # inverse path (use_eigen_decomp=False): QGt holds G_inv and QA holds
         # A_inv (both symmetric), V = (G_inv Grad) A_inv in two stages
-        self.QGt = _Operand(nG, nG, qp, device)
-        self.QA = _Operand(nA, nA, qp, device)
+        self.QGt = _Operand(nG, nG, qp, device, q_dtype)
+        self.QA = _Operand(nA, nA, qp, device, q_dtype)
         self.Gct = _Operand(nA, nG, planes, device)
         self.T1 = _Operand(nG, nA, planes, device)
         self.prediv = layer.prediv_eigenvalues and not inverse
@@ -193,23 +220,33 @@ class _LayerBufs(object):
             self.QG = self.QAt = self.T2t = self.T3 = None
             self.Dt = None
             return
-        self.QG = _Operand(nG, nG, qp, device)
-        self.QAt = _Operand(nA, nA, qp, device)
+        self.QG = _Operand(nG, nG, qp, device, q_dtype)
+        self.QAt = _Operand(nA, nA, qp, device, q_dtype)
         self.T2t = _Operand(nA, nG, planes, device)
         self.T3 = _Operand(nG, nA, planes, device)
         self.Dt = torch.zeros(nA, nG, dtype=torch.float32, device=device) if self.prediv else None
 
+    def staged(self, key, t):
+        """`t` as an fp32 contiguous matrix at a fixed address per key."""
+        if t.dtype == torch.float32 and t.is_contiguous():
+            return t
+        buf = self.stage.get(key)
+        if buf is None or buf.shape != t.shape:
+            buf = self.stage[key] = torch.empty(t.shape, dtype=torch.float32, device=t.device)
+        buf.copy_(t)
+        return buf
+
 
 class FusedPreconditioner(object):
     def __init__(self, layers, precision='bf16x3'):
-        if precision not in PRECISIONS:
+        if precision not in PRECISIONS and precision not in LP_CFG:
             raise ValueError('precision must be one of {}'.format(sorted(PRECISIONS)))
         _check_layouts()
         self.layers = list(layers)
         self.precision = precision
-        self.prec = PRECISIONS[precision]
+        self.prec = PRECISIONS.get(precision, 0)
         self.x3 = precision == 'bf16x3'
-        self.planes = PLANES[precision]
+        self.planes = PLANES.get(precision, 1)
         # precision of the stored operands: the gathered gradient (gather
         # launch) and the eigenvector operands (split launch)
         self.store_prec = self.q_store_prec = self.prec
@@ -217,7 +254,13 @@ class FusedPreconditioner(object):
         # kernel precision per stage: S1-S3 multiply an eigenvector operand
         # as A, S4 (and the inverse path's second stage) as B
         self.stage_prec = None
-        if precision == 'bf16x6' and X6_MODE != 'planes':
+        self.lp = LP_CFG.get(precision)
+        q_dtype = None
+        if self.lp is not None:
+            pa, pb, qstore, q_planes, q_dtype, _ = self.lp
+            self.prec, self.store_prec, self.planes, self.q_store_prec = pa, 0, 1, qstore
+            self.stage_prec = (pa, pa, pa, pb)
+        elif precision == 'bf16x6' and X6_MODE != 'planes':
             self.prec, self.store_prec, self.planes = PREC_BF16X6F, 0, 1
             self.q_store_prec = 0
             if X6_MODE == 'mixed':
@@ -228,9 +271,14 @@ class FusedPreconditioner(object):
         # the damped-inverse path (K9): V = G_inv Grad A_inv, two grouped stages
         self.inverse = bool(self.layers) and not self.layers[0].use_eigen_decomp
         if self.inverse and self.stage_prec is not None:
-            self.stage_prec = (PREC_BF16X6A, PREC_BF16X6B)
-        self.bufs = [_LayerBufs(l, self.planes, self.device, self.inverse, q_planes)
+            self.stage_prec = (self.stage_prec[0], self.stage_prec[3])
+        self.bufs = [_LayerBufs(l, self.planes, self.device, self.inverse, q_planes, q_dtype)
                      for l in self.layers]
+        # low-plane fp16 modes: per layer the max |x| bits of Gct, T1, T2t, T3
+        # (filled by their producers, read by their consumers; see run())
+        self.slots = None
+        if self.lp is not None and self.lp[5] and self.layers:
+            self.slots = torch.zeros(len(self.bufs), 4, dtype=torch.int32, device=self.device)
         for b in self.bufs:
             _lib.check_pgemm_extent(max(b.nG, b.nA), 'layer')
         self._gather_sig = None
@@ -264,7 +312,10 @@ class FusedPreconditioner(object):
                         r.epi, r.dmat, r.ldd = EPI_HADAMARD, b.Dt.data_ptr(), b.nG
                     else:
                         r.epi = EPI_HADAMARD_VEC
-                        r.vm, r.vn = st['dA'].data_ptr(), st['dG'].data_ptr()
+                        # fp32 eigenvalues (16-bit inv_dtype: fixed-address copies,
+                        # refreshed by refresh_eigen)
+                        r.vm = b.staged('dA', st['dA']).data_ptr()
+                        r.vn = b.staged('dG', st['dG']).data_ptr()
                         r.damping = self.damping
                 elif stage == 2:    # T3[g][a] = QG . T2t
                     A, B, C, M, N, K = b.QG, b.T2t, b.T3, b.nG, b.nA, b.nG
@@ -281,6 +332,18 @@ class FusedPreconditioner(object):
                 else:
                     r.c_hi, r.c_lo, r.ldc = C.hi, C.lo, C.ld
                 r.M, r.N, r.K = M, N, K
+                if self.slots is not None:
+                    # slot chain: gather -> Gct (0) -> S1 -> T1 (1) -> S2 -> T2t
+                    # (2) -> S3 -> T3 (3) -> S4, which frees slot 0 for the next
+                    # step (the gather zeroes 1..3); inverse path: Gct (0) -> T1 (1)
+                    bi = self.bufs.index(b)
+                    base = self.slots.data_ptr() + 16 * bi
+                    src = {0: 0, 1: 1, 2: 2, 3: 1 if self.inverse else 3}[stage]
+                    r.sc_in = base + 4 * src
+                    if C is not None:
+                        r.sc_out = base + 4 * (stage + 1)
+                    else:
+                        r.sc_zero = base
                 probs.append(r)
             launches = []
             classes = sorted({_tile_class(r.M, r.N, self.precision) for r in probs})
@@ -337,21 +400,21 @@ class FusedPreconditioner(object):
                     from ..layers import utils as lutils
                     Ai = lutils.fill_triu((b.nA, b.nA), Ai)
                     Gi = lutils.fill_triu((b.nG, b.nG), Gi)
-                Ai, Gi = Ai.float().contiguous(), Gi.float().contiguous()
-                keep += [Ai, Gi]
+                Ai, Gi = b.staged('A', Ai), b.staged('G', Gi)
                 add(jobs, Gi, b.QGt, False)
                 add(jobs, Ai, b.QA, False)
                 continue
-            QA = st['QA'].float().contiguous()
-            QG = st['QG'].float().contiguous()
-            keep += [QA, QG]
+            QA = b.staged('A', st['QA'])
+            QG = b.staged('G', st['QG'])
             add(jobs, QG, b.QG, False)
             add(jobs, QG, b.QGt, True)
             add(jobs, QA, b.QA, False)
             add(jobs, QA, b.QAt, True)
+            if not b.prediv:
+                b.staged('dA', st['dA'])
+                b.staged('dG', st['dG'])
             if b.prediv:
-                D = st['dGdA'].float().contiguous()
-                keep.append(D)
+                D = b.staged('D', st['dGdA'])
                 add(fjobs, D, _F32Dst(b.Dt), True)
         stream = _lib.stream(self.device)
         L = _lib.lib()
@@ -417,6 +480,9 @@ class FusedPreconditioner(object):
                 r.bias, r.bdtype = bias.data_ptr(), _lib.DTYPE_CODE[bias.dtype]
             r.o_hi, r.o_lo, r.ldo = b.Gct.hi, b.Gct.lo, b.Gct.ld
             r.nG, r.nA = b.nG, b.nA
+            if self.slots is not None:
+                base = self.slots.data_ptr() + 16 * self.bufs.index(b)
+                r.amax, r.zero3 = base, base + 4
         self._gather = recs
         self._gather_sig = sig
         return recs

@@ -1123,10 +1123,18 @@ class KFAC(optim.Optimizer):
         mats = [l.state[w].to(torch.float32) for l, w in jobs]
         if defer_check and self.use_eigen_decomp and mats[0].is_cuda:
             # no host read before the solve: flagged factors are solved as the
-            # identity and the flags are checked at the end of step()
+            # identity and the flags are checked at the end of step().  The
+            # raise then comes AFTER this step's state changes (the identity
+            # eigendata of a flagged factor is stored, broadcast and applied).
+            # Every rank checks EVERY layer's factors (they are replicated by
+            # the factor all-reduce), not only the ones it solved, so all
+            # ranks raise at the same step -- none trains on from a
+            # broadcast identity -- with no extra collective.
             finite = _factors_finite(mats)
             results = self._solve_inverses(jobs, mats, damping, finite)
-            self._deferred_checks.append((jobs, finite))
+            every = [(l, w) for l in self.layers for w in ('A', 'G')]
+            self._deferred_checks.append(
+                (every, _factors_finite([l.state[w] for l, w in every])))
         else:
             _check_factors_finite(jobs, mats)
             results = self._solve_inverses(jobs, mats, damping)
@@ -1286,7 +1294,13 @@ class KFAC(optim.Optimizer):
         every layer this rank preconditions, on the GPU: 4 grouped stages on
         the eigen path, 2 (G_inv Grad A_inv) on the damped-inverse path."""
         self.fused = None
-        if not (self.fused_precondition and self.layers and self.inv_dtype == torch.float32):
+        if self.inv_dtype == torch.float32:
+            precision = self.precond_precision
+        else:
+            # the reference's 16-bit inv_dtype (kfac/layers/base.py:435-441,
+            # 463, 470): 16-bit eigenvector operands, one MFMA per product
+            precision = precond_fused.INV_DTYPE_PRECISION.get(self.inv_dtype)
+        if not (self.fused_precondition and self.layers and precision is not None):
             return
         if not self.layers[0].module.weight.is_cuda:
             return
@@ -1295,9 +1309,9 @@ class KFAC(optim.Optimizer):
         if mine:
             split = self._overlap_split(mine)
             if split:
-                self.fused = precond_fused.SplitFused(mine, self.precond_precision, split)
+                self.fused = precond_fused.SplitFused(mine, precision, split)
             else:
-                self.fused = precond_fused.FusedPreconditioner(mine, self.precond_precision)
+                self.fused = precond_fused.FusedPreconditioner(mine, precision)
             self._fused_all = len(mine) == len(self.layers)
         self._register_top_hooks()
 

@@ -7,9 +7,13 @@ kfac/layers/utils.py:45-74 (ascending eigenvalues, eigenvectors in columns)."""
 import pytest
 import torch
 
-from distributed_kfac_pytorch_amd.ops import eigen
+from distributed_kfac_pytorch_amd.ops import _lib, eigen
 
-pytestmark = pytest.mark.gpu
+# built only with KFAC_BUILD_TWO_STAGE=1 (csrc/build.py): it loses to the
+# one-stage path on every routing measured
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not _lib.has('kfac_sy2sb_batched'),
+                                 reason='two-stage solver not built (KFAC_BUILD_TWO_STAGE=1)')]
 DEV = 'cuda'
 
 

@@ -68,7 +68,8 @@ def _phase(msg):
             os.fsync(f.fileno())
 
 
-def _grads(fused, precision='fp32', channels_last=False, prediv=True, steps=3, eigen=True):
+def _grads(fused, precision='fp32', channels_last=False, prediv=True, steps=3, eigen=True,
+           inv_dtype=torch.float32):
     torch.manual_seed(0)
     m = WideNet().cuda()
     if channels_last:
@@ -76,7 +77,7 @@ def _grads(fused, precision='fp32', channels_last=False, prediv=True, steps=3, e
     pre = kfac.KFAC(m, factor_update_freq=1, inv_update_freq=2, lr=0.05, damping=0.003,
                     fused_precondition=fused, precond_precision=precision,
                     precompute_outer_eigen=prediv, use_hip_graphs=False,
-                    use_eigen_decomp=eigen)
+                    use_eigen_decomp=eigen, inv_dtype=inv_dtype)
     opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9)
     if _TRACE:
         for name, mod in m.named_children():
@@ -102,7 +103,8 @@ def _grads(fused, precision='fp32', channels_last=False, prediv=True, steps=3, e
     return out, pre
 
 
-@pytest.mark.parametrize('precision,tol', [('fp32', 2e-6), ('bf16x6', 2e-6), ('bf16x3', 5e-5)])
+@pytest.mark.parametrize('precision,tol', [('fp32', 2e-6), ('bf16x6', 2e-6), ('bf16x3', 5e-5),
+                                           ('fp16x3', 2e-6)])
 @pytest.mark.parametrize('channels_last', [False, True])
 @pytest.mark.parametrize('prediv', [True, False])
 def test_fused_matches_per_layer(precision, tol, channels_last, prediv):
@@ -114,6 +116,36 @@ def test_fused_matches_per_layer(precision, tol, channels_last, prediv):
             err = ((a - b).norm() / b.norm().clamp_min(1e-20)).item()
             # a few steps compound through SGD momentum; still far below bf16 (4e-3)
             assert err < tol * (10 ** step), (step, err)
+
+
+@pytest.mark.parametrize('precision', ['fp16x3', 'bf16x6'])
+def test_fused_inverse_path_matches_per_layer(precision):
+    """use_eigen_decomp=False (V = G_inv Grad A_inv, two grouped stages)."""
+    ref, _ = _grads(False, eigen=False)
+    got, pre = _grads(True, precision, eigen=False)
+    assert pre.fused is not None
+    for step, (gs, rs) in enumerate(zip(got, ref)):
+        for a, b in zip(gs, rs):
+            err = ((a - b).norm() / b.norm().clamp_min(1e-20)).item()
+            assert err < 2e-6 * (10 ** step), (step, err)
+
+
+@pytest.mark.parametrize('inv_dtype', [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize('prediv', [True, False])
+def test_fused_chain_inv_dtype_matches_per_layer(inv_dtype, prediv):
+    """The reference's 16-bit inv_dtype (16-bit eigendata, 16-bit products)
+    on the grouped chain (one bf16 / fp16 MFMA per product) against the
+    per-layer torch.matmul path on the same 16-bit eigendata."""
+    from distributed_kfac_pytorch_amd.ops import precond_fused
+    ref, _ = _grads(False, prediv=prediv, inv_dtype=inv_dtype)
+    got, pre = _grads(True, prediv=prediv, inv_dtype=inv_dtype)
+    assert isinstance(pre.fused, precond_fused.FusedPreconditioner)
+    assert pre.fused.lp is not None        # the 16-bit MFMA mode, not the fp32 chain
+    for step, (gs, rs) in enumerate(zip(got, ref)):
+        for a, b in zip(gs, rs):
+            err = ((a - b).norm() / b.norm().clamp_min(1e-20)).item()
+            # both sides round every product operand to 16 bits (bf16: 2^-9)
+            assert err < 2e-2 * (3 ** step), (step, err)
 
 
 def test_fused_kl_matches_reference_dot():
