@@ -74,12 +74,13 @@ def parse():
     ap.add_argument('--profile-phases', action='store_true')
     ap.add_argument('--check-finite', action='store_true',
                     help='debug: sync and print the loss of every timed step')
-    ap.add_argument('--precond-precision', default='bf16x6', choices=['fp32', 'bf16x3', 'bf16x6'],
-                    help='fused preconditioning GEMM precision: bf16x6 (the default: three bf16 '
-                         'planes = the fp32 significand, six MFMAs per product, fp32 '
-                         'accumulation; error at or below fp32 GEMMs on every ResNet-50 layer, '
-                         'tests/test_gpu_resnet50_parity.py), fp32 (exact-f32 MFMA) or bf16x3 '
-                         '(split-bf16 MFMA, ~1e-5 relative error, opt-in)')
+    ap.add_argument('--precond-precision', default='fp16x3',
+                    choices=['fp32', 'bf16x3', 'bf16x6', 'fp16x3'],
+                    help='fused preconditioning GEMM precision: fp16x3 (the default: scaled '
+                         'fp16 hi/lo planes, 22 significand bits, three MFMAs per product, fp32 '
+                         'accumulation; error below torch fp32 GEMMs on every ResNet-50 layer, '
+                         'tests/test_gpu_resnet50_parity.py), bf16x6 (three bf16 planes, six '
+                         'MFMAs), fp32 (exact-f32 MFMA) or bf16x3 (~1e-5 relative error)')
     ap.add_argument('--sgd-delta', type=int, default=1,
                     help='also time the same steps without K-FAC (hooks removed) and report '
                          'the per-step K-FAC cost (kfac_step_ms)')

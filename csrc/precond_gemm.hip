@@ -905,9 +905,20 @@ KFAC_API int kfac_pgemm(int prec, int tile, const void* dev_table, int count, in
     hipLaunchKernelGGL((pgemm_kernel<PREC_BF16X6B, 128, 128, 2, 2, 2, false, true>), g, dim3(256),
                        0, stream, t, count, kl);
   } else if (prec >= PREC_F16X3A && prec <= PREC_F1B) {
+    // tile 6 / 7: 256 x 128 / 128 x 256 with 8 waves (fewer operand bytes per
+    // product for problems with a dimension >= 256), else 128 x 128
 #define KFAC_LP(P_)                                                                              \
-  hipLaunchKernelGGL((pgemm_kernel<P_, 128, 128, 2, 2, 2, false, true>), g, dim3(256), 0, stream, \
-                     t, count, kl)
+  do {                                                                                           \
+    if (tile == 6)                                                                               \
+      hipLaunchKernelGGL((pgemm_kernel<P_, 256, 128, 4, 2, 2, false, true>), g, dim3(512), 0,     \
+                         stream, t, count, kl);                                                  \
+    else if (tile == 7)                                                                          \
+      hipLaunchKernelGGL((pgemm_kernel<P_, 128, 256, 2, 4, 2, false, true>), g, dim3(512), 0,     \
+                         stream, t, count, kl);                                                  \
+    else                                                                                         \
+      hipLaunchKernelGGL((pgemm_kernel<P_, 128, 128, 2, 2, 2, false, true>), g, dim3(256), 0,     \
+                         stream, t, count, kl);                                                  \
+  } while (0)
     switch (prec) {
       case PREC_F16X3A: KFAC_LP(PREC_F16X3A); break;
       case PREC_F16X3B: KFAC_LP(PREC_F16X3B); break;

@@ -72,6 +72,7 @@ X6_MODE = os.environ.get('KFAC_X6_MODE') or \
     ('planes' if os.environ.get('KFAC_X6_PLANES') == '1' else 'mixed')
 X6_PLANES = X6_MODE == 'planes'
 X6_BIG = int(os.environ['KFAC_X6_BIG']) if os.environ.get('KFAC_X6_BIG') else None
+LP_BIG = int(os.environ['KFAC_LP_BIG']) if os.environ.get('KFAC_LP_BIG') else None
 EPI_STORE, EPI_HADAMARD, EPI_HADAMARD_VEC, EPI_FINAL = 0, 1, 2, 3
 TILE = 128        # small tile class (csrc/precond_gemm.hip)
 BIG_TILE = 256    # big tile class: half the operand traffic per FLOP
@@ -106,7 +107,13 @@ def _tile_class(M, N, precision):
             return X6_BIG
         return TILE_CFG if TILE_CFG in (8, 9) else 0
     if precision in LP_CFG:
-        return 0                 # the one instantiated configuration
+        # KFAC_LP_BIG=6 / 7: 256 x 128 / 128 x 256 tiles for problems with
+        # M resp. N >= 256 (experiments; 128 x 128 otherwise)
+        if LP_BIG == 6 and M >= 256:
+            return 6
+        if LP_BIG == 7 and N >= 256:
+            return 7
+        return 0
     if BIG_TILES and M >= 256 and N >= 256:
         return 1
     return TILE_CFG if TILE_CFG is not None else TILE_CFG_DEFAULT[precision]

@@ -8,7 +8,7 @@ by scripts/make_training_fixture.py) against:
      eager): the first steps before the trajectories decorrelate, the first
      step's preconditioned gradients, and every 25-step window of the loss;
 (ii) the bench configuration (bf16 autocast numerics through bf16-stored
-     weights with fp32 masters, bf16x6 preconditioning, the whole step as
+     weights with fp32 masters, fp16x3 preconditioning, the whole step as
      replayed hipGraphs, early A factors): every 25-step window within a band
      of run (i) -- a stale eigenbasis under graphs or a wrong EMA order shows
      up here, not in the one-step parity tests.
@@ -64,7 +64,7 @@ def _bench_config_run():
     net = T.model().to(dev).to(memory_format=torch.channels_last)
     weights = mixed.BF16Weights(net)
     opt = torch.optim.SGD(weights.parameters(net), fused=True, **T.SGD_KW)
-    pre = kfac.KFAC(net, precond_precision='bf16x6', early_factors=True, **T.KFAC_KW)
+    pre = kfac.KFAC(net, precond_precision='fp16x3', early_factors=True, **T.KFAC_KW)
     pre.set_grad_params(weights.grad_params())
     x = torch.zeros(T.BATCH, 3, 32, 32, device=dev).to(memory_format=torch.channels_last)
     y = torch.zeros(T.BATCH, dtype=torch.long, device=dev)
