@@ -149,8 +149,10 @@ def measured_cost(n):
 # 'measured' table summed to 1,432 ms for ResNet-50's 108 factors against
 # 157 ms measured batched).  T(S) = a n_max + b3 sum n^3 + b2 sum n^2 + b0 |S|,
 # least-squares fit to one-GPU solves of per-rank sets
-# (scripts/probes/probe_inverse_share.py, profiles/r3_inverse_share.log).
-BATCHED_COST_MS = (1.023e-2, 7.213e-11, 2.027e-7, 8.069e-2)
+# (scripts/probes/probe_inverse_share.py; refit in round 6 on the solver with
+# single-launch tail columns: mean error 2.7 %, max 11.7 %, where the round-3
+# table was off by 15.1 % mean; profiles/r6_inverse_share.log).
+BATCHED_COST_MS = (8.814e-3, 4.811e-11, 2.840e-7, -8.399e-3)
 
 
 def batched_cost(sizes):
