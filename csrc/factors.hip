@@ -27,6 +27,8 @@
 
 #include <cstdlib>
 #include "devtable.h"
+#include <algorithm>
+#include <vector>
 #include <type_traits>
 
 namespace {
@@ -111,7 +113,10 @@ __device__ __forceinline__ void decompose_row(const PatchArgs& p, long long row,
 // stored whole into its slot of p.part (plain stores: tile_reduce adds the
 // splits in a fixed order), or, with no partial buffer, f32 atomics into the
 // upper triangle of ws.
-__device__ __forceinline__ void store_tile(const PatchArgs& p, const f32x16_t (&acc)[2][2],
+// TW = tile width (128, or 256 for the wide grouped tiles); a wave owns MI x
+// NJ 32x32 blocks at rows wr * 32 MI, columns wc * 32 NJ of the tile.
+template <int TW = BT, int MI = 2, int NJ = 2>
+__device__ __forceinline__ void store_tile(const PatchArgs& p, const f32x16_t (&acc)[MI][NJ],
                                            int tile, int split, int ti, int tj, bool diag, int wr,
                                            int wc, int lr, int lh) {
   const float ds = p.dscale != nullptr ? *p.dscale : 1.f;
@@ -119,27 +124,27 @@ __device__ __forceinline__ void store_tile(const PatchArgs& p, const f32x16_t (&
   const bool drop = (ds == 0.f);
   if (p.part != nullptr) {
     const int tp = p.ntiles * (p.ntiles + 1) / 2;
-    float* dst = p.part + ((long long)split * tp + tile) * (BT * BT);
+    float* dst = p.part + ((long long)split * tp + tile) * (TW * TW);
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int m = 0; m < MI; ++m)
 #pragma unroll
-      for (int n = 0; n < 2; ++n)
+      for (int n = 0; n < NJ; ++n)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int lrow = wr * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          const int lcol = wc * 64 + n * 32 + lr;
-          dst[lrow * BT + lcol] = drop ? 0.f : sc * acc[m][n][r];
+          const int lrow = wr * 32 * MI + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          const int lcol = wc * 32 * NJ + n * 32 + lr;
+          dst[lrow * TW + lcol] = drop ? 0.f : sc * acc[m][n][r];
         }
     return;
   }
 #pragma unroll
-  for (int m = 0; m < 2; ++m)
+  for (int m = 0; m < MI; ++m)
 #pragma unroll
-    for (int n = 0; n < 2; ++n)
+    for (int n = 0; n < NJ; ++n)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        int row = ti * BT + wr * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        int col = tj * BT + wc * 64 + n * 32 + lr;
+        int row = ti * TW + wr * 32 * MI + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        int col = tj * TW + wc * 32 * NJ + n * 32 + lr;
         if (!drop && row < p.ncols && col < p.ncols && (!diag || row <= col))
           atomicAdd(p.ws + (long long)row * p.ldw + col, sc * acc[m][n][r]);
       }
@@ -157,6 +162,7 @@ struct RedJob {
   const float* part[MAX_CONTRIB];
   int splits[MAX_CONTRIB];
   int block_begin, accum;
+  int bt, pad;            // tile width of the partials (128 or 256)
 };
 constexpr int MAX_RED_JOBS = 24;
 struct RedBatch {
@@ -166,7 +172,7 @@ struct RedBatch {
 static_assert(sizeof(RedBatch) <= 4096, "kernel arguments are limited to 4 KB");
 
 // Each workgroup takes 1024 elements (a float4 per thread) of one tile pair:
-// RED_WG = 16 workgroups per tile pair.  The split loop loads 8 partials at
+// RED_WG = 16 workgroups per 128-wide tile pair (64 per 256-wide one).  The split loop loads 8 partials at
 // a time (independent, in flight together) and adds them in order: the
 // summation order (contribution, split) is fixed, so the result is
 // deterministic.
@@ -181,17 +187,18 @@ __global__ __launch_bounds__(256) void tile_reduce_kernel(const RedBatch* __rest
     if (t[mid].block_begin <= b) lo = mid; else hi = mid - 1;
   }
   const RedJob& J = t[lo];
+  const int bt = J.bt, bt2 = bt * bt, rwg = bt2 / 1024;
   const int loc = b - J.block_begin;
-  const int tile = loc / RED_WG, part = loc - tile * RED_WG;
+  const int tile = loc / rwg, part = loc - tile * rwg;
   int tt = tile, ti = 0, rem = J.ntiles;
   while (tt >= rem) { tt -= rem; ++ti; --rem; }
   const int tj = ti + tt;
   const int tp = J.ntiles * (J.ntiles + 1) / 2;
   const int e = part * 1024 + threadIdx.x * 4;          // 4 consecutive elements of a row
-  const long long sstride = (long long)tp * (BT * BT) / 4;   // float4 stride between splits
+  const long long sstride = (long long)tp * bt2 / 4;    // float4 stride between splits
   fx4 acc = {0.f, 0.f, 0.f, 0.f};
   for (int c = 0; c < J.ncontrib; ++c) {
-    const AS1 fx4* pc = (const AS1 fx4*)(gptr(J.part[c]) + (long long)tile * (BT * BT) + e);
+    const AS1 fx4* pc = (const AS1 fx4*)(gptr(J.part[c]) + (long long)tile * bt2 + e);
     const int ns = J.splits[c];
     int sp = 0;
     for (; sp + 8 <= ns; sp += 8) {
@@ -203,7 +210,7 @@ __global__ __launch_bounds__(256) void tile_reduce_kernel(const RedBatch* __rest
     }
     for (; sp < ns; ++sp) acc += pc[(long long)sp * sstride];
   }
-  const int row = ti * BT + e / BT, col0 = tj * BT + (e & (BT - 1));
+  const int row = ti * bt + e / bt, col0 = tj * bt + (e & (bt - 1));
   AS1 float* w = gptr(J.ws) + (long long)row * J.ldw + col0;
   const bool add = J.accum != 0;
 #pragma unroll
@@ -382,9 +389,9 @@ __global__ __launch_bounds__(256) void syrk_patch_kernel(PatchArgs p) {
 constexpr int VBK = 64;                 // patch rows per k-step (default configuration)
 // LDS of one syrk_vec workgroup: two [BT][VB + 8] operand images and the
 // double-buffered row table (VB 16-byte entries per slot)
-template <int VB> struct SyrkVecLds {
+template <int VB, int TW = BT> struct SyrkVecLds {
   static_assert(VB == 64, "the row decode is one wave: VB rows per k-step");
-  static constexpr int ELEMS = 2 * BT * (VB + 8) + 2 * VB * 8;
+  static constexpr int ELEMS = 2 * TW * (VB + 8) + 2 * VB * 8;
 };
 // 16-byte gather constants: zeros, and the ones column's first chunk [1, 0 x 7]
 // as bf16 and as f16
@@ -413,13 +420,19 @@ __device__ __forceinline__ uint32_t u4get(const u32x4_t& v, int i) { return v[i]
 // with ds_read_b64_tr_b16, no staging registers) measured 3.46 ms with two
 // stages (2 workgroups / CU) and 4.70 ms with three (1 / CU; hipcc still waits
 // vmcnt(0) before some ring reads): not kept (profiles/r3_factors_dma*.log).
-template <int DT, int VB = VBK>
+// TW: output tile width.  128 (4 waves, 2 x 2 of 64 x 64) or 256 (8 waves,
+// 2 x 4 of 128 x 64): a 256-wide tile streams its two column panels for four
+// times the products of a 128-wide one -- half the operand bytes per product
+// for the wide factors, whose panel gather is what the kernel waits on.
+template <int DT, int VB = VBK, int TW = BT>
 __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int split,
                                               uint16_t* smem) {
   constexpr int VLD = VB + 8;
   constexpr int RG = VB / 64;           // 64-row groups per k-step and loader thread
+  constexpr int WN = TW / 64;           // wave columns: 2 (TW 128) or 4 (TW 256)
+  constexpr int MI = TW / 64, NJ = 2;   // 32x32 blocks per wave: rows x columns
   uint16_t* sA = smem;
-  uint16_t* sB = smem + BT * VLD;
+  uint16_t* sB = smem + TW * VLD;
 
   int t = tile, ti = 0, rem = p.ntiles;
   while (t >= rem) { t -= rem; ++ti; --rem; }
@@ -444,11 +457,11 @@ __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int 
   // fastest put them 8 LDS rows apart = 288 dwords = the same 4 banks: 8-way
   // conflicts, 72 % of the kernel's LDS cycles, profiles/README.md.)  A wave's
   // global loads still read 128 contiguous bytes per patch row.
-  const int op = tid >> 7;
+  const int op = tid / TW;
   const int rg = tid & 7;               // rows rg*8 .. rg*8+7 of each 64-row group
-  const int cc = (tid & 127) >> 3;      // columns cc*8 .. cc*8+7 of the tile
+  const int cc = (tid % TW) >> 3;       // columns cc*8 .. cc*8+7 of the tile
   const bool loader = !(diag && op == 1);
-  const int gcol = (op ? tj : ti) * BT + cc * 8;
+  const int gcol = (op ? tj : ti) * TW + cc * 8;
   // chunk kind: 0 = data, 1 = bias (first column of the chunk is the ones column), 2 = zero
   int kind = 2, coff = 0, di = 0, dj = 0;
   if (gcol < p.kcols) {
@@ -471,7 +484,7 @@ __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int 
   // Padding / bias / zero / past-the-split elements load from a 16-B constant
   // (zeros, or the ones column's [1, 0, ...]) instead of being masked: no
   // select on the loaded data, one pointer select per row.
-  int4* rtab = (int4*)(smem + 2 * BT * VLD);            // [2][VB] entries
+  int4* rtab = (int4*)(smem + 2 * TW * VLD);            // [2][VB] entries
   constexpr int ROW_NONE = -(1 << 30);                  // hs of a row past the split
   const AS1 u32x4_t* zeros = gptr((const u32x4_t*)g_syrk_const[0]);
   const AS1 u32x4_t* alt = (kind == 1) ? gptr((const u32x4_t*)g_syrk_const[DT == KDT_BF16 ? 1 : 2])
@@ -558,13 +571,13 @@ __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int 
     }
   };
 
-  const int wr = wave >> 1, wc = wave & 1;
+  const int wr = wave / WN, wc = wave % WN;
   const int lr = lane & 31, lh = lane >> 5;
-  f32x16_t acc[2][2];
+  f32x16_t acc[MI][NJ];
 #pragma unroll
-  for (int m = 0; m < 2; ++m)
+  for (int m = 0; m < MI; ++m)
 #pragma unroll
-    for (int n = 0; n < 2; ++n)
+    for (int n = 0; n < NJ; ++n)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
   const uint16_t* sBr = diag ? sA : sB;
@@ -573,17 +586,17 @@ __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int 
     typedef typename std::conditional<DT == KDT_BF16, bf16x8_t, f16x8_t>::type frag_t;
 #pragma unroll
     for (int ks = 0; ks < VB / 16; ++ks) {
-      frag_t a[2], bb[2];
+      frag_t a[MI], bb[NJ];
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
-        a[m] = *(const frag_t*)(sA + (wr * 64 + m * 32 + lr) * VLD + ks * 16 + lh * 8);
+      for (int m = 0; m < MI; ++m)
+        a[m] = *(const frag_t*)(sA + (wr * 32 * MI + m * 32 + lr) * VLD + ks * 16 + lh * 8);
 #pragma unroll
-      for (int n = 0; n < 2; ++n)
-        bb[n] = *(const frag_t*)(sBr + (wc * 64 + n * 32 + lr) * VLD + ks * 16 + lh * 8);
+      for (int n = 0; n < NJ; ++n)
+        bb[n] = *(const frag_t*)(sBr + (wc * 32 * NJ + n * 32 + lr) * VLD + ks * 16 + lh * 8);
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
+      for (int m = 0; m < MI; ++m)
 #pragma unroll
-        for (int n = 0; n < 2; ++n) {
+        for (int n = 0; n < NJ; ++n) {
           if constexpr (DT == KDT_BF16)
             acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[m], bb[n], acc[m][n], 0, 0, 0);
           else
@@ -604,7 +617,7 @@ __device__ __forceinline__ void syrk_vec_tile(const PatchArgs& p, int tile, int 
     __syncthreads();
   }
 
-  store_tile(p, acc, tile, split, ti, tj, diag, wr, wc, lr, lh);
+  store_tile<TW, MI, NJ>(p, acc, tile, split, ti, tj, diag, wr, wc, lr, lh);
 }
 
 template <int DT>
@@ -619,7 +632,7 @@ __global__ __launch_bounds__(256) void syrk_vec_kernel(PatchArgs p) {
 // under-filled launches of their own.
 struct SyrkProblem {
   PatchArgs p;
-  int block_begin, blocks, dtype, pad;
+  int block_begin, blocks, dtype, tw;   // tw: tile width (128 / 256)
 };
 
 // Tables travel BY VALUE in the kernel arguments (< 4 KB), so a launch is
@@ -631,9 +644,9 @@ struct SyrkBatch {
 };
 static_assert(sizeof(SyrkBatch) <= 4096, "kernel arguments are limited to 4 KB");
 
-template <int DT, int VB = VBK>
-__global__ __launch_bounds__(256) void syrk_vec_grouped_kernel(const SyrkBatch* __restrict__ batch) {
-  __shared__ __attribute__((aligned(16))) uint16_t smem[SyrkVecLds<VB>::ELEMS];
+template <int DT, int TW = BT, int VB = VBK>
+__global__ __launch_bounds__(2 * TW) void syrk_vec_grouped_kernel(const SyrkBatch* __restrict__ batch) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[SyrkVecLds<VB, TW>::ELEMS];
   const SyrkProblem* t = batch->prob;
   const int count = batch->count;
   int lo = 0, hi = count - 1;
@@ -647,7 +660,7 @@ __global__ __launch_bounds__(256) void syrk_vec_grouped_kernel(const SyrkBatch* 
   const SyrkProblem& P = t[lo];
   const int local = b - P.block_begin;
   const int tiles = P.p.ntiles * (P.p.ntiles + 1) / 2;
-  syrk_vec_tile<DT, VB>(P.p, local % tiles, local / tiles, smem);
+  syrk_vec_tile<DT, VB, TW>(P.p, local % tiles, local / tiles, smem);
 }
 
 // Grouped EMA (with the internal->reference permutation): one block row per
@@ -959,7 +972,8 @@ KFAC_API int kfac_syrk_problem_init(SyrkProblem* P, int block_begin, int dtype, 
                                     long long sc, long long sh, long long sw, int B, int C, int H,
                                     int W, int kh, int kw, int sth, int stw, int ph, int pw, int dh,
                                     int dw, int has_bias, float scale, float* ws, int ldw,
-                                    long long split_rows) {
+                                    long long split_rows, int tile_width) {
+  if (tile_width != 128 && tile_width != 256) return 0;
   if (!(dtype == KDT_BF16 || dtype == KDT_F16)) return 0;
   if (sc != 1 || (C % 8) || (sb % 8) || (H > 1 && (sh % 8)) || (W > 1 && (sw % 8)) ||
       (((uintptr_t)x) & 15))
@@ -975,7 +989,7 @@ KFAC_API int kfac_syrk_problem_init(SyrkProblem* P, int block_begin, int dtype, 
   p.kcols = C * kh * kw;
   p.ncols = p.kcols + (has_bias ? 1 : 0);
   p.M = (long long)B * p.OH * p.OW;
-  p.ntiles = (p.ncols + BT - 1) / BT;
+  p.ntiles = (p.ncols + tile_width - 1) / tile_width;
   p.scale = scale; p.ws = ws; p.ldw = ldw;
   if (p.M <= 0) return 0;
   if (split_rows < VBK) split_rows = VBK;
@@ -986,37 +1000,54 @@ KFAC_API int kfac_syrk_problem_init(SyrkProblem* P, int block_begin, int dtype, 
   splits = (p.M + p.rows_per_split - 1) / p.rows_per_split;
   P->dtype = dtype;
   P->block_begin = block_begin;
-  P->pad = 0;
+  P->tw = tile_width;
   P->blocks = (int)(splits * (p.ntiles * (p.ntiles + 1) / 2));
   return P->blocks;
 }
 
 // host_table: `count` SyrkProblem records (block_begin relative to the
 // first); launched in batches of MAX_SYRK_PROBLEMS.
+// The 256-wide problems go first (their long k-loops start first), then the
+// 128-wide ones; one launch per tile width and MAX_SYRK_PROBLEMS problems.
 KFAC_API int kfac_syrk_grouped(const void* host_table, int count, int dtype, hipStream_t stream) {
   const SyrkProblem* t = (const SyrkProblem*)host_table;
-  for (int base = 0; base < count; base += MAX_SYRK_PROBLEMS) {
-    SyrkBatch b;
-    memset(&b, 0, sizeof(b));   // deterministic table bytes (devtable key)
-    b.count = count - base < MAX_SYRK_PROBLEMS ? count - base : MAX_SYRK_PROBLEMS;
-    int blocks = 0;
-    for (int k = 0; k < b.count; ++k) {
-      b.prob[k] = t[base + k];
-      b.prob[k].block_begin = blocks;
-      blocks += b.prob[k].blocks;
+  if (dtype != KDT_BF16 && dtype != KDT_F16) return -1;
+  for (int tw : {256, 128}) {
+    std::vector<int> sel;
+    for (int k = 0; k < count; ++k)
+      if (t[k].tw == tw) sel.push_back(k);
+    for (size_t base = 0; base < sel.size(); base += MAX_SYRK_PROBLEMS) {
+      SyrkBatch b;
+      memset(&b, 0, sizeof(b));   // deterministic table bytes (devtable key)
+      b.count = (int)std::min(sel.size() - base, (size_t)MAX_SYRK_PROBLEMS);
+      int blocks = 0;
+      for (int k = 0; k < b.count; ++k) {
+        b.prob[k] = t[sel[base + k]];
+        b.prob[k].block_begin = blocks;
+        blocks += b.prob[k].blocks;
+      }
+      if (blocks == 0) continue;
+      int terr = 0;
+      const SyrkBatch* d = (const SyrkBatch*)kfac_devtable::get(&b, sizeof(b), stream, &terr);
+      if (!d) return terr;
+      if (tw == 256) {
+        if (dtype == KDT_BF16)
+          hipLaunchKernelGGL((syrk_vec_grouped_kernel<KDT_BF16, 256>), dim3(blocks), dim3(512), 0,
+                             stream, d);
+        else
+          hipLaunchKernelGGL((syrk_vec_grouped_kernel<KDT_F16, 256>), dim3(blocks), dim3(512), 0,
+                             stream, d);
+      } else {
+        if (dtype == KDT_BF16)
+          hipLaunchKernelGGL((syrk_vec_grouped_kernel<KDT_BF16, 128>), dim3(blocks), dim3(256), 0,
+                             stream, d);
+        else
+          hipLaunchKernelGGL((syrk_vec_grouped_kernel<KDT_F16, 128>), dim3(blocks), dim3(256), 0,
+                             stream, d);
+      }
+      int err = (int)hipGetLastError();
+      if (err) return err;
     }
-    if (blocks == 0) continue;
-    int terr = 0;
-    const SyrkBatch* d = (const SyrkBatch*)kfac_devtable::get(&b, sizeof(b), stream, &terr);
-    if (!d) return terr;
-    if (dtype == KDT_BF16)
-      hipLaunchKernelGGL(syrk_vec_grouped_kernel<KDT_BF16>, dim3(blocks), dim3(256), 0, stream, d);
-    else if (dtype == KDT_F16)
-      hipLaunchKernelGGL(syrk_vec_grouped_kernel<KDT_F16>, dim3(blocks), dim3(256), 0, stream, d);
-    else
-      return -1;
-    int err = (int)hipGetLastError();
-    if (err) return err;
   }
   return 0;
 }
@@ -1080,8 +1111,9 @@ KFAC_API int kfac_tile_reduce(const void* host_jobs, int count, hipStream_t stre
     for (int k = 0; k < b.count; ++k) {
       b.job[k] = t[base + k];
       if (b.job[k].ncontrib > MAX_CONTRIB) return -2;
+      if (b.job[k].bt != 128 && b.job[k].bt != 256) return -3;
       b.job[k].block_begin = blocks;
-      blocks += RED_WG * (b.job[k].ntiles * (b.job[k].ntiles + 1) / 2);
+      blocks += (b.job[k].bt * b.job[k].bt / 1024) * (b.job[k].ntiles * (b.job[k].ntiles + 1) / 2);
     }
     if (blocks == 0) continue;
     int terr = 0;

@@ -111,7 +111,7 @@ _SIGS = {
     'kfac_ema_job_size': [],
     'kfac_syrk_problem_init': [c_vp, c_int, c_int, c_vp, c_ll, c_ll, c_ll, c_ll, c_int, c_int,
                                c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                               c_int, c_int, c_f, c_vp, c_int, c_ll],
+                               c_int, c_int, c_f, c_vp, c_int, c_ll, c_int],
     'kfac_syrk_grouped': [c_vp, c_int, c_int, c_vp],
     'kfac_ema_grouped': [c_vp, c_int, c_vp],
     'kfac_factor_ema_perm': [c_int, c_vp, c_vp, c_int, c_int, c_f, c_int, c_int, c_int, c_int,

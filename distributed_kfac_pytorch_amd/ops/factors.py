@@ -12,6 +12,7 @@ kfac/layers/linear.py:12-59, kfac/layers/utils.py:13-43,164-178.
 """
 import collections
 import ctypes
+import os
 
 import torch
 
@@ -76,10 +77,23 @@ def _vec_eligible(s):
 
 
 TILE = 128    # csrc/factors.hip output tile
+# grouped SYRK: factors with at least KFAC_SYRK_WIDE_MIN columns use 256-wide
+# output tiles (8 waves): each tile streams its two column panels for 4x the
+# products, half the operand bytes per product.  Opt-in (0 = off): the
+# ResNet-50 factor step measured 3.25-3.36 ms with wide tiles from n >= 256 /
+# 512 / 1024 against 3.26-3.30 ms without (profiles/r6_syrk_wide*.log) --
+# the grouped SYRK kernel (1.70 of the 3.3 ms) is not bound by its operand
+# bytes; the EMA (0.74 ms), the fp32 conv1 path (0.51) and the tile
+# reduction (0.36) are the rest (profiles/r6_factor_step_kernels.csv)
+WIDE_MIN = int(os.environ.get('KFAC_SYRK_WIDE_MIN', '0'))
 
 
-def _tile_pairs(n):
-    t = (n + TILE - 1) // TILE
+def _tile_width(n):
+    return 256 if WIDE_MIN > 0 and n >= WIDE_MIN else TILE
+
+
+def _tile_pairs(n, tw=TILE):
+    t = (n + tw - 1) // tw
     return t * (t + 1) // 2
 
 
@@ -88,17 +102,19 @@ class RedJob(ctypes.Structure):
     _fields_ = [('ws', ctypes.c_void_p), ('ldw', ctypes.c_int), ('ncols', ctypes.c_int),
                 ('ntiles', ctypes.c_int), ('ncontrib', ctypes.c_int),
                 ('part', ctypes.c_void_p * 8), ('splits', ctypes.c_int * 8),
-                ('block_begin', ctypes.c_int), ('accum', ctypes.c_int)]
+                ('block_begin', ctypes.c_int), ('accum', ctypes.c_int),
+                ('bt', ctypes.c_int), ('pad', ctypes.c_int)]
 
 
-def _red_jobs(ws_ptr, ldw, n, contribs):
+def _red_jobs(ws_ptr, ldw, n, contribs, tw=TILE):
     """contribs: [(part pointer, splits)] in the fixed summation order ->
     one RedJob per chunk of MAX_CONTRIB contributions: chunk 0 stores, the
     later chunks add (launched in order by _tile_reduce: deterministic)."""
     jobs = []
     for c0 in range(0, max(len(contribs), 1), MAX_CONTRIB):
         J = RedJob()
-        J.ws, J.ldw, J.ncols, J.ntiles = ws_ptr, ldw, n, (n + TILE - 1) // TILE
+        J.ws, J.ldw, J.ncols, J.ntiles = ws_ptr, ldw, n, (n + tw - 1) // tw
+        J.bt = tw
         chunk = contribs[c0:c0 + MAX_CONTRIB]
         J.ncontrib = len(chunk)
         J.accum = int(c0 > 0)
@@ -329,7 +345,7 @@ def update_factors_grouped(items, alpha, tag=''):
             nb = L.kfac_syrk_problem_init(
                 ctypes.byref(raw, i * psize), blocks, _lib.DTYPE_CODE[dtype], _lib.ptr(x),
                 sb, sc, sh, sw, B, C, H, W, g.kh, g.kw, g.sh, g.sw, g.ph, g.pw, g.dh, g.dw,
-                int(s.has_bias), s.scale, _lib.c_vp(ws_ptr), n, SPLIT_ROWS)
+                int(s.has_bias), s.scale, _lib.c_vp(ws_ptr), n, SPLIT_ROWS, _tile_width(n))
             if nb <= 0:
                 raise RuntimeError('grouped SYRK rejected an eligible source')
             nbs.append(nb)
@@ -337,7 +353,8 @@ def update_factors_grouped(items, alpha, tag=''):
         launches.append((dtype, probs, raw, nbs))
     # partial tiles of every (problem, split, tile pair): one arena, then the
     # fixed-order tile reduction per factor (sources in order, splits in order)
-    tot_parts = sum(sum(nbs) for _, _, _, nbs in launches) * TILE * TILE
+    tot_parts = sum(nb * _tile_width(ws_of[k][1]) ** 2
+                    for _, probs, _, nbs in launches for (k, _), nb in zip(probs, nbs))
     parts = _lib.workspace(dev, tot_parts, tag='syrk_parts_grouped' + tag)
     poff = 0
     for dtype, probs, raw, nbs in launches:
@@ -345,12 +362,13 @@ def update_factors_grouped(items, alpha, tag=''):
             ptr = parts.data_ptr() + 4 * poff
             L.kfac_syrk_problem_set_part(ctypes.byref(raw, i * psize), _lib.c_vp(ptr))
             L.kfac_syrk_problem_set_dscale(ctypes.byref(raw, i * psize), _dptr(s.dscale))
-            contribs[k].append((ptr, nb // _tile_pairs(ws_of[k][1])))
-            poff += nb * TILE * TILE
+            tw = _tile_width(ws_of[k][1])
+            contribs[k].append((ptr, nb // _tile_pairs(ws_of[k][1], tw)))
+            poff += nb * tw * tw
         _lib.check(L.kfac_syrk_grouped(raw, len(probs), _lib.DTYPE_CODE[dtype], stream),
                    'kfac_syrk_grouped')
     _tile_reduce([_red_jobs(arena.data_ptr() + 4 * ws_of[k][0], ws_of[k][1], ws_of[k][1],
-                            contribs[k]) for k in grouped], stream)
+                            contribs[k], _tile_width(ws_of[k][1])) for k in grouped], stream)
     jobs = (EmaJob * len(grouped))()
     a1, a2 = alpha / (1.0 - alpha), 1.0 - alpha
     for j, k in enumerate(grouped):

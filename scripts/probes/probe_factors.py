@@ -40,7 +40,8 @@ def timeit(fn, n=20):
     e1.record(); torch.cuda.synchronize()
     return e0.elapsed_time(e1) / n
 
-for split in (512, 1024, 2048, 4096, 8192):
+for split in [int(v) for v in os.environ.get('PROBE_SPLITS', '512,1024,2048,4096,8192').split(',')]:
     factors.SPLIT_ROWS = split
     t = timeit(lambda: factors.update_factors_grouped(items, 0.95))
-    print('SPLIT_ROWS %5d: %.3f ms per factor step (%.0f TFLOP/s)' % (split, t, flops / t / 1e9), flush=True)
+    print('SPLIT_ROWS %5d (wide tiles from n >= %d): %.3f ms per factor step (%.0f TFLOP/s)' % (
+        split, factors.WIDE_MIN, t, flops / t / 1e9), flush=True)
