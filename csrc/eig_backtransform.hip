@@ -55,6 +55,16 @@ const int g_bt_prec = [] {
   const char* e = getenv("KFAC_EIG_GEMM");
   return (e && !strcmp(e, "fp32")) ? (int)PREC_F32 : (int)PREC_BF16X6F;
 }();
+// the products whose operands are bounded by 1 -- G_k = V_k V_k^T and
+// W1 = Z^T V_k (reflector entries |v| <= 1, eigenvector entries |z| <= 1) --
+// run fp16x3 with a fixed 2^14 scale (PREC_F16X3F) unless KFAC_EIG_GEMM
+// names bf16x6 / fp32; T_k (S2) and the update with W2 (S3) keep bf16x6
+const int g_bt_prec_bounded = [] {
+  const char* e = getenv("KFAC_EIG_GEMM");
+  if (e && !strcmp(e, "fp32")) return (int)PREC_F32;
+  if (e && !strcmp(e, "bf16x6")) return (int)PREC_BF16X6F;
+  return (int)PREC_F16X3F;
+}();
 
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
@@ -234,7 +244,8 @@ struct BtArgs {
 
 // One recorded operation of the back-transformation.
 struct BtOp {
-  int kind;              // 0 pgemm, 1 split copy, 2 memset, 3 make_v, 4 larft, 5 slab sum (count = slabs)
+  int kind;              // 0 pgemm, 1 split copy, 2 memset, 3 make_v, 4 larft, 5 slab sum (count = slabs),
+                         // 6 pgemm of bounded operands (g_bt_prec_bounded)
   size_t off; int count; int tiles;    // table offset (bytes) / records / tiles
   void* ptr; size_t bytes;             // memset
 };
@@ -245,14 +256,16 @@ struct BtPlan {
   hipGraphExec_t exec = nullptr;
 };
 
-void add_pgemm(std::vector<unsigned char>& host, std::vector<BtOp>& ops, std::vector<PGemm>& recs) {
+void add_pgemm(std::vector<unsigned char>& host, std::vector<BtOp>& ops, std::vector<PGemm>& recs,
+               bool bounded = false) {
   int tiles = 0;
   for (auto& r : recs) {
     r.tiles_n = cdiv(r.N, 128);
     r.tile_begin = tiles;
     tiles += cdiv(r.M, 128) * r.tiles_n;
+    if (bounded) r.ea = r.eb = LP_QEXP;
   }
-  BtOp op{0, host.size(), (int)recs.size(), tiles, nullptr, 0};
+  BtOp op{bounded ? 6 : 0, host.size(), (int)recs.size(), tiles, nullptr, 0};
   const unsigned char* p = (const unsigned char*)recs.data();
   host.insert(host.end(), p, p + recs.size() * sizeof(PGemm));
   while (host.size() % 256) host.push_back(0);
@@ -288,7 +301,7 @@ void build_plan(const BtArgs& a, BtPlan& plan, std::vector<unsigned char>& host)
       recs.push_back(rec(Vk, a.lda, Vk, a.lda, G + m * tstride + (long long)k * BT * BT, BT, kb,
                          kb, a.lda - j0, EPI_STORE));
     }
-  add_pgemm(host, plan.ops, recs);
+  add_pgemm(host, plan.ops, recs, true);
   plan.ops.push_back(BtOp{4, 0, 0, 0, nullptr, 0});
   for (int k = nblk - 1; k >= 0; --k) {
     const int j0 = k * BT, kb = n - j0 < BT ? n - j0 : BT, Kn = a.lda - j0;
@@ -307,7 +320,7 @@ void build_plan(const BtArgs& a, BtPlan& plan, std::vector<unsigned char>& host)
                            a.W1 + ((long long)m * nsl + s) * w1s, BT, n, kb, kc, EPI_STORE));
       }
     }
-    add_pgemm(host, plan.ops, recs);
+    add_pgemm(host, plan.ops, recs, true);
     if (ns > 1) plan.ops.push_back(BtOp{5, 0, ns, 0, nullptr, 0});
     for (int m = 0; m < b; ++m)
       recs.push_back(rec(a.W1 + (long long)m * nsl * w1s, BT, T + m * tstride + (long long)k * BT * BT, BT,
@@ -345,6 +358,9 @@ int run_plan(const BtArgs& a, const BtPlan& plan, hipStream_t stream) {
     const unsigned char* t = (const unsigned char*)plan.tables + op.off;
     switch (op.kind) {
       case 0: err = kfac_pgemm(g_bt_prec, TILE_F32, t, op.count, op.tiles, nullptr, stream); break;
+      case 6:
+        err = kfac_pgemm(g_bt_prec_bounded, TILE_F32, t, op.count, op.tiles, nullptr, stream);
+        break;
       case 1: err = kfac_split_copy(PREC_F32, t, op.count, op.tiles, stream); break;
       case 2: {
         const long long n4 = (long long)(op.bytes / 16);

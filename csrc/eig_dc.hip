@@ -60,12 +60,15 @@ constexpr double EPS64 = 1.1102230246251565e-16;   // 2^-53
 constexpr int MAX_IT = 64;
 constexpr int RPB = 4;            // secular: roots (waves) per block
 constexpr int TILE_F32 = 0;       // pgemm 128 x 128, 4 waves (profiles/r2_pgemm_sweep.log)
-// GEMM precision of the merge (eigenvector update): bf16x6 on the fp32 operands
-// (PREC_BF16X6F: six bf16 MFMA products, fp32-level error, at the bf16 MFMA
-// rate) unless KFAC_EIG_GEMM=fp32 (exact f32 MFMA)
+// GEMM precision of the merge (eigenvector update Zw = U ZpT): both operands
+// are orthogonal-matrix entries (|x| <= 1), so fp16x3 with a fixed 2^14
+// scale (PREC_F16X3F: three fp16 MFMA products, 22 significand bits); or
+// KFAC_EIG_GEMM=bf16x6 (six bf16 products) / fp32 (exact f32 MFMA)
 const int g_dc_prec = [] {
   const char* e = getenv("KFAC_EIG_GEMM");
-  return (e && !strcmp(e, "fp32")) ? (int)PREC_F32 : (int)PREC_BF16X6F;
+  if (e && !strcmp(e, "fp32")) return (int)PREC_F32;
+  if (e && !strcmp(e, "bf16x6")) return (int)PREC_BF16X6F;
+  return (int)PREC_F16X3F;
 }();
 constexpr int TYP_SHIFT = 28;
 constexpr int SRC_MASK = (1 << TYP_SHIFT) - 1;
@@ -803,6 +806,7 @@ int build_plan(const std::vector<DcMat>& mats, DcPlan& P) {
         memset(&r, 0, sizeof(r));
         r.lda = M.ldw; r.ldb = M.ldw; r.ldc = M.ldw;
         r.M = 0; r.N = side ? n2 : n1; r.K = 0; r.epi = EPI_STORE;
+        r.ea = r.eb = LP_QEXP;             // |U|, |ZpT| <= 1 (PREC_F16X3F)
         // placeholders until the prep kernel patches them (never read with M = 0)
         r.a_hi = r.a_lo = (const void*)M.U; r.b_hi = r.b_lo = (const void*)M.ZpT;
         r.c_hi = r.c_lo = (void*)M.Zw;

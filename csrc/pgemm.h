@@ -26,9 +26,13 @@
 // PREC_H1A / B, PREC_F1A / B: one bf16 / fp16 plane, one MFMA per product:
 //   the reference's inv_dtype = bfloat16 / float16 preconditioning
 //   (kfac/layers/base.py:435-441,463,470) on the grouped chain.
+// PREC_F16X3F: both operands fp32, each split while staged into scaled fp16
+//   hi / lo planes with a FIXED exponent from the record (ea, eb): for
+//   products whose operands are bounded by construction -- the eigensolver's
+//   orthogonal factors (|x| <= 1: e = 14).
 enum { PREC_F32 = 0, PREC_BF16X3 = 1, PREC_BF16X6 = 2, PREC_BF16X6F = 3, PREC_BF16X6A = 4,
        PREC_BF16X6B = 5, PREC_F16X3A = 6, PREC_F16X3B = 7, PREC_H1A = 8, PREC_H1B = 9,
-       PREC_F1A = 10, PREC_F1B = 11 };
+       PREC_F1A = 10, PREC_F1B = 11, PREC_F16X3F = 12 };
 // split_copy / store_planes modes of the low-plane eigenvector operands
 enum { STORE_F16X2 = 20, STORE_BF16X1 = 21, STORE_F16X1 = 22 };
 constexpr int LP_QEXP = 14;      // scale exponent of the fp16 eigenvector planes
@@ -50,6 +54,7 @@ struct PGemm {
   // low-plane modes: max |x| bits of the fp32 operand (read), of this stage's
   // output (atomicMax, when it feeds the next stage), a slot to zero (or null)
   const unsigned* sc_in; unsigned* sc_out; unsigned* sc_zero;
+  int ea, eb;             // PREC_F16X3F: scale exponents of the A / B operands
 };
 
 // dst[r][c] (planes or fp32, ld ldo) <- src[r][c] (fp32, ld lds), or the

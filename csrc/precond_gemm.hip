@@ -141,10 +141,11 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   // low-plane mixed modes (pgemm.h): LPA / LPB = which operand is the planes one
   constexpr bool LPA = PREC == PREC_F16X3A || PREC == PREC_H1A || PREC == PREC_F1A;
   constexpr bool LPB = PREC == PREC_F16X3B || PREC == PREC_H1B || PREC == PREC_F1B;
-  constexpr bool LP = LPA || LPB;
+  constexpr bool F3F = PREC == PREC_F16X3F;      // both operands fp32, fixed scales
+  constexpr bool LP = LPA || LPB || F3F;
   constexpr bool LPH = PREC == PREC_F16X3A || PREC == PREC_F16X3B || PREC == PREC_F1A ||
-                       PREC == PREC_F1B;           // fp16 (scaled) vs bf16
-  constexpr int LPN = (PREC == PREC_F16X3A || PREC == PREC_F16X3B) ? 2 : 1;   // planes
+                       PREC == PREC_F1B || F3F;    // fp16 (scaled) vs bf16
+  constexpr int LPN = (PREC == PREC_F16X3A || PREC == PREC_F16X3B || F3F) ? 2 : 1;   // planes
   constexpr bool PA = X6A || LPA, PB = X6B || LPB;  // plane operand in memory
   constexpr bool X6M = X6A || X6B || LP;          // one operand planes, one fp32
   constexpr bool SPL = X3 || X6;                  // split-bf16 planes in memory
@@ -271,8 +272,10 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   }
   const u32x4n z4 = {0u, 0u, 0u, 0u};
   // low-plane fp16 modes: scale of the fp32 operand (its producer's max slot)
-  const int lp_e = (LP && LPH) ? lp_exp(*(const AS1 unsigned*)P.sc_in) : 0;
-  const float lp_s = pow2f(lp_e);
+  const int lp_e = (LP && LPH && !F3F) ? lp_exp(*(const AS1 unsigned*)P.sc_in) : 0;
+  // scale of the fp32 operand(s) as they are converted: A / B
+  const float lp_sa = F3F ? pow2f(P.ea) : pow2f(lp_e);
+  const float lp_sb = F3F ? pow2f(P.eb) : pow2f(lp_e);
   // X6F: buffer loads -- the per-thread byte offset stays in one VGPR and the
   // k-step advances the scalar soffset: no 64-bit address rebuilt per load
   // (operands < 4 GiB, checked on the host)
@@ -329,7 +332,7 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
     *(u32x2n*)(dst + 2 * plane_stride) = pl;
   };
   // LP: four fp32 values -> LPN fp16 (scaled by lp_s) or one bf16 quad
-  auto store_lp = [&](uint16_t* dst, long long plane_stride, const u32x4n& v) {
+  auto store_lp = [&](uint16_t* dst, long long plane_stride, const u32x4n& v, float lp_s) {
     typedef unsigned u32x2n __attribute__((ext_vector_type(2)));
     uint16_t h[4], l[4];
 #pragma unroll
@@ -366,7 +369,7 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
       chunk_rc(c, BM, CPRA, ESZA, row, kof);
       const u32x4n v = oka[q] ? ra[SET][q] : z4;
       if (PA) *(u32x4n*)((uint16_t*)img + (plane * BM + row) * LDB16 + x6f_off(row, kof)) = v;
-      else if (LP) store_lp((uint16_t*)img + row * LDB16 + x6f_off(row, kof), (long long)BM * LDB16, v);
+      else if (LP) store_lp((uint16_t*)img + row * LDB16 + x6f_off(row, kof), (long long)BM * LDB16, v, lp_sa);
       else if (SWZ) store_split((uint16_t*)img + row * LDB16 + x6f_off(row, kof), (long long)BM * LDB16, v);
       else if (SPL) *(u32x4n*)((uint16_t*)img + (plane * BM + row) * LDB16 + kof) = v;
       else *(u32x4n*)((float*)img + row * LDF32 + kof) = (row & 16) ? v.zwxy : v;
@@ -380,7 +383,7 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
       const u32x4n v = okb[q] ? rb[SET][q] : z4;
       if (PB) *(u32x4n*)((uint16_t*)img + (PL * BM + plane * BN + row) * LDB16 + x6f_off(row, kof)) = v;
       else if (LP) store_lp((uint16_t*)img + (PL * BM + row) * LDB16 + x6f_off(row, kof),
-                            (long long)BN * LDB16, v);
+                            (long long)BN * LDB16, v, lp_sb);
       else if (SWZ) store_split((uint16_t*)img + (PL * BM + row) * LDB16 + x6f_off(row, kof),
                                 (long long)BN * LDB16, v);
       else if (SPL) *(u32x4n*)((uint16_t*)img + (PL * BM + plane * BN + row) * LDB16 + kof) = v;
@@ -595,7 +598,8 @@ void pgemm_kernel(const PGemm* __restrict__ table, int count, double* __restrict
   const float damping = P.damping;
   float kl_part = 0.f;
   // LP fp16: C = acc 2^-(LP_QEXP + lp_e) (exact: a power of two)
-  const float lp_unscale = (LP && LPH) ? pow2f(-(LP_QEXP + lp_e)) : 1.f;
+  const float lp_unscale = (LP && LPH) ? (F3F ? pow2f(-(P.ea + P.eb)) : pow2f(-(LP_QEXP + lp_e)))
+                                       : 1.f;
   float lp_max = 0.f;                             // max |stored C| (next stage's scale)
   // one straight-line loop nest per epilogue kind (a run-time kind test per
   // element would split the loads into basic blocks with a wait each)
@@ -904,6 +908,13 @@ KFAC_API int kfac_pgemm(int prec, int tile, const void* dev_table, int count, in
   } else if (prec == PREC_BF16X6B) {
     hipLaunchKernelGGL((pgemm_kernel<PREC_BF16X6B, 128, 128, 2, 2, 2, false, true>), g, dim3(256),
                        0, stream, t, count, kl);
+  } else if (prec == PREC_F16X3F) {
+    if (g_pgemm_xcd)
+      hipLaunchKernelGGL((pgemm_kernel<PREC_F16X3F, 128, 128, 2, 2, 2, false, true>), g, dim3(256),
+                         0, stream, t, count, kl);
+    else
+      hipLaunchKernelGGL((pgemm_kernel<PREC_F16X3F, 128, 128, 2, 2, 2>), g, dim3(256), 0, stream,
+                         t, count, kl);
   } else if (prec >= PREC_F16X3A && prec <= PREC_F1B) {
     // tile 6 / 7: 256 x 128 / 128 x 256 with 8 waves (fewer operand bytes per
     // product for problems with a dimension >= 256), else 128 x 128

@@ -129,7 +129,7 @@ class PGemmRec(ctypes.Structure):
                 ('M', ctypes.c_int), ('N', ctypes.c_int), ('K', ctypes.c_int), ('epi', ctypes.c_int),
                 ('tile_begin', ctypes.c_int), ('tiles_n', ctypes.c_int),
                 ('sc_in', ctypes.c_void_p), ('sc_out', ctypes.c_void_p),
-                ('sc_zero', ctypes.c_void_p)]
+                ('sc_zero', ctypes.c_void_p), ('ea', ctypes.c_int), ('eb', ctypes.c_int)]
 
 
 class GatherRec(ctypes.Structure):
