@@ -48,6 +48,7 @@ for s in "$@"; do
         --output-format csv -- python3 bench.py --steps $STEPS --warmup $WARMUP $BENCH_ARGS
       f=$(find /tmp/prof_bench -name "*kernel_trace.csv" | head -1)
       python3 scripts/prof_window.py "$f" $STEPS > gpurun_out/prof_window_summary.txt
+      python3 scripts/probes/trace_inverse_start.py "$f" > gpurun_out/prof_inverse_start.txt || true
       head -40 gpurun_out/prof_window_summary.txt ;;
     probe) step probe 600 python -u $PROBE ;;
     probe-prof)

@@ -13,6 +13,10 @@ import sys
 
 def category(name):
     n = name
+    if 'pgemm_kernel<3,' in n or 'pgemm_kernel<12,' in n:
+        # both operands fp32 (PREC_BF16X6F / PREC_F16X3F): the eigensolver's
+        # merge and back-transformation GEMMs, never the chain
+        return 'kfac: eigensolver GEMMs (D&C merge, back-transform)'
     if 'pgemm_kernel' in n:
         return 'kfac: precondition GEMM chain'
     if 'gather_grad' in n or 'grouped_apply' in n or 'grouped_kl' in n:
@@ -23,7 +27,7 @@ def category(name):
         return 'kfac: factor SYRK + EMA'
     if 'jacobi' in n:
         return 'kfac: small-n Jacobi eigensolver'
-    if 'red_fin' in n or 'red_symv' in n or 'red_upd' in n:
+    if 'red_fin' in n or 'red_symv' in n or 'red_upd' in n or 'red_tail' in n:
         return 'kfac: eigensolver tridiagonal reduction'
     if 'dc_' in n:
         return 'kfac: eigensolver divide and conquer'
