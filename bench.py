@@ -393,7 +393,8 @@ def main():
                            'precond_precision': args.precond_precision,
                            'inverse_lag': args.inverse_lag,
                            'overlap_precondition': bool(args.overlap_precond) and world == 1,
-                           'early_factors': bool(args.early_factors)},
+                           'early_factors': bool(args.early_factors),
+                           'early_inverse_launches': pre.early_inverse_launches},
                        'hip_graphs': use_graphs,
                        'fused_sgd': bool(args.fused_sgd and device.type == 'cuda'),
                        'weights': 'bf16 + fp32 masters' if weights is not None

@@ -274,14 +274,25 @@ class GraphedTrainStep(object):
             self.eager_steps += 1
             self._prepare_factor()
             with (self.pre.hook_factors() if self.hybrid else contextlib.nullcontext()):
+                # early inverse update (KFAC.arm_early_inverse): this
+                # forward/backward runs EAGERLY and its first gradient hook
+                # launches the leading eigensolve group under the rest of the
+                # backward (a replayed graph would hold it to the graph's end)
+                early = self.hybrid and hasattr(self.pre, 'arm_early_inverse') and \
+                    self.pre.arm_early_inverse()
                 loss = None
                 for i, (fb, cm) in enumerate(zip(self.fbs, self.comms)):
-                    seg = 'invfb' if self.hybrid else ('fb' if i == 0 else 'fb%d' % i)
-                    out = self._run_segment(seg, 'factor', fb, advances=False)
+                    if early:
+                        out = self._run_eager(fb)
+                    else:
+                        seg = 'invfb' if self.hybrid else ('fb' if i == 0 else 'fb%d' % i)
+                        out = self._run_segment(seg, 'factor', fb, advances=False)
                     if i == 0:
                         loss = out
                     if cm is not None:
                         cm()
+                if early:
+                    self.pre.disarm_early_inverse()
                 cur = torch.cuda.current_stream()
                 self.side.wait_stream(cur)
                 with torch.cuda.stream(self.side):
@@ -336,6 +347,15 @@ class GraphedTrainStep(object):
         self.side.wait_stream(cur)
         with torch.cuda.stream(self.side):
             out = self._eager_body()
+        cur.wait_stream(self.side)
+        return out
+
+    def _run_eager(self, fn):
+        """One segment eagerly on the capture stream (as a warm-up run)."""
+        cur = torch.cuda.current_stream()
+        self.side.wait_stream(cur)
+        with torch.cuda.stream(self.side):
+            out = fn()
         cur.wait_stream(self.side)
         return out
 

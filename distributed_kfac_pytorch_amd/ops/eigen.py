@@ -211,7 +211,43 @@ FUSED_STREAMS = int(os.environ.get('KFAC_EIG_FUSED_STREAMS', '2'))
 FUSED_SPLIT = bool(int(os.environ.get('KFAC_EIG_FUSED_SPLIT', '1')))
 
 
-def _large_fused(mats, clip, stream, use_graph=True, finite=None):
+def leading_group(sizes):
+    """Indices of the group _fused_groups puts on the caller's stream first
+    (the critical chain: every n above half the largest), or None when the
+    solve is not split over streams."""
+    if not sizes or not FUSED_SPLIT or FUSED_STREAMS < 2:
+        return None
+    nmax = max(sizes)
+    return [i for i, n in enumerate(sizes) if 2 * n > nmax]
+
+
+def early_stream(device):
+    """The worker stream of symeig_group (the first of the side-stream pool:
+    the stream _large_fused's second group uses, so the early chain and the
+    caller's stream sit on two hardware queues as in a split solve)."""
+    return _side_streams(device, 1)[0]
+
+
+def symeig_group(mats, clip, stream, finite=None):
+    """Enqueue the fused solve of `mats` as ONE group on `stream` (staging,
+    reduction, divide and conquer, back-transformation; slot 0 buffers, as the
+    leading group of a split solve) and return [(Q, d)] without joining:
+    the caller orders its stream after `stream` before reading them.  KFAC's
+    early inverse update runs the leading group this way while the rest of
+    the step's factors are still being computed."""
+    if not mats:
+        return []
+    if any(A.shape[0] <= 1 or A.shape[0] > FUSED_MAX_N for A in mats):
+        raise ValueError('symeig_group: sizes 2 .. {} only'.format(FUSED_MAX_N))
+    _lib.check_pgemm_extent(max(A.shape[0] for A in mats))
+    outs = _fused_group(mats, clip, stream, True, 0, finite)
+    for A in mats:
+        A.record_stream(stream)
+    del _INFOS[:-256]
+    return outs
+
+
+def _large_fused(mats, clip, stream, use_graph=True, finite=None, split=True):
     """Every factor of the inverse update in ragged launch sequences: per
     group (_fused_groups) the fused one-launch-per-column reduction over all
     its matrices (csrc/eig_reduce.hip), the batched divide and conquer over
@@ -225,7 +261,7 @@ def _large_fused(mats, clip, stream, use_graph=True, finite=None):
     largest factors' chain on a high-priority stream (162 vs 157 ms; 277 ms
     in round 4)."""
     dev = mats[0].device
-    groups = _fused_groups(mats)
+    groups = _fused_groups(mats) if split else [list(range(len(mats)))]
     outs = [None] * len(mats)
     caller = stream
     streams = [stream] + _side_streams(dev, len(groups) - 1)
@@ -469,12 +505,14 @@ def sanitize(A, ok, out=None):
     return torch.where(ok, A, _eye(A.shape[0], A.device), out=out)
 
 
-def symeig_many(mats, clip=0.0, solver='auto', finite=None):
+def symeig_many(mats, clip=0.0, solver='auto', finite=None, split=True):
     """Eigendecompose a list of symmetric fp32 matrices -> list of (Q, d).
 
     finite: None, or a device bool tensor (one flag per matrix): a matrix
     whose flag is False is decomposed as the identity instead (see
-    sanitize); the caller checks the flags after enqueueing its work."""
+    sanitize); the caller checks the flags after enqueueing its work.
+    split=False: the fused path runs every factor as one group on the
+    caller's stream (the leading group already runs elsewhere: symeig_group)."""
     global STAGE_EVENTS
     if len(mats) == 0:
         return []
@@ -546,7 +584,8 @@ def symeig_many(mats, clip=0.0, solver='auto', finite=None):
     if large:
         sub = [mats[i] for i in large]
         res = _large_fused(sub, clip, cur,
-                           finite=None if finite is None else [finite[i] for i in large])
+                           finite=None if finite is None else [finite[i] for i in large],
+                           split=split)
         for A in sub:
             A.record_stream(cur)
         for i, r in zip(large, res):

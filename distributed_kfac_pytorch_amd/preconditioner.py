@@ -322,6 +322,25 @@ class KFAC(optim.Optimizer):
         self._pending_inv = None
         self._inv_stream = None
         self._have_inverses = False
+        # early inverse update (GPU, one rank, graphs.GraphedTrainStep's
+        # inverse steps): the factors of the solve's leading group (the
+        # largest, all A factors -- ResNet-50's three 4608^2) are updated from
+        # the backward's FIRST gradient hook and their eigensolve is launched
+        # there, on the eigensolver's worker stream, while the backward and
+        # the other factors still run; compute_inverses() solves the rest and
+        # joins it.  Same inputs, same kernels as the one-batch solve.
+        # Opt-in (KFAC_EARLY_INVERSE=1 or this attribute): the armed
+        # forward/backward runs eagerly, and its host-bound backward slows
+        # the early chain about as much as the early start wins -- ResNet-50
+        # inverse step 120.7-123.7 ms against 121.7-122.7 without
+        # (profiles/README.md, round 6)
+        self.early_inverse = __import__('os').environ.get('KFAC_EARLY_INVERSE', '0') == '1'
+        self._early_inv_armed = False
+        self._early_inv_a_done = False
+        self._early_inv = None          # the solve in flight: jobs, results, stream, flags
+        self._early_inv_key = None
+        self._early_inv_jobs = None
+        self.early_inverse_launches = 0
 
         comm.init_comm_backend()
         size = comm.backend.size()
@@ -608,6 +627,8 @@ class KFAC(optim.Optimizer):
             return
         if self._early_a_due():
             self._launch_early_a()
+        if self._early_inv_armed and not self._early_inv_a_done:
+            self._early_inverse_factors()
         layer.save_grad_outputs((grad,))
         if self.compute_factor_in_hook:
             if self._hook_factors_grouped():
@@ -705,6 +726,105 @@ class KFAC(optim.Optimizer):
         for layer, st in zip(refs, outs):
             layer.state['A'] = st
         self._early_a = items
+
+    # ----------------------------------------------- early inverse update
+    def early_inverse_jobs(self):
+        """The (layer, 'A') jobs of the eigensolve's leading group
+        (eigen.leading_group over this step's factor sizes) when the early
+        inverse update applies: eigen path on the GPU, one rank, grouped
+        factors, synchronous inverses, and a leading group of A factors only.
+        [] otherwise.  Fixed per execution plan."""
+        key = self.plan_generation
+        if self._early_inv_key == key and self._early_inv_jobs is not None:
+            return self._early_inv_jobs
+        jobs = []
+        if (self.early_inverse and self.workers_assigned and self.use_eigen_decomp
+                and self.inverse_lag == 0 and self.grouped_factors and self.layers
+                and self.eigen_solver == 'auto' and not eigen_ops.TWO_STAGE
+                and self.layers[0].module.weight.is_cuda and comm.backend.size() == 1
+                and not self._reverse_hooked and not self.accumulate_data
+                and _lib.use_native(self.layers[0].module.weight)):
+            every = [(l, w) for l in self.layers for w in ('A', 'G')]
+            sizes = [l.state[w].shape[0] if l.state.get(w) is not None else 0
+                     for l, w in every]
+            if not all(sizes):
+                return []       # factors not allocated yet: decide later
+            lead = eigen_ops.leading_group(sizes)
+            if lead and len(lead) < len(every) and all(every[i][1] == 'A' for i in lead) \
+                    and all(1 < sizes[i] <= eigen_ops.FUSED_MAX_N for i in lead):
+                jobs = [every[i] for i in lead]
+        self._early_inv_key, self._early_inv_jobs = key, jobs
+        return jobs
+
+    def arm_early_inverse(self):
+        """graphs.GraphedTrainStep, before an inverse step's forward/backward,
+        which it then runs EAGERLY: the first gradient hook updates the
+        leading group's A factors and launches their solve on the
+        eigensolver's worker stream right there, under the rest of the
+        backward (_early_inverse_factors).  A replayed graph cannot be the
+        gate: on this ROCm an event recorded inside a graph, or a forked
+        branch of it, completes with the whole graph (profiles/README.md).
+        True when armed."""
+        self._early_inv_armed = bool(self.early_inverse_jobs())
+        self._early_inv_a_done = False
+        if self._early_inv_armed and eigen_ops.STAGE_LOG:
+            # KFAC_EIG_STAGE_LOG=1: the stage times of this step's solves
+            # are printed from the start of its forward/backward
+            eigen_ops.STAGE_EVENTS = []
+            eigen_ops._mark(-1, 'step', torch.cuda.current_stream())
+        return self._early_inv_armed
+
+    def disarm_early_inverse(self):
+        """After the armed forward/backward: True when its solve was launched
+        (compute_inverses() picks it up)."""
+        armed, self._early_inv_armed = self._early_inv_armed, False
+        done, self._early_inv_a_done = self._early_inv_a_done, False
+        return armed and done and self._early_inv is not None
+
+    def _early_inverse_factors(self):
+        self._early_inv_a_done = True
+        if torch.cuda.is_current_stream_capturing():
+            return      # never gated inside a graph (arm_early_inverse); step() solves all
+        alpha = self.param_groups[0]['factor_decay']
+        items, refs = [], []
+        for layer, _ in self._early_inv_jobs:
+            job = layer.take_factor_job('A')
+            if job is None:
+                continue
+            items.append((layer.state['A'], job[0], job[1], job[2]))
+            refs.append(layer)
+        self.join_factor_comm()
+        if items:
+            with self._no_autocast(items[0][0]):
+                outs = factor_ops.update_factors_grouped(items, alpha, tag='_early_inv')
+            for layer, st in zip(refs, outs):
+                layer.state['A'] = st
+        jobs = list(self._early_inv_jobs)
+        cur = torch.cuda.current_stream()
+        st = eigen_ops.early_stream(cur.device)
+        st.wait_stream(cur)
+        eigen_ops._mark(-1, 'early gate', st)
+        with torch.cuda.stream(st):
+            mats = [l.state[w].to(torch.float32) for l, w in jobs]
+            finite = _factors_finite(mats)
+            results = eigen_ops.symeig_group(mats, 0.0, st, finite=finite)
+        self._early_inv = dict(jobs=jobs, results=results, stream=st, finite=finite)
+        self.early_inverse_launches += 1
+
+    def _join_early_inverses(self):
+        """The early solve's jobs and (Q, d) results, ordered before the
+        current stream; (None, None) when none is in flight."""
+        e, self._early_inv = self._early_inv, None
+        if e is None:
+            return None, None
+        cur = torch.cuda.current_stream()
+        cur.wait_stream(e['stream'])
+        for Q, d in e['results']:
+            Q.record_stream(cur)
+            d.record_stream(cur)
+        e['finite'].record_stream(cur)
+        return e, [(Q.to(l.inv_dtype), d.to(l.inv_dtype))
+                   for (l, _), (Q, d) in zip(e['jobs'], e['results'])]
 
     def side_streams(self):
         """The streams other than the current one that K-FAC's last step may
@@ -1071,10 +1191,10 @@ class KFAC(optim.Optimizer):
                     jobs.append((layer, which))
         return jobs
 
-    def _solve_inverses(self, jobs, mats, damping, finite=None):
+    def _solve_inverses(self, jobs, mats, damping, finite=None, split=True):
         if self.use_eigen_decomp:
             results = eigen_ops.symeig_many(mats, clip=0.0, solver=self.eigen_solver,
-                                            finite=finite)
+                                            finite=finite, split=split)
             if _DEBUG_EIG:
                 _debug_check_eig(jobs, mats, results)
             return [(Q.to(l.inv_dtype), d.to(l.inv_dtype))
@@ -1120,9 +1240,30 @@ class KFAC(optim.Optimizer):
         self.join_factor_comm()
         jobs = self._inverse_jobs()
         self._have_inverses = True
-        if not jobs:
+        early = self._early_inv
+        if early is not None:
+            # the leading group is already being solved (_early_inverse_factors):
+            # the rest as one group on this stream, beside it
+            ek = {(id(l), w) for l, w in early['jobs']}
+            if not defer_check or not ek <= {(id(l), w) for l, w in jobs}:
+                raise RuntimeError('early inverse update in flight outside step()')
+            jobs = [(l, w) for l, w in jobs if (id(l), w) not in ek]
+        if not jobs and early is None:
             return
         mats = [l.state[w].to(torch.float32) for l, w in jobs]
+        if early is not None:
+            results = []
+            if jobs:
+                finite = _factors_finite(mats)
+                results = self._solve_inverses(jobs, mats, damping, finite, split=False)
+            e, eres = self._join_early_inverses()
+            every = [(l, w) for l in self.layers for w in ('A', 'G')]
+            self._deferred_checks.append(
+                (every, _factors_finite([l.state[w] for l, w in every])))
+            if self.check_solver:
+                self._solver_check_due = True
+            self._store_inverses(jobs + e['jobs'], results + eres, damping)
+            return
         if defer_check and self.use_eigen_decomp and mats[0].is_cuda:
             # no host read before the solve: flagged factors are solved as the
             # identity and the flags are checked at the end of step().  The

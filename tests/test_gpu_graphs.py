@@ -22,13 +22,14 @@ def deterministic_convs():
 
 
 def _train(use_graphs, steps=25, precision='fp32', segmented=False, set_to_none=False, lag=0,
-           amp=True, hybrid=False):
+           amp=True, hybrid=False, early=False):
     torch.manual_seed(0)
     m = resnet_cifar.resnet20().cuda().to(memory_format=torch.channels_last)
     opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9)
     pre = kfac.KFAC(m, factor_update_freq=2, inv_update_freq=10, lr=0.05,
                     precond_precision=precision, compute_factor_in_hook=segmented,
                     inverse_lag=lag)
+    pre.early_inverse = early
     g = torch.Generator(device='cuda').manual_seed(3)
     xs = [torch.randn(16, 3, 32, 32, device='cuda', generator=g) for _ in range(steps)]
     ys = [torch.randint(0, 10, (16,), device='cuda', generator=g) for _ in range(steps)]
@@ -116,10 +117,40 @@ def test_hybrid_inverse_steps_replay_their_forward_backward():
         torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = prev
     assert sh.hybrid and sh.replays > 0
     assert any(k[0] == 'invfb' for k in sh.graphs), list(sh.graphs)
+    assert sh.pre.early_inverse_launches == 0
     assert not sh.pre.compute_factor_in_hook        # restored after each inverse step
     for a, b in zip(le, lh):
         assert abs(a - b) <= 1e-6 * max(1.0, abs(a)), (le, lh)
     assert _pdiff(pe, ph) <= 1e-6, _pdiff(pe, ph)
+
+
+def test_early_inverse_update_matches_one_batch_solve():
+    """Hybrid trainer with the opt-in early inverse update (resnet20's five
+    576^2 A factors -- layer3 -- are the solve's leading group: updated
+    at the first gradient hook of the inverse step's eager
+    forward/backward and solved from there on the eigensolver's worker
+    stream, joined in step()) against the same trainer replaying an 'invfb'
+    graph and solving every factor in step(): same factors, the eigendata of
+    the same kernels."""
+    prev = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        lo, po, so = _train(True, steps=25, amp=False, hybrid=True, early=False)
+        le, pe, se = _train(True, steps=25, amp=False, hybrid=True, early=True)
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = prev
+    assert so.pre.early_inverse_launches == 0 and se.pre.early_inverse_launches == 2
+    assert any(k[0] == 'invfb' for k in so.graphs)
+    assert not any(k[0] == 'invfb' for k in se.graphs)
+    for a, b in zip(lo, le):
+        assert abs(a - b) <= 1e-6 * max(1.0, abs(a)), (lo, le)
+    assert _pdiff(po, pe) <= 1e-6, _pdiff(po, pe)
+    # eigenvalues (eigenvectors of clustered eigenvalues may rotate within the
+    # cluster between batch compositions; the preconditioned steps above agree)
+    for lo_, le_ in zip(so.pre.layers, se.pre.layers):
+        for key in ('dA', 'dG'):
+            a, b = lo_.state[key].float(), le_.state[key].float()
+            assert (a - b).abs().max().item() <= 1e-4 * max(1.0, a.abs().max().item()), key
 
 
 def _check_losses(le, le2, lg, rel):

@@ -291,3 +291,25 @@ def test_load_state_dict_keeps_plan_and_buffers():
     pre.load_state_dict(pre.state_dict())
     assert pre.plan is plan and pre.plan_generation == gen
     assert pre.layers[0].state['QA'].data_ptr() == qa.data_ptr()
+
+
+def test_early_inverse_leading_group_and_cpu_noop():
+    """eigen.leading_group names the split solve's first (critical) group --
+    every factor above half the largest; the early inverse update needs it
+    to hold A factors only and the native GPU path, so on the CPU it is off
+    and arming is a no-op (step() solves everything in one batch)."""
+    from distributed_kfac_pytorch_amd.ops import eigen
+    assert eigen.leading_group([4608, 512, 4608, 2304, 2305, 10]) == [0, 2, 4]
+    assert eigen.leading_group([64]) == [0]
+    assert eigen.leading_group([]) is None
+    m = resnet_cifar.resnet20()
+    pre = kfac.KFAC(m, factor_update_freq=1, inv_update_freq=2)
+    assert pre.early_inverse is False          # opt-in
+    pre.early_inverse = True
+    x, y = torch.randn(4, 3, 32, 32), torch.randint(0, 10, (4,))
+    for _ in range(3):
+        nn.functional.cross_entropy(m(x), y).backward()
+        assert pre.arm_early_inverse() is False
+        assert pre.disarm_early_inverse() is False
+        pre.step()
+    assert pre.early_inverse_jobs() == [] and pre.early_inverse_launches == 0
