@@ -52,7 +52,8 @@ def pytest_runtest_logfinish(nodeid, location):
 
 @pytest.hookimpl(tryfirst=True, hookwrapper=True)
 def pytest_runtest_makereport(item, call):
-    if _MARK and call.excinfo is not None and call.when in ('setup', 'call', 'teardown'):
+    if _MARK and call.excinfo is not None and call.when in ('setup', 'call', 'teardown') \
+            and not call.excinfo.errisinstance(pytest.skip.Exception):
         ex = call.excinfo
         try:
             frames = traceback.extract_tb(ex.tb)[-4:]
