@@ -162,7 +162,9 @@ struct RedJob {
   const float* part[MAX_CONTRIB];
   int splits[MAX_CONTRIB];
   int block_begin, accum;
-  int bt, pad;            // tile width of the partials (128 or 256)
+  int bt;                 // tile width of the partials (128 or 256)
+  int mirror;             // 1: also store the strict lower triangle (the grouped EMA
+                          // then reads whole rows, no column walks)
 };
 constexpr int MAX_RED_JOBS = 24;
 struct RedBatch {
@@ -171,11 +173,11 @@ struct RedBatch {
 };
 static_assert(sizeof(RedBatch) <= 4096, "kernel arguments are limited to 4 KB");
 
-// Each workgroup takes 1024 elements (a float4 per thread) of one tile pair:
-// RED_WG = 16 workgroups per 128-wide tile pair (64 per 256-wide one).  The split loop loads 8 partials at
-// a time (independent, in flight together) and adds them in order: the
-// summation order (contribution, split) is fixed, so the result is
-// deterministic.
+// Each workgroup takes a 32 x 32 block (a float4 of one row per thread) of
+// one tile pair: RED_WG = 16 workgroups per 128-wide tile pair (64 per
+// 256-wide one).  The split loop loads 8 partials at a time (independent, in
+// flight together) and adds them in order: the summation order
+// (contribution, split) is fixed, so the result is deterministic.
 constexpr int RED_WG = (BT * BT) / 1024;
 
 __global__ __launch_bounds__(256) void tile_reduce_kernel(const RedBatch* __restrict__ batch) {
@@ -187,14 +189,16 @@ __global__ __launch_bounds__(256) void tile_reduce_kernel(const RedBatch* __rest
     if (t[mid].block_begin <= b) lo = mid; else hi = mid - 1;
   }
   const RedJob& J = t[lo];
-  const int bt = J.bt, bt2 = bt * bt, rwg = bt2 / 1024;
+  const int bt = J.bt, bt2 = bt * bt, rwg = bt2 / 1024, nbc = bt / 32;
   const int loc = b - J.block_begin;
   const int tile = loc / rwg, part = loc - tile * rwg;
   int tt = tile, ti = 0, rem = J.ntiles;
   while (tt >= rem) { tt -= rem; ++ti; --rem; }
   const int tj = ti + tt;
   const int tp = J.ntiles * (J.ntiles + 1) / 2;
-  const int e = part * 1024 + threadIdx.x * 4;          // 4 consecutive elements of a row
+  const int br = part / nbc, bc = part - br * nbc;        // 32 x 32 block of the tile
+  const int lr = threadIdx.x >> 3, c4 = (threadIdx.x & 7) * 4;
+  const int e = (br * 32 + lr) * bt + bc * 32 + c4;       // 4 consecutive elements of a row
   const long long sstride = (long long)tp * bt2 / 4;    // float4 stride between splits
   fx4 acc = {0.f, 0.f, 0.f, 0.f};
   for (int c = 0; c < J.ncontrib; ++c) {
@@ -210,12 +214,33 @@ __global__ __launch_bounds__(256) void tile_reduce_kernel(const RedBatch* __rest
     }
     for (; sp < ns; ++sp) acc += pc[(long long)sp * sstride];
   }
-  const int row = ti * bt + e / bt, col0 = tj * bt + (e & (bt - 1));
+  const int row = ti * bt + br * 32 + lr, col0 = tj * bt + bc * 32 + c4;
   AS1 float* w = gptr(J.ws) + (long long)row * J.ldw + col0;
   const bool add = J.accum != 0;
 #pragma unroll
   for (int u = 0; u < 4; ++u)
     if (row <= col0 + u && col0 + u < J.ncols) w[u] = add ? w[u] + acc[u] : acc[u];
+  if (!J.mirror) return;
+  // mirror: ws[col][row] = ws[row][col] for row < col (the same values as
+  // the upper store: the lower triangle is bitwise its mirror), through an
+  // LDS transpose of the block; consecutive lanes store consecutive
+  // elements of a mirrored row (128-byte runs)
+  __shared__ float tr[32][33];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) tr[lr][c4 + u] = acc[u];
+  __syncthreads();
+  const int r0 = ti * bt + br * 32, q0 = tj * bt + bc * 32;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int idx = k * 256 + threadIdx.x;
+    const int mr = idx >> 5, mc = idx & 31;               // mirrored row / column in the block
+    const int grow = q0 + mr, gcol = r0 + mc;
+    if (gcol < grow && grow < J.ncols) {
+      AS1 float* m = gptr(J.ws) + (long long)grow * J.ldw + gcol;
+      const float v = tr[mc][mr];
+      *m = add ? *m + v : v;
+    }
+  }
 }
 
 // LANE_COLS = true when channels are the unit-stride dim (NHWC / Linear):
@@ -667,7 +692,8 @@ __global__ __launch_bounds__(2 * TW) void syrk_vec_grouped_kernel(const SyrkBatc
 // (factor, row i).
 struct EmaJob {
   void* state; const float* ws;
-  int n, ldw, kcols, C, kk, sdtype, row_begin, pad;
+  int n, ldw, kcols, C, kk, sdtype, row_begin;
+  int full;              // ws holds both triangles (tile_reduce mirror): row reads only
   float a1, a2;
   int mode, pad2;
   const float* keep;     // nullptr, or device flag: 0 leaves the factor untouched (AMP)
@@ -705,9 +731,10 @@ __device__ __forceinline__ void ema_perm_row(const EmaJob& J, int i) {
   if (J.keep != nullptr && *J.keep == 0.f) return;
   typename Tr::raw_t* state = (typename Tr::raw_t*)J.state;
   const int pi = perm_col(i, J.kcols, J.C, J.kk);
+  const float* wrow = J.ws + (long long)pi * J.ldw;
   for (int j = threadIdx.x; j < J.n; j += 256) {
     const int pj = perm_col(j, J.kcols, J.C, J.kk);
-    const float w = (pi <= pj) ? J.ws[(long long)pi * J.ldw + pj] : J.ws[(long long)pj * J.ldw + pi];
+    const float w = (J.full || pi <= pj) ? wrow[pj] : J.ws[(long long)pj * J.ldw + pi];
     const long long o = (long long)i * J.n + j;
     const float v = (J.mode == 0) ? (Tr::to_f32(state[o]) * J.a1 + w) * J.a2 : w;
     state[o] = Tr::from_f32(v);

@@ -103,18 +103,20 @@ class RedJob(ctypes.Structure):
                 ('ntiles', ctypes.c_int), ('ncontrib', ctypes.c_int),
                 ('part', ctypes.c_void_p * 8), ('splits', ctypes.c_int * 8),
                 ('block_begin', ctypes.c_int), ('accum', ctypes.c_int),
-                ('bt', ctypes.c_int), ('pad', ctypes.c_int)]
+                ('bt', ctypes.c_int), ('mirror', ctypes.c_int)]
 
 
-def _red_jobs(ws_ptr, ldw, n, contribs, tw=TILE):
+def _red_jobs(ws_ptr, ldw, n, contribs, tw=TILE, mirror=False):
     """contribs: [(part pointer, splits)] in the fixed summation order ->
     one RedJob per chunk of MAX_CONTRIB contributions: chunk 0 stores, the
-    later chunks add (launched in order by _tile_reduce: deterministic)."""
+    later chunks add (launched in order by _tile_reduce: deterministic).
+    mirror: store the strict lower triangle too (the grouped EMA's row reads)."""
     jobs = []
     for c0 in range(0, max(len(contribs), 1), MAX_CONTRIB):
         J = RedJob()
         J.ws, J.ldw, J.ncols, J.ntiles = ws_ptr, ldw, n, (n + tw - 1) // tw
         J.bt = tw
+        J.mirror = int(mirror)
         chunk = contribs[c0:c0 + MAX_CONTRIB]
         J.ncontrib = len(chunk)
         J.accum = int(c0 > 0)
@@ -275,7 +277,7 @@ class EmaJob(ctypes.Structure):
     _fields_ = [('state', ctypes.c_void_p), ('ws', ctypes.c_void_p),
                 ('n', ctypes.c_int), ('ldw', ctypes.c_int), ('kcols', ctypes.c_int),
                 ('C', ctypes.c_int), ('kk', ctypes.c_int), ('sdtype', ctypes.c_int),
-                ('row_begin', ctypes.c_int), ('pad', ctypes.c_int),
+                ('row_begin', ctypes.c_int), ('full', ctypes.c_int),
                 ('a1', ctypes.c_float), ('a2', ctypes.c_float),
                 ('mode', ctypes.c_int), ('pad2', ctypes.c_int), ('keep', ctypes.c_void_p)]
 
@@ -367,8 +369,11 @@ def update_factors_grouped(items, alpha, tag=''):
             poff += nb * tw * tw
         _lib.check(L.kfac_syrk_grouped(raw, len(probs), _lib.DTYPE_CODE[dtype], stream),
                    'kfac_syrk_grouped')
+    # both triangles: the EMA below reads whole rows of the workspace (its
+    # column walks over the upper triangle were most of its time)
     _tile_reduce([_red_jobs(arena.data_ptr() + 4 * ws_of[k][0], ws_of[k][1], ws_of[k][1],
-                            contribs[k], _tile_width(ws_of[k][1])) for k in grouped], stream)
+                            contribs[k], _tile_width(ws_of[k][1]), mirror=True)
+                  for k in grouped], stream)
     jobs = (EmaJob * len(grouped))()
     a1, a2 = alpha / (1.0 - alpha), 1.0 - alpha
     for j, k in enumerate(grouped):
@@ -386,6 +391,7 @@ def update_factors_grouped(items, alpha, tag=''):
         J.n, J.ldw, J.kcols, J.C, J.kk = n, n, C * kk, C, kk
         J.sdtype = _lib.DTYPE_CODE[state.dtype]
         J.a1, J.a2, J.mode = a1, a2, 0
+        J.full = 1
         J.keep = None if keep is None else keep.data_ptr()
     _lib.check(L.kfac_ema_grouped(jobs, len(grouped), stream), 'kfac_ema_grouped')
     return out

@@ -441,7 +441,10 @@ class FusedPreconditioner(object):
             table = self._split_tables.get(raw)
             if table is None:
                 if len(self._split_tables) >= 8:
-                    self._retired_tables.extend(self._split_tables.values())
+                    # split copies run only in eager inverse steps, never in a
+                    # captured graph, and every table was record_stream'ed at
+                    # its launch: dropping them is stream-safe (no retired list
+                    # growing over a long run: ADVICE r5)
                     self._split_tables.clear()
                 table = self._split_tables[raw] = _upload((SplitRec * len(lst))(*lst),
                                                           self.device)
