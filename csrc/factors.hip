@@ -688,6 +688,84 @@ __global__ __launch_bounds__(2 * TW) void syrk_vec_grouped_kernel(const SyrkBatc
   syrk_vec_tile<DT, VB, TW>(P.p, local % tiles, local / tiles, smem);
 }
 
+// ---------------------------------------------------------------------------
+// fp32 inputs with few channels (ResNet's conv1: C = 3) onto the channels-
+// contiguous MFMA path: x * s is split into fp16 hi / lo planes, channels
+// [hi_0 .. hi_{C-1}, lo_0 .. lo_{C-1}, 0 ..] of an 8-channel NHWC tensor
+// (22 significand bits; s = 2^k puts max |x| s in [2^13, 2^14)), and the
+// factor is the sum of the SYRK's four plane-pair blocks scaled by 1 / s^2
+// (a device factor: the SYRK store's dscale).  The generic fp32 SYRK this
+// replaces ran conv1's A factor (401408 x 147) at 0.51 ms on the f32 MFMA.
+constexpr int SPLIT_BLOCKS = 512;
+
+__device__ __forceinline__ float block_max256(float m) {
+  __shared__ float red[4];
+  for (int d = 32; d > 0; d >>= 1) m = fmaxf(m, __shfl_xor(m, d, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  return m;
+}
+
+// per-block max |x| -> part[blockIdx.x] (fixed grid, no atomics)
+__global__ __launch_bounds__(256) void split_absmax_kernel(const float* __restrict__ x, int C,
+                                                           int H, int W, long long sb,
+                                                           long long sc, long long sh,
+                                                           long long sw, long long total,
+                                                           float* __restrict__ part) {
+  float m = 0.f;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    long long t = i / C;
+    const int w = (int)(t % W);
+    t /= W;
+    const int h = (int)(t % H);
+    const long long b = t / H;
+    m = fmaxf(m, fabsf(x[b * sb + c * sc + h * sh + w * sw]));
+  }
+  m = block_max256(m);
+  if (threadIdx.x == 0) part[blockIdx.x] = m;
+}
+
+__global__ __launch_bounds__(256) void split_f16_kernel(const float* __restrict__ x, int C, int H,
+                                                        int W, long long sb, long long sc,
+                                                        long long sh, long long sw, long long npix,
+                                                        const float* __restrict__ part,
+                                                        uint4* __restrict__ out,
+                                                        float* __restrict__ dscale) {
+  float m = 0.f;
+  for (int i = threadIdx.x; i < SPLIT_BLOCKS; i += 256) m = fmaxf(m, part[i]);
+  m = block_max256(m);
+  int e = 0;
+  (void)frexpf(m, &e);
+  int k = (m > 0.f && m <= 3.0e38f) ? 14 - e : 0;
+  k = k < -60 ? -60 : (k > 60 ? 60 : k);
+  const float s = ldexpf(1.f, k);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *dscale = ldexpf(1.f, -2 * k);
+  for (long long p = blockIdx.x * 256LL + threadIdx.x; p < npix; p += (long long)gridDim.x * 256) {
+    const int w = (int)(p % W);
+    long long t = p / W;
+    const int h = (int)(t % H);
+    const long long b = t / H;
+    const float* px = x + b * sb + h * sh + w * sw;
+    unsigned short v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int c = 0; c < C; ++c) {
+      const float y = px[c * sc] * s;
+      const _Float16 hi = (_Float16)y;
+      const _Float16 lo = (_Float16)(y - (float)hi);
+      v[c] = __builtin_bit_cast(unsigned short, hi);
+      v[C + c] = __builtin_bit_cast(unsigned short, lo);
+    }
+    uint4 o;
+    o.x = v[0] | ((unsigned)v[1] << 16);
+    o.y = v[2] | ((unsigned)v[3] << 16);
+    o.z = v[4] | ((unsigned)v[5] << 16);
+    o.w = v[6] | ((unsigned)v[7] << 16);
+    out[p] = o;
+  }
+}
+
 // Grouped EMA (with the internal->reference permutation): one block row per
 // (factor, row i).
 struct EmaJob {
@@ -695,15 +773,23 @@ struct EmaJob {
   int n, ldw, kcols, C, kk, sdtype, row_begin;
   int full;              // ws holds both triangles (tile_reduce mirror): row reads only
   float a1, a2;
-  int mode, pad2;
+  int mode;
+  int cint;              // channels of the internal order (C, or 8 for split planes)
+  int lo;                // 0, or the channel offset of the low plane (kfac_split_f16):
+                         // the factor is the sum of the four plane-pair blocks
+  int pad3;
   const float* keep;     // nullptr, or device flag: 0 leaves the factor untouched (AMP)
 };
 
-// Reference column order (c, i, j) -> internal order (i, j, c) of syrk_vec.
-__device__ __forceinline__ int perm_col(int x, int kcols, int C, int kk) {
-  if (x >= kcols || kk == 1) return x;
+// Reference column order (c, i, j) -> internal order (i, j, c) of syrk_vec
+// with `cint` channels per tap.
+__device__ __forceinline__ int perm_col(int x, int kcols, int C, int kk, int cint) {
+  if (x >= kcols || (kk == 1 && cint == C)) return x;
   const int c = x / kk, r = x - c * kk;
-  return r * C + c;
+  return r * cint + c;
+}
+__device__ __forceinline__ int perm_col(int x, int kcols, int C, int kk) {
+  return perm_col(x, kcols, C, kk, C);
 }
 
 // EMA with the internal->reference column permutation (see syrk_vec).
@@ -730,18 +816,24 @@ __device__ __forceinline__ void ema_perm_row(const EmaJob& J, int i) {
   typedef DTypeTraits<SDT> Tr;
   if (J.keep != nullptr && *J.keep == 0.f) return;
   typename Tr::raw_t* state = (typename Tr::raw_t*)J.state;
-  const int pi = perm_col(i, J.kcols, J.C, J.kk);
+  const int pi = perm_col(i, J.kcols, J.C, J.kk, J.cint);
   const float* wrow = J.ws + (long long)pi * J.ldw;
+  const float* wlo = wrow + (long long)J.lo * J.ldw;
   for (int j = threadIdx.x; j < J.n; j += 256) {
-    const int pj = perm_col(j, J.kcols, J.C, J.kk);
-    const float w = (J.full || pi <= pj) ? wrow[pj] : J.ws[(long long)pj * J.ldw + pi];
+    const int pj = perm_col(j, J.kcols, J.C, J.kk, J.cint);
+    float w;
+    if (J.lo)      // (hi + lo)^T (hi + lo): the four plane-pair blocks (full ws),
+                   // added in an order the transpose reproduces bitwise
+      w = (wrow[pj] + wlo[pj + J.lo]) + (wrow[pj + J.lo] + wlo[pj]);
+    else
+      w = (J.full || pi <= pj) ? wrow[pj] : J.ws[(long long)pj * J.ldw + pi];
     const long long o = (long long)i * J.n + j;
     const float v = (J.mode == 0) ? (Tr::to_f32(state[o]) * J.a1 + w) * J.a2 : w;
     state[o] = Tr::from_f32(v);
   }
 }
 
-constexpr int MAX_EMA_JOBS = 56;
+constexpr int MAX_EMA_JOBS = 50;
 struct EmaBatch {
   int count, pad[3];
   EmaJob job[MAX_EMA_JOBS];
@@ -1078,6 +1170,23 @@ KFAC_API int kfac_syrk_grouped(const void* host_table, int count, int dtype, hip
   }
   return 0;
 }
+
+// x: (B, C, H, W) fp32 with any strides, C <= 4; out: B*H*W x 8 fp16 (NHWC,
+// 16-byte aligned); part: SPLIT_BLOCKS floats of scratch; dscale: 1 float.
+KFAC_API int kfac_split_f16(const float* x, int B, int C, int H, int W, long long sb,
+                            long long sc, long long sh, long long sw, void* out, float* part,
+                            float* dscale, hipStream_t stream) {
+  if (C < 1 || C > 4 || B < 1 || H < 1 || W < 1 || ((uintptr_t)out & 15)) return -2;
+  const long long npix = (long long)B * H * W;
+  hipLaunchKernelGGL(split_absmax_kernel, dim3(SPLIT_BLOCKS), dim3(256), 0, stream, x, C, H, W,
+                     sb, sc, sh, sw, npix * C, part);
+  long long nb = (npix + 255) / 256;
+  if (nb > 4096) nb = 4096;
+  hipLaunchKernelGGL(split_f16_kernel, dim3((unsigned)nb), dim3(256), 0, stream, x, C, H, W, sb,
+                     sc, sh, sw, npix, part, (uint4*)out, dscale);
+  return (int)hipGetLastError();
+}
+KFAC_API int kfac_split_blocks() { return SPLIT_BLOCKS; }
 
 KFAC_API int kfac_ema_grouped(const void* host_table, int count, hipStream_t stream) {
   const EmaJob* t = (const EmaJob*)host_table;

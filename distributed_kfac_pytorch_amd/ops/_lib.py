@@ -114,6 +114,9 @@ _SIGS = {
                                c_int, c_int, c_f, c_vp, c_int, c_ll, c_int],
     'kfac_syrk_grouped': [c_vp, c_int, c_int, c_vp],
     'kfac_ema_grouped': [c_vp, c_int, c_vp],
+    'kfac_split_f16': [c_vp, c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_ll, c_vp, c_vp,
+                       c_vp, c_vp],
+    'kfac_split_blocks': [],
     'kfac_factor_ema_perm': [c_int, c_vp, c_vp, c_int, c_int, c_f, c_int, c_int, c_int, c_int,
                              c_vp, c_vp],
     'kfac_triu_pack': [c_int, c_vp, c_vp, c_int, c_vp],

@@ -76,6 +76,41 @@ def _vec_eligible(s):
             (W == 1 or sw % 8 == 0) and x.data_ptr() % 16 == 0)
 
 
+# fp32 inputs with at most 4 channels (ResNet's conv1 images) take the
+# channels-contiguous grouped path as fp16 hi / lo planes (kfac_split_f16:
+# 22 significand bits, the factor is the four plane-pair blocks' sum):
+# KFAC_FACTOR_SPLIT=0 keeps them on the generic fp32 SYRK
+SPLIT_F32 = os.environ.get('KFAC_FACTOR_SPLIT', '1') != '0'
+split_launches = 0
+
+
+def _split_eligible(sources):
+    if not SPLIT_F32 or len(sources) != 1:
+        return False
+    s = sources[0]
+    x = s.x
+    return (x.is_cuda and x.dtype == torch.float32 and 1 <= x.shape[1] <= 4 and not s.has_bias
+            and s.dscale is None and x.dim() == 4)
+
+
+def _split_source(s):
+    """The fp16 hi / lo plane image of an fp32 source (8 channels, NHWC) as
+    a channels-contiguous source whose device dscale is 1 / s^2."""
+    x = s.x
+    B, C, H, W = x.shape
+    dev = x.device
+    out = torch.empty(B, H, W, 8, dtype=torch.float16, device=dev)
+    part = torch.empty(int(_lib.lib().kfac_split_blocks()), dtype=torch.float32, device=dev)
+    dscale = torch.empty(1, dtype=torch.float32, device=dev)
+    sb, sc, sh, sw = x.stride()
+    global split_launches
+    split_launches += 1
+    _lib.check(_lib.lib().kfac_split_f16(_lib.ptr(x), B, C, H, W, sb, sc, sh, sw, _lib.ptr(out),
+                                         _lib.ptr(part), _lib.ptr(dscale), _lib.stream(dev)),
+               'kfac_split_f16')
+    return FactorSource(out.permute(0, 3, 1, 2), s.geom, False, s.scale, dscale=dscale), C
+
+
 TILE = 128    # csrc/factors.hip output tile
 # grouped SYRK: factors with at least KFAC_SYRK_WIDE_MIN columns use 256-wide
 # output tiles (8 waves): each tile streams its two column panels for 4x the
@@ -279,7 +314,8 @@ class EmaJob(ctypes.Structure):
                 ('C', ctypes.c_int), ('kk', ctypes.c_int), ('sdtype', ctypes.c_int),
                 ('row_begin', ctypes.c_int), ('full', ctypes.c_int),
                 ('a1', ctypes.c_float), ('a2', ctypes.c_float),
-                ('mode', ctypes.c_int), ('pad2', ctypes.c_int), ('keep', ctypes.c_void_p)]
+                ('mode', ctypes.c_int), ('cint', ctypes.c_int), ('lo', ctypes.c_int),
+                ('pad3', ctypes.c_int), ('keep', ctypes.c_void_p)]
 
 
 SPLIT_ROWS = 2048   # patch rows per block of the grouped SYRK
@@ -306,9 +342,14 @@ def update_factors_grouped(items, alpha, tag=''):
     out = [None] * len(items)
     grouped, rest = [], []
     items = [tuple(it) + (None,) * (4 - len(it)) for it in items]
-    for k, (state, sources, out_dtype, _) in enumerate(items):
+    split = {}        # k -> reference channel count of a split (fp16 hi / lo) factor
+    for k, (state, sources, out_dtype, keep) in enumerate(items):
         if alpha != 1 and all(_vec_eligible(s) for s in sources) and \
                 len({(s.x.dtype, s.x.shape[1], s.geom.kh * s.geom.kw) for s in sources}) == 1:
+            grouped.append(k)
+        elif alpha != 1 and _split_eligible(sources):
+            src, split[k] = _split_source(sources[0])
+            items[k] = (state, [src], out_dtype, keep)
             grouped.append(k)
         else:
             rest.append(k)
@@ -378,17 +419,22 @@ def update_factors_grouped(items, alpha, tag=''):
     a1, a2 = alpha / (1.0 - alpha), 1.0 - alpha
     for j, k in enumerate(grouped):
         state, sources, out_dtype, keep = items[k]
-        n = sizes[j]
+        n = ldw = sizes[j]
+        s0 = sources[0]
+        kk = s0.geom.kh * s0.geom.kw
+        C = cint = s0.x.shape[1]
+        lo = 0
+        if k in split:      # internal 8-channel planes -> the reference C x kh x kw factor
+            C = lo = split[k]
+            n = C * kk
         if state is None:
             state = torch.eye(n, dtype=out_dtype, device=dev)
         out[k] = state
-        s0 = sources[0]
-        kk = s0.geom.kh * s0.geom.kw
-        C = s0.x.shape[1]
         woff, _ = ws_of[k]
         J = jobs[j]
         J.state, J.ws = state.data_ptr(), arena.data_ptr() + 4 * woff
-        J.n, J.ldw, J.kcols, J.C, J.kk = n, n, C * kk, C, kk
+        J.n, J.ldw, J.kcols, J.C, J.kk = n, ldw, C * kk, C, kk
+        J.cint, J.lo = cint, lo
         J.sdtype = _lib.DTYPE_CODE[state.dtype]
         J.a1, J.a2, J.mode = a1, a2, 0
         J.full = 1

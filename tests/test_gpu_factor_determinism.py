@@ -53,6 +53,35 @@ def test_factor_update_bitwise_reproducible(dtype, cl):
     assert err < (2e-3 if dtype == torch.bfloat16 else 1e-5), err
 
 
+@pytest.mark.parametrize('cl', [True, False])
+def test_fp32_few_channel_split_factor(cl):
+    """ResNet's conv1 input (fp32, C = 3, 7x7 / 2): the grouped path takes it
+    as fp16 hi / lo planes (kfac_split_f16) -- bitwise reproducible, within
+    fp32-level error of the fp64 covariance and of the generic fp32 SYRK."""
+    g = torch.Generator(device='cuda').manual_seed(7)
+    x = torch.randn(8, 3, 64, 64, device='cuda', generator=g) * 2.5 + 0.3
+    if cl:
+        x = x.contiguous(memory_format=torch.channels_last)
+    geom = _Geom(7, 2, 3)
+    n = 3 * 49
+    src = factors.FactorSource(x, geom, False, 1.0)
+    src.scale = 1.0 / src.rows[0]
+    before = factors.split_launches
+    outs = []
+    for _ in range(3):
+        st = torch.zeros(n, n, device='cuda')
+        outs.append(factors.update_factors_grouped([(st, [src], torch.float32)], 0.0)[0].clone())
+    assert factors.split_launches == before + 3
+    generic = factors.update_factor(torch.zeros(n, n, device='cuda'), [src], 0.0, torch.float32)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert torch.equal(outs[0], outs[0].t())
+    ref = _ref_cov(x, 7, 2, 3, False)
+    err = ((outs[0].double() - ref).norm() / ref.norm()).item()
+    gerr = ((generic.double() - ref).norm() / ref.norm()).item()
+    assert err < 2e-6 and err < 20 * max(gerr, 1e-8), (err, gerr)
+
+
 def test_multi_source_factor_reproducible():
     """Several sources of one factor (gradient accumulation): the partials of
     every (source, split) are summed in a fixed order."""
