@@ -70,6 +70,12 @@ const int g_dc_prec = [] {
   if (e && !strcmp(e, "bf16x6")) return (int)PREC_BF16X6F;
   return (int)PREC_F16X3F;
 }();
+// the wave-parallel deflation scan of dc_prep (KFAC_DC_SERIAL_SCAN=1: every
+// chunk through the sequential path -- the reference for the bitwise test)
+int g_dc_fast_scan = [] {
+  const char* e = getenv("KFAC_DC_SERIAL_SCAN");
+  return (e && e[0] == '1') ? 0 : 1;
+}();
 constexpr int TYP_SHIFT = 28;
 constexpr int SRC_MASK = (1 << TYP_SHIFT) - 1;
 
@@ -259,7 +265,8 @@ __device__ inline int run_count(P a, int s, int e, double v, bool le) {
 
 __global__ __launch_bounds__(256) void dc_prep_kernel(const DcMat* __restrict__ mats,
                                                       const DcNode* __restrict__ nodes,
-                                                      PGemm* __restrict__ table, int use_lds) {
+                                                      PGemm* __restrict__ table, int use_lds,
+                                                      int use_fast) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
   __shared__ double red[4];
   __shared__ int sh_k, sh_nrot, sh_cnt[3][256];
@@ -324,76 +331,131 @@ __global__ __launch_bounds__(256) void dc_prep_kernel(const DcMat* __restrict__ 
   dmx = block_max(dmx, red);
   zmx = block_max(zmx, red);
   const double tol = 8.0 * EPS32 * fmax(dmx, rho * zmx);
-  // -- 4. sequential deflation scan (LAPACK dlaed2 order); survivors compacted
-  // in place at the front of sd2 / sz2 / ssrc2, deflated run ascending
-  if (tid == 0) {
+  // -- 4. deflation scan (LAPACK dlaed2 order); survivors compacted in place at
+  // the front of sd2 / sz2 / ssrc2, deflated run ascending.  Wave 0 takes 64
+  // elements at a time: z-deflation is per element, and with no Givens
+  // deflation in the chunk (the rotation test of every surviving pole
+  // against the one before it comes out false -- the usual case) the chunk's
+  // effect is a compaction: survivors flushed in order, z-deflated values
+  // appended (the run stays ascending: sd2 is sorted).  A chunk with a
+  // rotation, or whose first appended value sorts below the run's end, runs
+  // element by element on lane 0 (the exact sequential scan).  The serial
+  // scan over up to 4608 elements was ~40 % of the divide and conquer.
+  if (tid < 64) {
+    const int lane = tid;
     int q = 0, t = 0, r = 0;
     bool have = false;
     double pd = 0.0, pz = 0.0;
     int ps = 0;
     AS1 int* rp = M.rp + 2LL * lo;
     AS1 float* rcs = M.rcs + 2LL * lo;
-    // the next element's values are loaded before this one's stores (which
-    // only write survivors at q <= p): the scan is one serial lane, and a
-    // load issued behind the stores waited out the whole LDS round trip
-    double dn = sd2[0], zn = sz2[0];
-    int sn = ssrc2[0];
-    for (int p = 0; p < m; ++p) {
-      const double dp = dn, zp = zn;
-      const int sp = sn;
-      if (p + 1 < m) {
-        dn = sd2[p + 1]; zn = sz2[p + 1]; sn = ssrc2[p + 1];
+    const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    for (int base = 0; base < m; base += 64) {
+      const int p = base + lane;
+      const bool in = p < m;
+      const double dp = in ? (double)sd2[p] : 0.0, zp = in ? (double)sz2[p] : 0.0;
+      const int sp = in ? (int)ssrc2[p] : 0;
+      const bool zdef = in && rho * fabs(zp) <= tol;
+      const bool cand = in && !zdef;
+      const unsigned long long cmask = __ballot(cand), dmask = __ballot(zdef);
+      const unsigned long long prevc = cmask & below;
+      const int pl = prevc ? 63 - __clzll(prevc) : 0;
+      const double ppd = __shfl(dp, pl, 64), ppz = __shfl(zp, pl, 64);
+      bool rot = false;
+      if (cand && (prevc || have)) {
+        const double qd = prevc ? ppd : pd, qz = prevc ? ppz : pz;
+        rot = fabs((dp - qd) * zp * qz) <= tol * fma(zp, zp, qz * qz);
       }
-      double dv = 0.0;
-      int dsrc_v = -1;
-      if (rho * fabs(zp) <= tol) {
-        dv = dp; dsrc_v = sp & SRC_MASK;
-      } else if (!have) {
-        have = true; pd = dp; pz = zp; ps = sp;
+      bool fast = use_fast && __ballot(rot) == 0ull;
+      if (fast && dmask && t > 0) {
+        const double fdv = __shfl(dp, __ffsll((long long)dmask) - 1, 64);
+        fast = !((double)sdef[t - 1] > fdv);
+      }
+      if (fast) {
+        const int kc = __popcll(cmask);
+        if (kc > 0) {
+          const int f0 = have ? 1 : 0;
+          if (lane == 0 && have) { sd2[q] = pd; sz2[q] = pz; ssrc2[q] = ps; }
+          const int rank = __popcll(prevc);
+          if (cand && rank < kc - 1) {
+            sd2[q + f0 + rank] = dp; sz2[q + f0 + rank] = zp; ssrc2[q + f0 + rank] = sp;
+          }
+          const int last = 63 - __clzll(cmask);
+          pd = __shfl(dp, last, 64); pz = __shfl(zp, last, 64); ps = __shfl(sp, last, 64);
+          q += f0 + kc - 1;
+          have = true;
+        }
+        if (zdef) {
+          const int dr = t + __popcll(dmask & below);
+          sdef[dr] = dp;
+          sdefsrc[dr] = sp & SRC_MASK;
+        }
+        t += __popcll(dmask);
         continue;
-      } else {
-        const double tt = dp - pd;
-        // |tt c s| <= tol with c = zp / tau, s = -pz / tau, tau = hypot(zp, pz),
-        // tested as |tt zp pz| <= tol (zp^2 + pz^2): the square root and the
-        // divisions only when a rotation deflates (rare)
-        if (fabs(tt * zp * pz) <= tol * fma(zp, zp, pz * pz)) {
-          const double tau = hypot(zp, pz);
-          const double c = zp / tau, s = -pz / tau;
-          rp[2 * r] = ps & SRC_MASK;
-          rp[2 * r + 1] = sp & SRC_MASK;
-          rcs[2 * r] = (float)c;
-          rcs[2 * r + 1] = (float)s;
-          ++r;
-          dv = pd * c * c + dp * s * s;
-          dsrc_v = ps & SRC_MASK;
-          const int ta = ps >> TYP_SHIFT, tb = sp >> TYP_SHIFT;
-          const int typ = (ta == tb) ? tb : 2;
-          pd = pd * s * s + dp * c * c;
-          pz = tau;
-          ps = (sp & SRC_MASK) | (typ << TYP_SHIFT);
-        } else {
-          sd2[q] = pd; sz2[q] = pz; ssrc2[q] = ps; ++q;
-          pd = dp; pz = zp; ps = sp;
-          continue;
+      }
+      // exact sequential semantics for this chunk
+      if (lane == 0) {
+        const int pend = base + 64 < m ? base + 64 : m;
+        for (int pp = base; pp < pend; ++pp) {
+          const double ed = sd2[pp], ez = sz2[pp];
+          const int es = ssrc2[pp];
+          double dv = 0.0;
+          int dsrc_v = -1;
+          if (rho * fabs(ez) <= tol) {
+            dv = ed; dsrc_v = es & SRC_MASK;
+          } else if (!have) {
+            have = true; pd = ed; pz = ez; ps = es;
+            continue;
+          } else {
+            const double tt = ed - pd;
+            // |tt c s| <= tol with c = ez / tau, s = -pz / tau, tau = hypot(ez, pz),
+            // tested as |tt ez pz| <= tol (ez^2 + pz^2): the square root and the
+            // divisions only when a rotation deflates (rare)
+            if (fabs(tt * ez * pz) <= tol * fma(ez, ez, pz * pz)) {
+              const double tau = hypot(ez, pz);
+              const double c = ez / tau, sn = -pz / tau;
+              rp[2 * r] = ps & SRC_MASK;
+              rp[2 * r + 1] = es & SRC_MASK;
+              rcs[2 * r] = (float)c;
+              rcs[2 * r + 1] = (float)sn;
+              ++r;
+              dv = pd * c * c + ed * sn * sn;
+              dsrc_v = ps & SRC_MASK;
+              const int ta = ps >> TYP_SHIFT, tb = es >> TYP_SHIFT;
+              const int typ = (ta == tb) ? tb : 2;
+              pd = pd * sn * sn + ed * c * c;
+              pz = tau;
+              ps = (es & SRC_MASK) | (typ << TYP_SHIFT);
+            } else {
+              sd2[q] = pd; sz2[q] = pz; ssrc2[q] = ps; ++q;
+              pd = ed; pz = ez; ps = es;
+              continue;
+            }
+          }
+          // insertion into the ascending deflated run
+          int j = t;
+          while (j > 0 && sdef[j - 1] > dv) {
+            sdef[j] = sdef[j - 1];
+            sdefsrc[j] = sdefsrc[j - 1];
+            --j;
+          }
+          sdef[j] = dv;
+          sdefsrc[j] = dsrc_v;
+          ++t;
         }
       }
-      // insertion into the ascending deflated run
-      int j = t;
-      while (j > 0 && sdef[j - 1] > dv) {
-        sdef[j] = sdef[j - 1];
-        sdefsrc[j] = sdefsrc[j - 1];
-        --j;
-      }
-      sdef[j] = dv;
-      sdefsrc[j] = dsrc_v;
-      ++t;
+      q = __shfl(q, 0, 64); t = __shfl(t, 0, 64); r = __shfl(r, 0, 64);
+      have = __shfl((int)have, 0, 64) != 0;
+      pd = __shfl(pd, 0, 64); pz = __shfl(pz, 0, 64); ps = __shfl(ps, 0, 64);
     }
-    if (have) { sd2[q] = pd; sz2[q] = pz; ssrc2[q] = ps; ++q; }
-    sh_k = q;
-    sh_nrot = r;
-    M.kk[lo] = q;
-    M.nrot[lo] = r;
-    M.rho[lo] = rho;
+    if (lane == 0) {
+      if (have) { sd2[q] = pd; sz2[q] = pz; ssrc2[q] = ps; ++q; }
+      sh_k = q;
+      sh_nrot = r;
+      M.kk[lo] = q;
+      M.nrot[lo] = r;
+      M.rho[lo] = rho;
+    }
   }
   __syncthreads();
   const int k = sh_k;
@@ -728,6 +790,14 @@ size_t al256(size_t b) { return (b + 255) / 256 * 256; }
 }  // namespace
 
 // workspace layout per matrix (bytes): see carve()
+// run-time switch of the deflation scan (eager launches; a captured plan keeps
+// the mode it was captured with): 1 wave-parallel, 0 sequential
+KFAC_API int kfac_dc_set_fast_scan(int on) {
+  const int prev = g_dc_fast_scan;
+  g_dc_fast_scan = on ? 1 : 0;
+  return prev;
+}
+
 KFAC_API long long kfac_dc_ws_bytes(int n) {
   const long long ldw = rup(n + PADK, 64);
   size_t b = 0;
@@ -846,7 +916,8 @@ int enqueue(const DcPlan& P, hipStream_t stream) {
     PGemm* tab = P.d_tables + L.tables_off;
     const int prep_lds = L.mmax <= LDS_M_MAX;
     hipLaunchKernelGGL(dc_prep_kernel, dim3(L.count), dim3(256),
-                       prep_lds ? (size_t)L.mmax * 32 : 0, stream, P.d_mats, nodes, tab, prep_lds);
+                       prep_lds ? (size_t)L.mmax * 32 : 0, stream, P.d_mats, nodes, tab, prep_lds,
+                       g_dc_fast_scan);
     hipLaunchKernelGGL(dc_rotate_kernel, dim3(cdiv(L.mmax, 256), L.count), dim3(256), 0, stream,
                        P.d_mats, nodes);
     const int tiles_c = cdiv(L.mmax, 64), tiles_j = cdiv(L.mmax + PADK, 64);

@@ -148,6 +148,7 @@ _SIGS = {
     'kfac_reduce_stamps': [c_vp],
     'kfac_dc_prepare': [ctypes.POINTER(DcRecord), c_int],
     'kfac_dc_ws_bytes': [c_int],
+    'kfac_dc_set_fast_scan': [c_int],
     'kfac_dc_info_offset': [c_int],
     'kfac_bn_ws_floats': [c_ll, c_int],
     'kfac_bn_forward': [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll,

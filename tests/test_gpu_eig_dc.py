@@ -54,6 +54,40 @@ def test_dc_ragged_batch(kind):
             _check(d, e, w, Z)
 
 
+@pytest.mark.parametrize('kind', ['rand', 'glued', 'graded', 'equal', 'kfac'])
+def test_dc_parallel_scan_bitwise(kind):
+    """The wave-parallel deflation scan of dc_prep (64 elements at a time, the
+    exact sequential scan for chunks with a Givens rotation) gives bitwise the
+    eigenpairs of the sequential scan -- merges in LDS (m <= 4800) and in
+    global scratch (n = 6000)."""
+    from distributed_kfac_pytorch_amd.ops import _lib
+    L = _lib.lib()
+    sizes = [65, 577, 1152, 4608, 6000]
+    if kind == 'kfac':
+        mats = []
+        for n in (577, 1152, 2304):
+            A = _kfac_factor(n, n)
+            ev = torch.linalg.eigvalsh(A).float().cpu()
+            g = torch.Generator(device='cpu').manual_seed(n)
+            e = (ev[1:] - ev[:-1]).abs().clamp_min(1e-12) * torch.rand(n - 1, generator=g)
+            mats.append((ev.contiguous(), e.float()))
+    else:
+        mats = [_tridiag(n, kind, 11 * n) for n in sizes]
+    outs = {}
+    prev = L.kfac_dc_set_fast_scan(1)
+    try:
+        for mode in (1, 0):
+            L.kfac_dc_set_fast_scan(mode)
+            outs[mode] = eigen.tridiag_eigh([d.to(DEV) for d, _ in mats],
+                                            [e.to(DEV) for _, e in mats], use_graph=False)
+    finally:
+        L.kfac_dc_set_fast_scan(prev)
+    for (d, e), (wf, Zf), (ws, Zs) in zip(mats, outs[1], outs[0]):
+        assert torch.equal(wf, ws) and torch.equal(Zf, Zs), d.shape[0]
+        if kind != 'kfac':
+            _check(d, e, wf, Zf, tol_res=4e-6, tol_orth=5e-5)
+
+
 @pytest.mark.parametrize('n', [2304, 4608])
 def test_dc_large(n):
     d, e = _tridiag(n, 'rand', n)
