@@ -1189,13 +1189,14 @@ inline int h_tri(int m) { return m * (m + 1) / 2; }
 // launches (KFAC_REDUCE_TAIL, 0 = never); capped so the tail's P partials fit
 // its unroll classes (<= 40 row blocks)
 constexpr int TAIL_MAX = 38 * TB;
+int g_tail_override = -1;    // kfac_reduce_set_tail: the next plans' threshold
 int tail_rows() {
   static const int t = [] {
     const char* e = getenv("KFAC_REDUCE_TAIL");
     const int v = e ? atoi(e) : 768;
     return std::max(0, std::min(v, TAIL_MAX));
   }();
-  return t;
+  return g_tail_override >= 0 ? std::min(g_tail_override, TAIL_MAX) : t;
 }
 
 // the panel start j0 after which matrix n runs tail launches (n: no tail)
@@ -1309,6 +1310,15 @@ std::map<std::string, RPlan> g_plans;
 
 // workspace floats per matrix (V, W and the 2-slot partial rings), zeroed by
 // the caller once (rows past n of XH / AV / P must read 0)
+// Tail threshold for plans built from now on (-1: KFAC_REDUCE_TAIL / 768); a
+// plan keeps the threshold it was built with.  Returns the previous override.
+KFAC_API int kfac_reduce_set_tail(int rows) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  const int prev = g_tail_override;
+  g_tail_override = rows;
+  return prev;
+}
+
 KFAC_API long long kfac_reduce_ws_floats(int n) { return ws_layout(n).total; }
 
 struct KfacReduceRecord {

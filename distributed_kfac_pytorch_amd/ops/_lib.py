@@ -145,6 +145,7 @@ _SIGS = {
     'kfac_reduce_batched': [ctypes.POINTER(ReduceRecord), c_int, c_int, c_vp],
     'kfac_reduce_prepare': [ctypes.POINTER(ReduceRecord), c_int],
     'kfac_reduce_ws_floats': [c_int],
+    'kfac_reduce_set_tail': [c_int],
     'kfac_reduce_stamps': [c_vp],
     'kfac_dc_prepare': [ctypes.POINTER(DcRecord), c_int],
     'kfac_dc_ws_bytes': [c_int],

@@ -208,6 +208,12 @@ def _fused_groups(mats):
 
 
 FUSED_STREAMS = int(os.environ.get('KFAC_EIG_FUSED_STREAMS', '2'))
+# tail threshold (csrc/eig_reduce.hip KFAC_REDUCE_TAIL, 768) of the groups after
+# the leading one (-1 = the same): their single-launch tail columns redo F's row
+# work over every tile, traffic that slows the leading chain beside them.
+# ResNet-50's 108 factors, same box (profiles/r6_reduce_tail_rest_sweep.log):
+# 768 103.7-103.8 ms; 256 / 384 / 512 102.2-102.7; 0 104.9; 1536 110.2; 2304 122
+TAIL_REST = int(os.environ.get('KFAC_REDUCE_TAIL_REST', '384'))
 FUSED_SPLIT = bool(int(os.environ.get('KFAC_EIG_FUSED_SPLIT', '1')))
 
 
@@ -318,7 +324,13 @@ def _fused_group(mats, clip, stream, use_graph, slot=0, finite=None):
                 dr[k] = dcr[i]
                 k += 1
         _mark(slot, 'staged', stream)
-        _lib.check(L.kfac_reduce_batched(rr, total, int(use_graph), cs), 'kfac_reduce_batched')
+        prev = L.kfac_reduce_set_tail(TAIL_REST) if slot > 0 and TAIL_REST >= 0 else None
+        try:
+            _lib.check(L.kfac_reduce_batched(rr, total, int(use_graph), cs),
+                       'kfac_reduce_batched')
+        finally:
+            if prev is not None:
+                L.kfac_reduce_set_tail(prev)
         _mark(slot, 'reduce', stream)
         _lib.check(L.kfac_dc_batched(dr, total, int(use_graph), cs), 'kfac_dc_batched')
         _mark(slot, 'dc', stream)
